@@ -23,6 +23,34 @@ at::Tensor norm_bwd_apply(const at::Tensor& x, const at::Tensor& dout, const at:
                           const at::Tensor& k1, const at::Tensor& k2, const at::Tensor& k3,
                           const c10::optional<at::Tensor>& gamma,
                           const c10::optional<at::Tensor>& beta, double slope);
+// bias_act.hip (k2)
+at::Tensor bias_act_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& bias, double slope,
+                        bool inplace);
+std::vector<at::Tensor> bias_act_bwd(const at::Tensor& out, const at::Tensor& dy, double slope);
+// partial_conv.hip (k3)
+std::vector<at::Tensor> partial_conv_renorm(const at::Tensor& raw, const at::Tensor& mask,
+                                            const c10::optional<at::Tensor>& bias, int64_t kh,
+                                            int64_t kw, int64_t sh, int64_t sw, int64_t ph,
+                                            int64_t pw, int64_t dh, int64_t dw, double winsize,
+                                            double eps);
+// multi_tensor.hip (k4 / k5)
+void mt_adam(const std::vector<at::Tensor>& params, const std::vector<at::Tensor>& grads,
+             const std::vector<at::Tensor>& exp_avgs, const std::vector<at::Tensor>& exp_avg_sqs,
+             const std::vector<at::Tensor>& shadows, double lr, double beta1, double beta2,
+             double eps, int64_t step, double weight_decay, bool adamw, double grad_scale);
+at::Tensor mt_sn_sigma(const std::vector<at::Tensor>& weights, const std::vector<at::Tensor>& us,
+                       const std::vector<at::Tensor>& vs);
+void mt_ema(const std::vector<at::Tensor>& targets, const std::vector<at::Tensor>& sources,
+            double beta, const c10::optional<at::Tensor>& sigma);
+void mt_scale(const std::vector<at::Tensor>& xs, const at::Tensor& s);
+at::Tensor mt_sqnorm(const std::vector<at::Tensor>& xs);
+// flow_warp.hip (k9 warp, k7 resample2d)
+at::Tensor flow_warp_fwd(const at::Tensor& img, const at::Tensor& flow);
+std::vector<at::Tensor> flow_warp_bwd(const at::Tensor& img, const at::Tensor& flow,
+                                      const at::Tensor& dout);
+at::Tensor resample2d_forward(const at::Tensor& in1, const at::Tensor& flow, int64_t ks);
+std::vector<at::Tensor> resample2d_backward(const at::Tensor& in1, const at::Tensor& flow,
+                                            const at::Tensor& dout, int64_t ks);
 }  // namespace iamd
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -31,4 +59,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("norm_apply", &iamd::norm_apply, "norm + SPADE modulation + activation (k1 fwd)");
   m.def("norm_bwd_reduce", &iamd::norm_bwd_reduce, "k1 backward reduction");
   m.def("norm_bwd_apply", &iamd::norm_bwd_apply, "k1 backward dx");
+  m.def("bias_act_fwd", &iamd::bias_act_fwd, "bias + activation epilogue (k2)");
+  m.def("bias_act_bwd", &iamd::bias_act_bwd, "k2 backward: dx and dbias");
+  m.def("partial_conv_renorm", &iamd::partial_conv_renorm, "partial conv mask/renorm (k3)");
+  m.def("mt_adam", &iamd::mt_adam, "multi-tensor Adam/AdamW (k4)");
+  m.def("mt_sn_sigma", &iamd::mt_sn_sigma, "multi-tensor spectral-norm sigma (k5)");
+  m.def("mt_ema", &iamd::mt_ema, "multi-tensor EMA with SN absorption (k5)");
+  m.def("mt_scale", &iamd::mt_scale, "multi-tensor scale");
+  m.def("mt_sqnorm", &iamd::mt_sqnorm, "multi-tensor squared L2 norm");
+  m.def("flow_warp_fwd", &iamd::flow_warp_fwd, "bilinear flow warp, border (k9)");
+  m.def("flow_warp_bwd", &iamd::flow_warp_bwd, "k9 backward");
+  m.def("resample2d_forward", &iamd::resample2d_forward, "FlowNet2 Resample2d (k7)");
+  m.def("resample2d_backward", &iamd::resample2d_backward, "k7 backward");
 }

@@ -1,0 +1,357 @@
+// k4 / k5: multi-tensor optimizer and model-averaging kernels.
+//
+// One launch covers every parameter tensor of a network: the host builds a
+// device-resident table {pointers, numel} plus a block map (tensor id, chunk
+// offset) once per distinct tensor list (cached by pointer signature, so the
+// steady state costs no host work beyond a hash and is hipGraph-capturable),
+// and each workgroup streams one 16-byte-vectorised chunk.
+//
+//   mt_adam     : Adam / AdamW (reference FusedAdam, utils/trainer.py:271-281)
+//                 fp32 master params, fp32 or bf16 grads, optional bf16 shadow
+//                 copy of the updated weights written in the same pass.
+//   mt_sn_sigma : σ_i = u_iᵀ W_i v_i for every spectral-normalised weight
+//                 (reference ModelAverage.sn_compute_weight, model_average.py:183-197)
+//   mt_ema      : t = β·t + (1-β)·s·scale_i  (model_average.py:87-131; scale_i = 1/σ_i
+//                 absorbs spectral norm into the averaged model)
+//   mt_scale    : x *= s (gradient clipping / unscale)
+//   mt_sqnorm   : Σ x² per list (gradient-norm for clipping)
+#include "common.h"
+
+#include <mutex>
+#include <unordered_map>
+
+namespace iamd {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kChunk = 256 * 4 * 16;  // elements per workgroup (fp32: 64 KiB per operand)
+
+struct TensorEntry {
+  void* p[5];
+  int64_t numel;
+  int64_t cols;  // numel / size(0): row length when viewed as a matrix (spectral norm)
+};
+
+struct Table {
+  at::Tensor entries;  // device: TensorEntry[T]
+  at::Tensor blocks;   // device: int2 {tensor, chunk} per workgroup
+  int nblocks;
+};
+
+std::mutex g_mu;
+std::unordered_map<uint64_t, Table> g_cache;
+
+uint64_t mix(uint64_t h, uint64_t v) {
+  h ^= v + 0x9e3779b97f4a7c15ULL + (h << 6) + (h >> 2);
+  return h;
+}
+
+// Build (or fetch from cache) the device table for up to 5 parallel tensor lists.
+Table& get_table(const std::vector<std::vector<at::Tensor>>& lists, const at::Device& dev) {
+  const size_t T = lists[0].size();
+  uint64_t h = 1469598103934665603ULL ^ (uint64_t)lists.size();
+  for (size_t i = 0; i < T; ++i) {
+    for (auto& l : lists) h = mix(h, reinterpret_cast<uint64_t>(l[i].data_ptr()));
+    h = mix(h, (uint64_t)lists[0][i].numel());
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_cache.find(h);
+  if (it != g_cache.end()) return it->second;
+  std::vector<TensorEntry> ents(T);
+  std::vector<int32_t> bm;
+  for (size_t i = 0; i < T; ++i) {
+    for (size_t k = 0; k < 5; ++k) ents[i].p[k] = k < lists.size() ? lists[k][i].data_ptr() : nullptr;
+    ents[i].numel = lists[0][i].numel();
+    ents[i].cols = lists[0][i].dim() > 0 && lists[0][i].size(0) > 0
+                       ? ents[i].numel / lists[0][i].size(0) : 1;
+    const int64_t nch = (ents[i].numel + kChunk - 1) / kChunk;
+    for (int64_t c = 0; c < nch; ++c) {
+      bm.push_back((int32_t)i);
+      bm.push_back((int32_t)c);
+    }
+  }
+  // pinned staging + async copy on the current stream: a cache miss never
+  // blocks the host (the caching host allocator keeps the staging alive).
+  auto pin = at::TensorOptions().dtype(at::kByte).pinned_memory(true);
+  auto cpu_e = at::empty({(int64_t)(T * sizeof(TensorEntry))}, pin);
+  memcpy(cpu_e.data_ptr(), ents.data(), T * sizeof(TensorEntry));
+  auto cpu_b = at::empty({(int64_t)(bm.size() * sizeof(int32_t))}, pin);
+  memcpy(cpu_b.data_ptr(), bm.data(), bm.size() * sizeof(int32_t));
+  Table t;
+  t.entries = cpu_e.to(dev, /*non_blocking=*/true);
+  t.blocks = cpu_b.to(dev, /*non_blocking=*/true).view(at::kInt);
+  t.nblocks = (int)(bm.size() / 2);
+  if (g_cache.size() > 256) g_cache.clear();
+  auto res = g_cache.emplace(h, std::move(t));
+  return res.first->second;
+}
+
+template <typename G>
+__global__ void __launch_bounds__(kThreads)
+adam_kernel(const TensorEntry* __restrict__ ents, const int* __restrict__ blocks, float lr,
+            float beta1, float beta2, float eps, float bc1, float bc2, float wd, int adamw,
+            float grad_scale) {
+  const int b = blockIdx.x;
+  const int t = blocks[2 * b], chunk = blocks[2 * b + 1];
+  const TensorEntry e = ents[t];
+  float* __restrict__ p = reinterpret_cast<float*>(e.p[0]);
+  const G* __restrict__ g = reinterpret_cast<const G*>(e.p[1]);
+  float* __restrict__ m = reinterpret_cast<float*>(e.p[2]);
+  float* __restrict__ v = reinterpret_cast<float*>(e.p[3]);
+  __hip_bfloat16* __restrict__ shadow = reinterpret_cast<__hip_bfloat16*>(e.p[4]);
+  const int64_t start = (int64_t)chunk * kChunk;
+  const int64_t end = min(e.numel, start + (int64_t)kChunk);
+  const float step_size = lr / bc1;
+  const float rbc2 = rsqrtf(bc2);
+  const bool vec_ok = (((uintptr_t)p | (uintptr_t)m | (uintptr_t)v) % 16 == 0) &&
+                      ((uintptr_t)g % (4 * sizeof(G)) == 0) && (start % 4 == 0);
+  if (vec_ok) {
+    for (int64_t i = start + threadIdx.x * 4; i + 3 < end; i += kThreads * 4) {
+      float pv[4], gv[4], mv[4], vv[4];
+      load_vec<float, 4>(p + i, pv);
+      load_vec<G, 4>(g + i, gv);
+      load_vec<float, 4>(m + i, mv);
+      load_vec<float, 4>(v + i, vv);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float gr = gv[k] * grad_scale;
+        if (!adamw && wd != 0.f) gr = fmaf(wd, pv[k], gr);
+        mv[k] = fmaf(beta1, mv[k], (1.f - beta1) * gr);
+        vv[k] = fmaf(beta2, vv[k], (1.f - beta2) * gr * gr);
+        const float denom = sqrtf(vv[k]) * rbc2 + eps;
+        if (adamw && wd != 0.f) pv[k] *= (1.f - lr * wd);
+        pv[k] -= step_size * mv[k] / denom;
+      }
+      store_vec<float, 4>(p + i, pv);
+      store_vec<float, 4>(m + i, mv);
+      store_vec<float, 4>(v + i, vv);
+      if (shadow) store_vec<__hip_bfloat16, 4>(shadow + i, pv);
+    }
+    // tail (numel not multiple of 4)
+    const int64_t tail0 = start + ((end - start) / 4) * 4;
+    for (int64_t i = tail0 + threadIdx.x; i < end; i += kThreads) {
+      float gr = to_f<G>(g[i]) * grad_scale;
+      float pv = p[i];
+      if (!adamw && wd != 0.f) gr = fmaf(wd, pv, gr);
+      float mv = fmaf(beta1, m[i], (1.f - beta1) * gr);
+      float vv = fmaf(beta2, v[i], (1.f - beta2) * gr * gr);
+      if (adamw && wd != 0.f) pv *= (1.f - lr * wd);
+      pv -= step_size * mv / (sqrtf(vv) * rbc2 + eps);
+      p[i] = pv; m[i] = mv; v[i] = vv;
+      if (shadow) shadow[i] = __float2bfloat16(pv);
+    }
+  } else {
+    for (int64_t i = start + threadIdx.x; i < end; i += kThreads) {
+      float gr = to_f<G>(g[i]) * grad_scale;
+      float pv = p[i];
+      if (!adamw && wd != 0.f) gr = fmaf(wd, pv, gr);
+      float mv = fmaf(beta1, m[i], (1.f - beta1) * gr);
+      float vv = fmaf(beta2, v[i], (1.f - beta2) * gr * gr);
+      if (adamw && wd != 0.f) pv *= (1.f - lr * wd);
+      pv -= step_size * mv / (sqrtf(vv) * rbc2 + eps);
+      p[i] = pv; m[i] = mv; v[i] = vv;
+      if (shadow) shadow[i] = __float2bfloat16(pv);
+    }
+  }
+}
+
+// σ_i = Σ_{r,c} u[r] W[r,c] v[c]  (W viewed as [rows, numel/rows]); atomic per chunk.
+// entry: p0 = W (fp32), p1 = u, p2 = v; rows carried in the sigma-rows array.
+__global__ void __launch_bounds__(kThreads)
+sn_sigma_kernel(const TensorEntry* __restrict__ ents, const int* __restrict__ blocks,
+                float* __restrict__ sigma) {
+  __shared__ float sh[kThreads / 64];
+  const int b = blockIdx.x;
+  const int t = blocks[2 * b], chunk = blocks[2 * b + 1];
+  const TensorEntry e = ents[t];
+  const float* __restrict__ W = reinterpret_cast<const float*>(e.p[0]);
+  const float* __restrict__ u = reinterpret_cast<const float*>(e.p[1]);
+  const float* __restrict__ v = reinterpret_cast<const float*>(e.p[2]);
+  const int64_t ncol = e.cols;
+  const int64_t start = (int64_t)chunk * kChunk;
+  const int64_t end = min(e.numel, start + (int64_t)kChunk);
+  float acc = 0.f;
+  for (int64_t i = start + threadIdx.x; i < end; i += kThreads) {
+    const int64_t r = i / ncol, c = i - r * ncol;
+    acc = fmaf(u[r] * W[i], v[c], acc);
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int k = 0; k < kThreads / 64; ++k) s += sh[k];
+    atomicAdd(sigma + t, s);
+  }
+}
+
+// t = beta*t + (1-beta)*s*scale[t_idx]; p0 = target, p1 = source (same dtype: fp32)
+template <typename T>
+__global__ void __launch_bounds__(kThreads)
+ema_kernel(const TensorEntry* __restrict__ ents, const int* __restrict__ blocks, float beta,
+           const float* __restrict__ inv_scale) {
+  const int b = blockIdx.x;
+  const int t = blocks[2 * b], chunk = blocks[2 * b + 1];
+  const TensorEntry e = ents[t];
+  T* __restrict__ dst = reinterpret_cast<T*>(e.p[0]);
+  const T* __restrict__ src = reinterpret_cast<const T*>(e.p[1]);
+  const float sc = inv_scale ? 1.f / inv_scale[t] : 1.f;
+  const float a = 1.f - beta;
+  const int64_t start = (int64_t)chunk * kChunk;
+  const int64_t end = min(e.numel, start + (int64_t)kChunk);
+  for (int64_t i = start + threadIdx.x; i < end; i += kThreads)
+    dst[i] = from_f<T>(fmaf(beta, to_f<T>(dst[i]), a * sc * to_f<T>(src[i])));
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kThreads)
+scale_kernel(const TensorEntry* __restrict__ ents, const int* __restrict__ blocks,
+             const float* __restrict__ s) {
+  const int b = blockIdx.x;
+  const int t = blocks[2 * b], chunk = blocks[2 * b + 1];
+  const TensorEntry e = ents[t];
+  T* __restrict__ x = reinterpret_cast<T*>(e.p[0]);
+  const float f = *s;
+  const int64_t start = (int64_t)chunk * kChunk;
+  const int64_t end = min(e.numel, start + (int64_t)kChunk);
+  for (int64_t i = start + threadIdx.x; i < end; i += kThreads) x[i] = from_f<T>(to_f<T>(x[i]) * f);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kThreads)
+sqnorm_kernel(const TensorEntry* __restrict__ ents, const int* __restrict__ blocks,
+              float* __restrict__ out) {
+  __shared__ float sh[kThreads / 64];
+  const int b = blockIdx.x;
+  const int t = blocks[2 * b], chunk = blocks[2 * b + 1];
+  const TensorEntry e = ents[t];
+  const T* __restrict__ x = reinterpret_cast<const T*>(e.p[0]);
+  const int64_t start = (int64_t)chunk * kChunk;
+  const int64_t end = min(e.numel, start + (int64_t)kChunk);
+  float acc = 0.f;
+  for (int64_t i = start + threadIdx.x; i < end; i += kThreads) {
+    const float v = to_f<T>(x[i]);
+    acc = fmaf(v, v, acc);
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int k = 0; k < kThreads / 64; ++k) s += sh[k];
+    atomicAdd(out, s);
+  }
+}
+
+void check_same_dtype(const std::vector<at::Tensor>& l, at::ScalarType st, const char* what) {
+  for (auto& t : l) {
+    IAMD_CHECK(t.scalar_type() == st, what, ": dtype mismatch");
+    IAMD_CHECK(t.is_contiguous(), what, ": tensors must be contiguous");
+  }
+}
+
+}  // namespace
+
+void mt_adam(const std::vector<at::Tensor>& params, const std::vector<at::Tensor>& grads,
+             const std::vector<at::Tensor>& exp_avgs, const std::vector<at::Tensor>& exp_avg_sqs,
+             const std::vector<at::Tensor>& shadows, double lr, double beta1, double beta2,
+             double eps, int64_t step, double weight_decay, bool adamw, double grad_scale) {
+  if (params.empty()) return;
+  IAMD_CHECK(params.size() == grads.size() && params.size() == exp_avgs.size() &&
+                 params.size() == exp_avg_sqs.size(),
+             "mt_adam: list sizes differ");
+  check_same_dtype(params, at::kFloat, "mt_adam params");
+  check_same_dtype(exp_avgs, at::kFloat, "mt_adam exp_avg");
+  check_same_dtype(exp_avg_sqs, at::kFloat, "mt_adam exp_avg_sq");
+  const auto gdt = grads[0].scalar_type();
+  check_same_dtype(grads, gdt, "mt_adam grads");
+  std::vector<std::vector<at::Tensor>> lists{params, grads, exp_avgs, exp_avg_sqs};
+  if (!shadows.empty()) {
+    IAMD_CHECK(shadows.size() == params.size(), "mt_adam: shadow list size");
+    check_same_dtype(shadows, at::kBFloat16, "mt_adam shadow");
+    lists.push_back(shadows);
+  }
+  Table& tb = get_table(lists, params[0].device());
+  const float bc1 = 1.f - (float)std::pow(beta1, (double)step);
+  const float bc2 = 1.f - (float)std::pow(beta2, (double)step);
+  auto ents = reinterpret_cast<const TensorEntry*>(tb.entries.data_ptr());
+  auto blks = tb.blocks.data_ptr<int>();
+  if (gdt == at::kFloat)
+    hipLaunchKernelGGL((adam_kernel<float>), dim3(tb.nblocks), dim3(kThreads), 0, stream(), ents,
+                       blks, (float)lr, (float)beta1, (float)beta2, (float)eps, bc1, bc2,
+                       (float)weight_decay, adamw ? 1 : 0, (float)grad_scale);
+  else if (gdt == at::kBFloat16)
+    hipLaunchKernelGGL((adam_kernel<__hip_bfloat16>), dim3(tb.nblocks), dim3(kThreads), 0,
+                       stream(), ents, blks, (float)lr, (float)beta1, (float)beta2, (float)eps,
+                       bc1, bc2, (float)weight_decay, adamw ? 1 : 0, (float)grad_scale);
+  else
+    IAMD_CHECK(false, "mt_adam: grads must be fp32 or bf16");
+  IAMD_LAUNCH_CHECK();
+}
+
+at::Tensor mt_sn_sigma(const std::vector<at::Tensor>& weights, const std::vector<at::Tensor>& us,
+                       const std::vector<at::Tensor>& vs) {
+  IAMD_CHECK(!weights.empty(), "mt_sn_sigma: empty list");
+  check_same_dtype(weights, at::kFloat, "mt_sn_sigma W");
+  check_same_dtype(us, at::kFloat, "mt_sn_sigma u");
+  check_same_dtype(vs, at::kFloat, "mt_sn_sigma v");
+  Table& tb = get_table({weights, us, vs}, weights[0].device());
+  auto sigma = at::zeros({(int64_t)weights.size()}, weights[0].options());
+  hipLaunchKernelGGL(sn_sigma_kernel, dim3(tb.nblocks), dim3(kThreads), 0, stream(),
+                     reinterpret_cast<const TensorEntry*>(tb.entries.data_ptr()),
+                     tb.blocks.data_ptr<int>(), sigma.data_ptr<float>());
+  IAMD_LAUNCH_CHECK();
+  return sigma;
+}
+
+void mt_ema(const std::vector<at::Tensor>& targets, const std::vector<at::Tensor>& sources,
+            double beta, const c10::optional<at::Tensor>& sigma) {
+  if (targets.empty()) return;
+  const auto dt = targets[0].scalar_type();
+  check_same_dtype(targets, dt, "mt_ema targets");
+  check_same_dtype(sources, dt, "mt_ema sources");
+  Table& tb = get_table({targets, sources}, targets[0].device());
+  const float* sp = nullptr;
+  if (sigma.has_value() && sigma->defined()) {
+    IAMD_CHECK(sigma->numel() == (int64_t)targets.size() && sigma->scalar_type() == at::kFloat,
+               "mt_ema: sigma must be fp32 [T]");
+    sp = sigma->data_ptr<float>();
+  }
+  IAMD_DISPATCH_FLOAT_TYPES(dt, "mt_ema", [&] {
+    hipLaunchKernelGGL((ema_kernel<scalar_t>), dim3(tb.nblocks), dim3(kThreads), 0, stream(),
+                       reinterpret_cast<const TensorEntry*>(tb.entries.data_ptr()),
+                       tb.blocks.data_ptr<int>(), (float)beta, sp);
+  });
+  IAMD_LAUNCH_CHECK();
+}
+
+void mt_scale(const std::vector<at::Tensor>& xs, const at::Tensor& s) {
+  if (xs.empty()) return;
+  const auto dt = xs[0].scalar_type();
+  check_same_dtype(xs, dt, "mt_scale");
+  Table& tb = get_table({xs}, xs[0].device());
+  auto sf = s.to(at::kFloat).contiguous();
+  IAMD_DISPATCH_FLOAT_TYPES(dt, "mt_scale", [&] {
+    hipLaunchKernelGGL((scale_kernel<scalar_t>), dim3(tb.nblocks), dim3(kThreads), 0, stream(),
+                       reinterpret_cast<const TensorEntry*>(tb.entries.data_ptr()),
+                       tb.blocks.data_ptr<int>(), sf.data_ptr<float>());
+  });
+  IAMD_LAUNCH_CHECK();
+}
+
+at::Tensor mt_sqnorm(const std::vector<at::Tensor>& xs) {
+  IAMD_CHECK(!xs.empty(), "mt_sqnorm: empty");
+  const auto dt = xs[0].scalar_type();
+  check_same_dtype(xs, dt, "mt_sqnorm");
+  Table& tb = get_table({xs}, xs[0].device());
+  auto out = at::zeros({1}, xs[0].options().dtype(at::kFloat));
+  IAMD_DISPATCH_FLOAT_TYPES(dt, "mt_sqnorm", [&] {
+    hipLaunchKernelGGL((sqnorm_kernel<scalar_t>), dim3(tb.nblocks), dim3(kThreads), 0, stream(),
+                       reinterpret_cast<const TensorEntry*>(tb.entries.data_ptr()),
+                       tb.blocks.data_ptr<int>(), out.data_ptr<float>());
+  });
+  IAMD_LAUNCH_CHECK();
+  return out;
+}
+
+}  // namespace iamd

@@ -242,15 +242,20 @@ apply_fwd(const T* __restrict__ x, T* __restrict__ out, int N, int C, int HW,
 // backward reduce: writes dgamma / dbeta, accumulates S1 = Σ g, S2 = Σ g·x̂
 // per (n, pixel-chunk, c) where g = d(norm-affine output).
 // ------------------------------------------------------------------------
-template <typename T, bool CL, int VEC, bool MOD>
+template <typename T, bool CL, int VEC, bool MOD, bool BCAST>
 __global__ void __launch_bounds__(kThreads)
 bwd_reduce(const T* __restrict__ x, const T* __restrict__ dout, int N, int C, int HW, int P,
            int chunk, int tpr, const float* __restrict__ scale, const float* __restrict__ shift,
            const float* __restrict__ mean, const float* __restrict__ rstd, int per_n_aff,
            int per_n_stat, ModView gam, ModView bet, ModView dgam, ModView dbet, float slope,
-           float* __restrict__ ps1, float* __restrict__ ps2) {
+           float* __restrict__ ps1, float* __restrict__ ps2, float* __restrict__ ps3,
+           float* __restrict__ ps4) {
+  // BCAST: gamma/beta are per-(n,c) (pixel stride 0, AdaIN / CBN); their
+  // gradients are pixel reductions (S3 = Σ dy·nrm, S4 = Σ dy) instead of maps.
   __shared__ float sh1[kThreads][CL ? VEC : 1];
   __shared__ float sh2[kThreads][CL ? VEC : 1];
+  __shared__ float sh3[BCAST ? kThreads : 1][CL ? VEC : 1];
+  __shared__ float sh4[BCAST ? kThreads : 1][CL ? VEC : 1];
   const T* __restrict__ gp = reinterpret_cast<const T*>(gam.ptr);
   const T* __restrict__ bp = reinterpret_cast<const T*>(bet.ptr);
   T* __restrict__ dgp = reinterpret_cast<T*>(const_cast<void*>(dgam.ptr));
@@ -263,9 +268,9 @@ bwd_reduce(const T* __restrict__ x, const T* __restrict__ dout, int N, int C, in
     const int tc = tid % tpr, r = tid / tpr;
     const int c0 = (blockIdx.z * tpr + tc) * VEC;
     const bool active = (r < rpb) && (c0 < C);
-    float a1[VEC], a2[VEC];
+    float a1[VEC], a2[VEC], a3[VEC], a4[VEC];
 #pragma unroll
-    for (int v = 0; v < VEC; ++v) { a1[v] = 0.f; a2[v] = 0.f; }
+    for (int v = 0; v < VEC; ++v) { a1[v] = 0.f; a2[v] = 0.f; a3[v] = 0.f; a4[v] = 0.f; }
     if (active) {
       float sc[VEC], sh[VEC], mu[VEC], rs[VEC];
 #pragma unroll
@@ -301,15 +306,19 @@ bwd_reduce(const T* __restrict__ x, const T* __restrict__ dout, int N, int C, in
           const float xh = (xv[v] - mu[v]) * rs[v];
           a1[v] += g;
           a2[v] = fmaf(g, xh, a2[v]);
+          if (BCAST) { a3[v] += dg[v]; a4[v] += db[v]; }
         }
-        if (MOD) {
+        if (MOD && !BCAST) {
           store_vec<T, VEC>(dgp + n * dgam.sn + (int64_t)c0 * dgam.sc + (int64_t)pix * dgam.sp, dg);
           store_vec<T, VEC>(dbp + n * dbet.sn + (int64_t)c0 * dbet.sc + (int64_t)pix * dbet.sp, db);
         }
       }
     }
 #pragma unroll
-    for (int v = 0; v < VEC; ++v) { sh1[tid][v] = a1[v]; sh2[tid][v] = a2[v]; }
+    for (int v = 0; v < VEC; ++v) {
+      sh1[tid][v] = a1[v]; sh2[tid][v] = a2[v];
+      if (BCAST) { sh3[tid][v] = a3[v]; sh4[tid][v] = a4[v]; }
+    }
     __syncthreads();
     int s = 1;
     while (s < rpb) s <<= 1;
@@ -319,6 +328,10 @@ bwd_reduce(const T* __restrict__ x, const T* __restrict__ dout, int N, int C, in
         for (int v = 0; v < VEC; ++v) {
           sh1[tid][v] += sh1[tid + s * tpr][v];
           sh2[tid][v] += sh2[tid + s * tpr][v];
+          if (BCAST) {
+            sh3[tid][v] += sh3[tid + s * tpr][v];
+            sh4[tid][v] += sh4[tid + s * tpr][v];
+          }
         }
       }
       __syncthreads();
@@ -327,14 +340,17 @@ bwd_reduce(const T* __restrict__ x, const T* __restrict__ dout, int N, int C, in
       const int64_t o = ((int64_t)n * P + p) * C + c0;
 #pragma unroll
       for (int v = 0; v < VEC; ++v)
-        if (c0 + v < C) { ps1[o + v] = sh1[tid][v]; ps2[o + v] = sh2[tid][v]; }
+        if (c0 + v < C) {
+          ps1[o + v] = sh1[tid][v]; ps2[o + v] = sh2[tid][v];
+          if (BCAST) { ps3[o + v] = sh3[tid][v]; ps4[o + v] = sh4[tid][v]; }
+        }
     }
   } else {
     const int c = blockIdx.z;
     const int64_t ai = (int64_t)(per_n_aff ? n : 0) * C + c;
     const int64_t si = (int64_t)(per_n_stat ? n : 0) * C + c;
     const float sc = scale[ai], sh = shift[ai], mu = mean[si], rs = rstd[si];
-    float a1 = 0.f, a2 = 0.f;
+    float a1 = 0.f, a2 = 0.f, a3 = 0.f, a4 = 0.f;
     const int64_t base = ((int64_t)n * C + c) * HW;
     for (int pix = pix0 + tid * VEC; pix < pix1; pix += kThreads * VEC) {
       float xv[VEC], dv[VEC], gv[VEC], bv[VEC], dg[VEC], db[VEC];
@@ -357,41 +373,48 @@ bwd_reduce(const T* __restrict__ x, const T* __restrict__ dout, int N, int C, in
         }
         a1 += g;
         a2 = fmaf(g, (xv[v] - mu) * rs, a2);
+        if (BCAST) { a3 += dg[v]; a4 += db[v]; }
       }
-      if (MOD) {
+      if (MOD && !BCAST) {
         store_vec<T, VEC>(dgp + n * dgam.sn + (int64_t)c * dgam.sc + pix * dgam.sp, dg);
         store_vec<T, VEC>(dbp + n * dbet.sn + (int64_t)c * dbet.sc + pix * dbet.sp, db);
       }
     }
     a1 = wave_sum(a1);
     a2 = wave_sum(a2);
+    if (BCAST) { a3 = wave_sum(a3); a4 = wave_sum(a4); }
     const int lane = tid & 63, w = tid >> 6;
-    if (lane == 0) { sh1[w][0] = a1; sh2[w][0] = a2; }
+    if (lane == 0) {
+      sh1[w][0] = a1; sh2[w][0] = a2;
+      if (BCAST) { sh3[w][0] = a3; sh4[w][0] = a4; }
+    }
     __syncthreads();
     if (tid == 0) {
-      float t1 = 0.f, t2 = 0.f;
-      for (int i = 0; i < kThreads / 64; ++i) { t1 += sh1[i][0]; t2 += sh2[i][0]; }
+      float t1 = 0.f, t2 = 0.f, t3 = 0.f, t4 = 0.f;
+      for (int i = 0; i < kThreads / 64; ++i) {
+        t1 += sh1[i][0]; t2 += sh2[i][0];
+        if (BCAST) { t3 += sh3[i][0]; t4 += sh4[i][0]; }
+      }
       const int64_t o = ((int64_t)n * P + p) * C + c;
       ps1[o] = t1;
       ps2[o] = t2;
+      if (BCAST) { ps3[o] = t3; ps4[o] = t4; }
     }
   }
 }
 
 // Sum partials over the chunk axis: [N][P][C] -> [N][C].
-__global__ void sum_partials(const float* __restrict__ ps1, const float* __restrict__ ps2, int N,
-                             int P, int C, float* __restrict__ s1, float* __restrict__ s2) {
+__global__ void sum_partials(const float* __restrict__ ps, int Q, int64_t qstride, int N, int P,
+                             int C, float* __restrict__ out) {
+  // ps: Q planes of [N][P][C] (plane stride qstride) -> out: Q planes of [N][C]
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= N * C) return;
   const int n = idx / C, c = idx % C;
-  float t1 = 0.f, t2 = 0.f;
-  for (int p = 0; p < P; ++p) {
-    const int64_t o = ((int64_t)n * P + p) * C + c;
-    t1 += ps1[o];
-    t2 += ps2[o];
+  for (int q = 0; q < Q; ++q) {
+    float t = 0.f;
+    for (int p = 0; p < P; ++p) t += ps[q * qstride + ((int64_t)n * P + p) * C + c];
+    out[(int64_t)q * N * C + idx] = t;
   }
-  s1[idx] = t1;
-  s2[idx] = t2;
 }
 
 // ------------------------------------------------------------------------
@@ -655,28 +678,40 @@ std::vector<at::Tensor> norm_bwd_reduce(const at::Tensor& x, const at::Tensor& d
   ModView gm = view_of(gamma, g), bt = view_of(beta, g), dgm = view_of(dgamma, g),
           dbt = view_of(dbeta, g);
   const bool mod = gm.ptr != nullptr;
+  // broadcast modulation (per-(n,c) gamma/beta): pixel stride 0
+  const bool bcast = mod && gm.sp == 0 && bt.sp == 0 && g.HW > 1;
+  IAMD_CHECK(!mod || bcast || (dgm.ptr != nullptr && dbt.ptr != nullptr),
+             "norm_bwd_reduce: spatial modulation needs dgamma/dbeta outputs");
   const int vec = pick_vec(g, x.element_size(), {gm, bt, dgm, dbt});
   int P, chunk, tpr, nzc;
   reduce_plan(g, vec, P, chunk, tpr, nzc);
   auto fopt = x.options().dtype(at::kFloat);
-  auto ps1 = at::empty({g.N, P, g.C}, fopt), ps2 = at::empty({g.N, P, g.C}, fopt);
+  const int Q = bcast ? 4 : 2;
+  auto ps = at::empty({Q, g.N, P, g.C}, fopt);
+  const int64_t qs = (int64_t)g.N * P * g.C;
+  float* ps1 = ps.data_ptr<float>();
+  float* ps2 = ps1 + qs;
+  float* ps3 = bcast ? ps1 + 2 * qs : nullptr;
+  float* ps4 = bcast ? ps1 + 3 * qs : nullptr;
   dim3 grid(P, g.N, g.cl ? nzc : g.C);
   IAMD_DISPATCH_FLOAT_TYPES(x.scalar_type(), "norm_bwd_reduce", [&] {
     const scalar_t* xp = reinterpret_cast<const scalar_t*>(x.data_ptr());
     const scalar_t* dp = reinterpret_cast<const scalar_t*>(dout.data_ptr());
-    auto launch = [&](auto vtag, auto cltag, auto modtag) {
+    auto launch = [&](auto vtag, auto cltag, auto modtag, auto bctag) {
       constexpr int V = decltype(vtag)::value;
       constexpr bool CLv = decltype(cltag)::value;
       constexpr bool M = decltype(modtag)::value;
-      hipLaunchKernelGGL((bwd_reduce<scalar_t, CLv, V, M>), grid, dim3(kThreads), 0, stream(), xp,
-                         dp, g.N, g.C, g.HW, P, chunk, tpr, scale.data_ptr<float>(),
+      constexpr bool B = decltype(bctag)::value;
+      hipLaunchKernelGGL((bwd_reduce<scalar_t, CLv, V, M, B>), grid, dim3(kThreads), 0, stream(),
+                         xp, dp, g.N, g.C, g.HW, P, chunk, tpr, scale.data_ptr<float>(),
                          shift.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
-                         per_n_aff, per_n_stat, gm, bt, dgm, dbt, (float)slope,
-                         ps1.data_ptr<float>(), ps2.data_ptr<float>());
+                         per_n_aff, per_n_stat, gm, bt, dgm, dbt, (float)slope, ps1, ps2, ps3,
+                         ps4);
     };
     auto by_mod = [&](auto vtag, auto cltag) {
-      if (mod) launch(vtag, cltag, std::true_type());
-      else launch(vtag, cltag, std::false_type());
+      if (bcast) launch(vtag, cltag, std::true_type(), std::true_type());
+      else if (mod) launch(vtag, cltag, std::true_type(), std::false_type());
+      else launch(vtag, cltag, std::false_type(), std::false_type());
     };
     auto by_cl = [&](auto vtag) {
       if (g.cl) by_mod(vtag, std::true_type());
@@ -690,12 +725,14 @@ std::vector<at::Tensor> norm_bwd_reduce(const at::Tensor& x, const at::Tensor& d
     }
   });
   IAMD_LAUNCH_CHECK();
-  auto s1 = at::empty({g.N, g.C}, fopt), s2 = at::empty({g.N, g.C}, fopt);
+  auto sums = at::empty({Q, g.N, g.C}, fopt);
   hipLaunchKernelGGL(sum_partials, dim3(ceil_div((int64_t)g.N * g.C, 256)), dim3(256), 0, stream(),
-                     ps1.data_ptr<float>(), ps2.data_ptr<float>(), g.N, P, g.C,
-                     s1.data_ptr<float>(), s2.data_ptr<float>());
+                     ps1, Q, qs, g.N, P, g.C, sums.data_ptr<float>());
   IAMD_LAUNCH_CHECK();
-  return {s1, s2};
+  // (S1, S2[, S3 = dgamma, S4 = dbeta for broadcast modulation]), each [N, C]
+  std::vector<at::Tensor> out;
+  for (int q = 0; q < Q; ++q) out.push_back(sums[q]);
+  return out;
 }
 
 at::Tensor norm_bwd_apply(const at::Tensor& x, const at::Tensor& dout, const at::Tensor& scale,

@@ -1,0 +1,13 @@
+"""Placeholder discriminator (reference discriminators/dummy.py:10-29)."""
+import torch.nn as nn
+
+from imaginaire_amd.layers import LinearBlock
+
+
+class Discriminator(nn.Module):
+    def __init__(self, dis_cfg, data_cfg):
+        super().__init__()
+        self.dummy_layer = LinearBlock(1, 1)
+
+    def forward(self, data):
+        return

@@ -1,0 +1,43 @@
+"""SAGAN self-attention block (reference layers/non_local.py:13-79).
+
+θ/φ/g 1×1 convs, 2×2 max-pool on keys/values; the attention itself runs
+through PyTorch's fused scaled-dot-product kernel (no scaling, matching the
+reference's raw ``softmax(θᵀφ)``), which avoids materialising the HW×HW/4
+energy matrix in HBM.
+"""
+from functools import partial
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .conv import Conv2dBlock
+
+
+class NonLocal2dBlock(nn.Module):
+    def __init__(self, in_channels, scale=True, clamp=False, weight_norm_type='none'):
+        super().__init__()
+        self.clamp = clamp
+        self.gamma = nn.Parameter(torch.zeros(1)) if scale else 1.0
+        self.in_channels = in_channels
+        base_conv2d_block = partial(Conv2dBlock, kernel_size=1, stride=1, padding=0,
+                                    weight_norm_type=weight_norm_type)
+        self.theta = base_conv2d_block(in_channels, in_channels // 8)
+        self.phi = base_conv2d_block(in_channels, in_channels // 8)
+        self.g = base_conv2d_block(in_channels, in_channels // 2)
+        self.out_conv = base_conv2d_block(in_channels // 2, in_channels)
+        self.softmax = nn.Softmax(dim=-1)
+        self.max_pool = nn.MaxPool2d(2)
+
+    def forward(self, x):
+        n, c, h, w = x.size()
+        theta = self.theta(x).reshape(n, -1, h * w).permute(0, 2, 1)          # [n, hw, c/8]
+        phi = self.max_pool(self.phi(x)).reshape(n, -1, h * w // 4).permute(0, 2, 1)  # [n, hw/4, c/8]
+        g = self.max_pool(self.g(x)).reshape(n, -1, h * w // 4).permute(0, 2, 1)      # [n, hw/4, c/2]
+        out = F.scaled_dot_product_attention(theta[:, None], phi[:, None], g[:, None],
+                                             scale=1.0)[:, 0]                # [n, hw, c/2]
+        out = out.permute(0, 2, 1).reshape(n, c // 2, h, w)
+        out = self.out_conv(out)
+        if self.clamp:
+            return self.gamma.clamp(-1, 1) * out + x
+        return self.gamma * out + x

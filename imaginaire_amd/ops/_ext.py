@@ -1,0 +1,55 @@
+"""Loader for the gfx950 HIP extension ``imaginaire_amd._C``.
+
+Policy: on a GPU tensor every op in ``imaginaire_amd.ops`` runs its HIP kernel.
+If the extension is missing on a machine that has a GPU the op raises (no
+silent eager fallback). CPU tensors use the PyTorch reference implementation
+of the same math (this is what the CPU test-suite and the CPU plumbing config
+exercise). Set ``IMAGINAIRE_AMD_EAGER=1`` to force the reference path on GPU
+(used only by the self-baseline benchmark and numerics tests).
+"""
+import importlib
+import os
+
+_EXT = None
+_ERR = None
+
+
+def load():
+    global _EXT, _ERR
+    if _EXT is not None or _ERR is not None:
+        return _EXT
+    try:
+        _EXT = importlib.import_module('imaginaire_amd._C')
+    except ImportError as e:  # pragma: no cover - depends on build state
+        _ERR = e
+        _EXT = None
+    return _EXT
+
+
+def available():
+    return load() is not None
+
+
+def force_eager():
+    return os.environ.get('IMAGINAIRE_AMD_EAGER', '0') == '1'
+
+
+def use_native(t):
+    """True if tensor ``t`` should go through the HIP kernel."""
+    if t is None or not t.is_cuda:
+        return False
+    if force_eager():
+        return False
+    ext = load()
+    if ext is None:
+        raise RuntimeError(
+            'imaginaire_amd: the HIP extension _C is not built but a GPU tensor '
+            'was given ({}). Run `python -m imaginaire_amd._build`.'.format(_ERR))
+    return True
+
+
+def ext():
+    e = load()
+    if e is None:
+        raise RuntimeError('imaginaire_amd._C not available: {}'.format(_ERR))
+    return e

@@ -1,0 +1,296 @@
+"""Fused normalisation + (spatially) adaptive modulation + activation (k1).
+
+One op serves every normalisation the reference builds in its blocks:
+
+* ``SpatiallyAdaptiveNorm`` (SPADE; reference layers/activation_norm.py:109-234)
+  ``out = act((norm(x)·a + b)·(1 + γ) + β)`` with γ, β ∈ [N, C, H, W];
+* ``AdaptiveNorm`` (AdaIN / CBN; activation_norm.py:22-106) — same with γ, β
+  ∈ [N, C] broadcast over pixels;
+* plain batch / sync-batch / instance norm followed by the block's activation.
+
+``mode`` is ``'batch'``, ``'sync_batch'``, ``'instance'`` or ``'none'``; the
+activation is a leaky slope (1.0 = identity, 0.0 = relu, 0.2 = the reference's
+``leakyrelu``). On GPU tensors the HIP kernels of ``csrc/spade_norm.hip`` run
+(stats → finalize → apply; backward reduce → apply); on CPU the PyTorch
+reference below runs. SyncBN exchanges per-rank (count, mean, var) with one
+all-gather in forward and Σg, Σg·x̂ with one all-reduce in backward.
+"""
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+from imaginaire_amd.ops import _ext
+
+
+def _world(group):
+    if not (dist.is_available() and dist.is_initialized()):
+        return 1
+    return dist.get_world_size(group)
+
+
+def _merge_stats(cnt, mean, var, group):
+    """All-gather per-rank (count, mean, var) [1, C] and merge (Chan)."""
+    stacked = torch.stack([cnt.reshape(-1), mean.reshape(-1), var.reshape(-1)], 0)
+    world = _world(group)
+    bufs = [torch.empty_like(stacked) for _ in range(world)]
+    dist.all_gather(bufs, stacked.contiguous(), group=group)
+    allst = torch.stack(bufs, 0)  # [W, 3, C]
+    n_i, m_i, v_i = allst[:, 0], allst[:, 1], allst[:, 2]
+    n = n_i.sum(0)
+    mean_g = (n_i * m_i).sum(0) / n.clamp_min(1)
+    m2 = (n_i * (v_i + (m_i - mean_g) ** 2)).sum(0)
+    var_g = m2 / n.clamp_min(1)
+    return n.reshape(1, -1), mean_g.reshape(1, -1), var_g.reshape(1, -1)
+
+
+def _update_running(running_mean, running_var, mean, var, count, factor):
+    if running_mean is None:
+        return
+    with torch.no_grad():
+        n = count.reshape(-1)
+        unbiased = var.reshape(-1) * n / (n - 1).clamp_min(1)
+        running_mean.mul_(1 - factor).add_(mean.reshape(-1).to(running_mean.dtype), alpha=factor)
+        running_var.mul_(1 - factor).add_(unbiased.to(running_var.dtype), alpha=factor)
+
+
+def _expand_mod(t, x):
+    if t is None:
+        return None
+    if t.dim() == 2:
+        return t[:, :, None, None].expand(-1, -1, x.shape[2], x.shape[3])
+    return t
+
+
+class _NormCfg:
+    __slots__ = ('mode', 'training', 'momentum', 'eps', 'slope', 'group', 'use_batch_stats')
+
+    def __init__(self, mode, training, momentum, eps, slope, group):
+        self.mode = mode
+        self.training = training
+        self.momentum = momentum
+        self.eps = eps
+        self.slope = slope
+        self.group = group
+        self.use_batch_stats = mode == 'instance' or (mode in ('batch', 'sync_batch') and training)
+
+
+class _FusedNormActFn(torch.autograd.Function):
+    """HIP path. ``gb`` (combined [N, 2C, H, W] γ|β tensor) or (γ, β)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, gamma, beta, gb, running_mean, running_var, cfg):
+        C = x.shape[1]
+        ext = _ext.ext()
+        if gb is not None:
+            gamma_v, beta_v = gb[:, :C], gb[:, C:]
+        else:
+            gamma_v, beta_v = _expand_mod(gamma, x), _expand_mod(beta, x)
+            if gamma_v is not None and gamma_v.dtype != x.dtype:
+                gamma_v, beta_v = gamma_v.to(x.dtype), beta_v.to(x.dtype)
+        wf = weight.float() if weight is not None else None
+        bf = bias.float() if bias is not None else None
+        per_instance = cfg.mode == 'instance'
+        if cfg.mode == 'none':
+            mean = x.new_zeros((1, C), dtype=torch.float32)
+            var = x.new_ones((1, C), dtype=torch.float32)
+            rstd = torch.ones_like(var)
+            scale = wf.reshape(1, C).contiguous() if wf is not None else torch.ones_like(var)
+            shift = bf.reshape(1, C).contiguous() if bf is not None else torch.zeros_like(var)
+            count = None
+        elif cfg.use_batch_stats:
+            sync = cfg.mode == 'sync_batch' and _world(cfg.group) > 1
+            count, mean, var, scale, shift = ext.norm_stats(x, per_instance, cfg.eps, wf, bf, sync)
+            if sync:
+                count, mean, var = _merge_stats(count, mean, var, cfg.group)
+            rstd = torch.rsqrt(var + cfg.eps)
+            if sync:
+                a = wf.reshape(1, C) if wf is not None else 1.0
+                b = bf.reshape(1, C) if bf is not None else 0.0
+                scale = (rstd * a).contiguous()
+                shift = (b - mean * scale).contiguous()
+            if cfg.training and not per_instance:
+                _update_running(running_mean, running_var, mean, var, count, cfg.momentum)
+        else:  # eval with running statistics
+            mean = running_mean.float().reshape(1, C)
+            var = running_var.float().reshape(1, C)
+            rstd = torch.rsqrt(var + cfg.eps)
+            a = wf.reshape(1, C) if wf is not None else 1.0
+            b = bf.reshape(1, C) if bf is not None else 0.0
+            scale = (rstd * a).contiguous()
+            shift = (b - mean * scale).contiguous()
+            count = None
+        out = ext.norm_apply(x, scale, shift, gamma_v, beta_v, cfg.slope)
+        ctx.cfg = cfg
+        ctx.has_gb = gb is not None
+        ctx.has_mod = gamma_v is not None
+        ctx.mod_bcast = gb is None and gamma is not None and gamma.dim() == 2
+        ctx.mod_dtypes = (gamma.dtype if gamma is not None else None,
+                          beta.dtype if beta is not None else None)
+        ctx.count = count
+        ctx.save_for_backward(x, weight, gamma, beta, gb, scale, shift, mean, rstd)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, weight, gamma, beta, gb, scale, shift, mean, rstd = ctx.saved_tensors
+        cfg = ctx.cfg
+        ext = _ext.ext()
+        C = x.shape[1]
+        fmt = torch.channels_last if (x.is_contiguous(memory_format=torch.channels_last)
+                                      and not x.is_contiguous()) else torch.contiguous_format
+        dout = dout.contiguous(memory_format=fmt)
+        if dout.dtype != x.dtype:
+            dout = dout.to(x.dtype)
+        dgb = dgamma = dbeta = None
+        if ctx.has_gb:
+            gamma_v, beta_v = gb[:, :C], gb[:, C:]
+            dgb = torch.empty_like(gb)
+            dgam_v, dbet_v = dgb[:, :C], dgb[:, C:]
+        elif ctx.has_mod:
+            gamma_v, beta_v = _expand_mod(gamma, x), _expand_mod(beta, x)
+            if gamma_v.dtype != x.dtype:
+                gamma_v, beta_v = gamma_v.to(x.dtype), beta_v.to(x.dtype)
+            if ctx.mod_bcast:
+                dgam_v = dbet_v = None
+            else:
+                dgam_v = torch.empty_like(gamma_v, memory_format=fmt) if gamma_v.dtype == x.dtype else None
+                dbet_v = torch.empty_like(beta_v, memory_format=fmt)
+        else:
+            gamma_v = beta_v = dgam_v = dbet_v = None
+        sums = ext.norm_bwd_reduce(x, dout, scale, shift, mean, rstd, gamma_v, beta_v,
+                                   dgam_v, dbet_v, cfg.slope)
+        S1, S2 = sums[0], sums[1]
+        if ctx.has_mod and ctx.mod_bcast:
+            dgamma = sums[2].to(ctx.mod_dtypes[0])
+            dbeta = sums[3].to(ctx.mod_dtypes[1])
+        elif ctx.has_mod and not ctx.has_gb:
+            dgamma, dbeta = dgam_v, dbet_v
+        N, HW = x.shape[0], x.shape[2] * x.shape[3]
+        dweight = S2.sum(0).to(weight.dtype) if weight is not None and ctx.needs_input_grad[1] else None
+        dbias = S1.sum(0).to(weight.dtype if weight is not None else torch.float32) \
+            if ctx.needs_input_grad[2] else None
+        if cfg.mode == 'none' or not cfg.use_batch_stats:
+            # no batch statistics in the graph: dx = g * scale
+            k1 = scale.contiguous()
+            k2 = torch.zeros_like(k1)
+            k3 = k2
+        elif cfg.mode == 'instance':
+            k1 = (rstd * (weight.float().reshape(1, C) if weight is not None else 1.0))
+            k1 = k1.expand(N, C).contiguous()
+            k2 = (S1 / HW).contiguous()
+            k3 = (S2 / HW).contiguous()
+        else:
+            s = torch.stack([S1.sum(0), S2.sum(0)], 0)
+            if cfg.mode == 'sync_batch' and _world(cfg.group) > 1:
+                dist.all_reduce(s, group=cfg.group)
+                M = ctx.count.reshape(1, C)
+            else:
+                M = float(N * HW)
+            k1 = (rstd * (weight.float().reshape(1, C) if weight is not None else 1.0)).contiguous()
+            k2 = (s[0:1] / M).contiguous()
+            k3 = (s[1:2] / M).contiguous()
+        mean_b, rstd_b = mean, rstd
+        dx = ext.norm_bwd_apply(x, dout, scale, shift, mean_b, rstd_b, k1, k2, k3,
+                                gamma_v, beta_v, cfg.slope) if ctx.needs_input_grad[0] else None
+        return dx, dweight, dbias, dgamma, dbeta, dgb, None, None, None
+
+
+def _reference(x, mode, weight, bias, gamma, beta, gb, running_mean, running_var, cfg):
+    C = x.shape[1]
+    if mode == 'none':
+        y = x
+        if weight is not None:
+            y = y * weight.reshape(1, C, 1, 1) + bias.reshape(1, C, 1, 1)
+    elif mode == 'instance':
+        y = F.instance_norm(x, weight=weight, bias=bias, eps=cfg.eps)
+    else:
+        sync = mode == 'sync_batch' and _world(cfg.group) > 1
+        if cfg.training:
+            xf = x.float()
+            dims = (0, 2, 3)
+            if sync:
+                cnt = torch.full((1, C), float(x.shape[0] * x.shape[2] * x.shape[3]),
+                                 device=x.device)
+                mean_l = xf.mean(dims).reshape(1, C)
+                var_l = xf.var(dims, unbiased=False).reshape(1, C)
+                cnt_g, mean_g, var_g = _SyncStats.apply(cnt, mean_l, var_l, cfg.group)
+            else:
+                mean_g = xf.mean(dims).reshape(1, C)
+                var_g = xf.var(dims, unbiased=False).reshape(1, C)
+                cnt_g = torch.full((1, C), float(x.shape[0] * x.shape[2] * x.shape[3]),
+                                   device=x.device)
+            _update_running(running_mean, running_var, mean_g.detach(), var_g.detach(),
+                            cnt_g.detach(), cfg.momentum)
+            y = (xf - mean_g.reshape(1, C, 1, 1)) * torch.rsqrt(var_g.reshape(1, C, 1, 1) + cfg.eps)
+            y = y.to(x.dtype)
+        else:
+            y = (x - running_mean.reshape(1, C, 1, 1)) * torch.rsqrt(
+                running_var.reshape(1, C, 1, 1) + cfg.eps)
+        if weight is not None:
+            y = y * weight.reshape(1, C, 1, 1) + bias.reshape(1, C, 1, 1)
+    if gb is not None:
+        gamma, beta = gb[:, :C], gb[:, C:]
+    if gamma is not None:
+        if gamma.dim() == 2:
+            gamma, beta = gamma[:, :, None, None], beta[:, :, None, None]
+        y = y * (1 + gamma) + beta
+    if cfg.slope != 1.0:
+        y = F.leaky_relu(y, cfg.slope) if cfg.slope > 0 else F.relu(y)
+    return y
+
+
+class _SyncStats(torch.autograd.Function):
+    """Differentiable cross-rank merge of (count, mean, var) for the CPU reference."""
+
+    @staticmethod
+    def forward(ctx, cnt, mean, var, group):
+        ctx.group = group
+        ctx.save_for_backward(cnt)
+        n, m, v = _merge_stats(cnt, mean, var, group)
+        ctx.mark_non_differentiable(n)
+        ctx.local = (cnt, mean, var, n, m)
+        return n, m, v
+
+    @staticmethod
+    def backward(ctx, dn, dmean_g, dvar_g):
+        cnt, mean_l, var_l, n, mean_g = ctx.local
+        # d mean_g / d mean_l = cnt/n ; d var_g / d var_l = cnt/n ;
+        # d var_g / d mean_l = 2 cnt (mean_l - mean_g) / n
+        w = cnt / n
+        dmean_l = dmean_g * w + dvar_g * 2 * w * (mean_l - mean_g)
+        dvar_l = dvar_g * w
+        return None, dmean_l, dvar_l, None
+
+
+def fused_norm_act(x, mode='batch', weight=None, bias=None, gamma=None, beta=None, gb=None,
+                   running_mean=None, running_var=None, training=True, momentum=0.1,
+                   eps=1e-5, slope=1.0, process_group=None):
+    """``act((norm(x)·w + b)·(1+γ) + β)`` — see module docstring.
+
+    ``momentum`` is the already-resolved exponential-average factor.
+    ``gb`` is an alternative to (γ, β): one [N, 2C, H, W] tensor whose first C
+    channels are γ and last C are β (output of a fused γ|β convolution).
+    """
+    if mode == 'sync_batch' and not training:
+        mode_eff = 'batch'
+    else:
+        mode_eff = mode
+    cfg = _NormCfg(mode_eff, training, momentum, eps, slope, process_group)
+    if gamma is not None and gamma.dim() == 2 and x.shape[2] * x.shape[3] == 1:
+        gamma = gamma.reshape(x.shape[0], x.shape[1], 1, 1)
+        beta = beta.reshape(x.shape[0], x.shape[1], 1, 1)
+    if _ext.use_native(x):
+        fmt = torch.channels_last if x.is_contiguous(memory_format=torch.channels_last) \
+            else torch.contiguous_format
+        if not x.is_contiguous(memory_format=fmt):
+            x = x.contiguous()
+        if gb is not None and gb.dtype != x.dtype:
+            gb = gb.to(x.dtype)
+        if gb is not None and not gb.is_contiguous(memory_format=fmt):
+            gb = gb.contiguous(memory_format=fmt)
+        if gamma is not None and gamma.dim() == 4 and not gamma.is_contiguous(memory_format=fmt):
+            gamma = gamma.contiguous(memory_format=fmt)
+            beta = beta.contiguous(memory_format=fmt)
+        return _FusedNormActFn.apply(x, weight, bias, gamma, beta, gb, running_mean,
+                                     running_var, cfg)
+    return _reference(x, mode_eff, weight, bias, gamma, beta, gb, running_mean, running_var, cfg)

@@ -1,0 +1,87 @@
+"""Multi-tensor fused Adam / AdamW (k4, ``csrc/multi_tensor.hip``).
+
+Replaces apex ``FusedAdam`` (reference utils/trainer.py:16, 271-281): one HIP
+launch updates every parameter of a param group (fp32 master weights, fp32 or
+bf16 gradients). Gradients are consumed as they are (no unscale pass: bf16
+autocast needs no loss scaler). On CPU the update runs through
+``torch._foreach_*`` with identical math.
+"""
+import math
+
+import torch
+from torch.optim import Optimizer
+
+from imaginaire_amd.ops import _ext
+
+
+class FusedAdam(Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
+                 adam_w_mode=False, amsgrad=False):
+        if amsgrad:
+            raise NotImplementedError('amsgrad is not supported by FusedAdam')
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
+                        adam_w_mode=adam_w_mode)
+        super().__init__(params, defaults)
+
+    def zero_grad(self, set_to_none=True):
+        super().zero_grad(set_to_none=set_to_none)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        for group in self.param_groups:
+            params, grads, m, v = [], [], [], []
+            for p in group['params']:
+                if p.grad is None:
+                    continue
+                if p.grad.is_sparse:
+                    raise RuntimeError('FusedAdam does not support sparse gradients')
+                state = self.state[p]
+                if len(state) == 0:
+                    state['step'] = 0
+                    state['exp_avg'] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    state['exp_avg_sq'] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                state['step'] += 1
+                params.append(p)
+                grads.append(p.grad)
+                m.append(state['exp_avg'])
+                v.append(state['exp_avg_sq'])
+            if not params:
+                continue
+            step = self.state[params[0]]['step']
+            beta1, beta2 = group['betas']
+            lr, eps, wd = group['lr'], group['eps'], group['weight_decay']
+            adamw = group['adam_w_mode']
+            if isinstance(lr, torch.Tensor):
+                lr = float(lr)
+            native = _ext.use_native(params[0]) and all(
+                p.dtype == torch.float32 and p.is_contiguous() for p in params)
+            if native:
+                gdt = grads[0].dtype
+                gl = [g if (g.dtype == gdt and g.is_contiguous()) else g.contiguous().to(gdt)
+                      for g in grads]
+                if gdt not in (torch.float32, torch.bfloat16):
+                    gl = [g.float() for g in gl]
+                _ext.ext().mt_adam(params, gl, m, v, [], lr, beta1, beta2, eps, int(step), wd,
+                                   bool(adamw), 1.0)
+            else:
+                _reference_adam(params, grads, m, v, lr, beta1, beta2, eps, step, wd, adamw)
+        return loss
+
+
+def _reference_adam(params, grads, m, v, lr, beta1, beta2, eps, step, wd, adamw):
+    grads = [g.float() for g in grads]
+    if wd != 0 and not adamw:
+        grads = torch._foreach_add(grads, params, alpha=wd)
+    torch._foreach_mul_(m, beta1)
+    torch._foreach_add_(m, grads, alpha=1 - beta1)
+    torch._foreach_mul_(v, beta2)
+    torch._foreach_addcmul_(v, grads, grads, value=1 - beta2)
+    bc1 = 1 - beta1 ** step
+    bc2 = 1 - beta2 ** step
+    denom = torch._foreach_sqrt(v)
+    torch._foreach_div_(denom, math.sqrt(bc2))
+    torch._foreach_add_(denom, eps)
+    if wd != 0 and adamw:
+        torch._foreach_mul_(params, 1 - lr * wd)
+    torch._foreach_addcdiv_(params, m, denom, value=-lr / bc1)

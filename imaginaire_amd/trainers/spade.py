@@ -1,0 +1,192 @@
+"""SPADE trainer (reference trainers/spade.py:23-312).
+
+Losses: hinge GAN + feature matching + VGG-19 perceptual + KL (style VAE).
+D step: G under ``no_grad``; G step: D on real and fake (batched into one D
+forward on MI355X, see discriminators/spade.py). Video batches (5-D) are
+folded into the label like the fork does (spade.py:108-123). FID for the
+regular and the EMA generator.
+"""
+import functools
+import math
+
+import torch
+import torch.nn.functional as F
+
+from imaginaire_amd.evaluation import compute_fid
+from imaginaire_amd.losses import FeatureMatchingLoss, GANLoss, GaussianKLLoss, PerceptualLoss
+from imaginaire_amd.trainers.base import BaseTrainer
+from imaginaire_amd.utils.distributed import master_only_print as print
+from imaginaire_amd.utils.meters import Meter
+from imaginaire_amd.utils.misc import split_labels
+from imaginaire_amd.registry import canonical_module_name
+from imaginaire_amd.utils.visualization import tensor2label
+
+
+class Trainer(BaseTrainer):
+    def __init__(self, cfg, net_G, net_D, opt_G, opt_D, sch_G, sch_D, train_data_loader,
+                 val_data_loader):
+        super().__init__(cfg, net_G, net_D, opt_G, opt_D, sch_G, sch_D, train_data_loader,
+                         val_data_loader)
+        self.video_mode = canonical_module_name(cfg.data.type) == \
+            'imaginaire_amd.datasets.paired_videos'
+
+    def _init_loss(self, cfg):
+        self.criteria['GAN'] = GANLoss(cfg.trainer.gan_mode)
+        self.weights['GAN'] = cfg.trainer.loss_weight.gan
+        if hasattr(cfg.trainer, 'perceptual_loss'):
+            self.criteria['Perceptual'] = PerceptualLoss(
+                cfg=cfg, network=cfg.trainer.perceptual_loss.mode,
+                layers=cfg.trainer.perceptual_loss.layers,
+                weights=cfg.trainer.perceptual_loss.weights)
+            self.weights['Perceptual'] = cfg.trainer.loss_weight.perceptual
+        self.criteria['FeatureMatching'] = FeatureMatchingLoss()
+        self.weights['FeatureMatching'] = cfg.trainer.loss_weight.feature_matching
+        self.criteria['GaussianKL'] = GaussianKLLoss()
+        self.weights['GaussianKL'] = cfg.trainer.loss_weight.kl
+
+    def _init_tensorboard(self):
+        self.regular_fid_meter = Meter('FID/regular')
+        if self.cfg.trainer.model_average:
+            self.average_fid_meter = Meter('FID/average')
+        self.image_meter = Meter('images')
+        self.meters = {}
+        for name in ['optim/gen_lr', 'optim/dis_lr', 'time/iteration', 'time/epoch']:
+            self.meters[name] = Meter(name)
+
+    def _start_of_iteration(self, data, current_iteration):
+        if data['label'].dim() == 5:
+            label_image_raw = data['images'][:, 0:-1]
+            label_image = label_image_raw.reshape(
+                [label_image_raw.size(0), -1, label_image_raw.size(3), label_image_raw.size(4)])
+            images = data['images'][:, -1]
+            label_label = data['label'].reshape(
+                [data['label'].size(0), -1, data['label'].size(3), data['label'].size(4)])
+            data['label'] = torch.cat([label_label, label_image], 1)
+            data['images'] = images
+        data = self.to_device(data)
+        return self._resize_data(data)
+
+    def gen_forward(self, data):
+        net_G_output = self.net_G(data)
+        net_D_output = self.net_D(data, net_G_output)
+        self._time_before_loss()
+        output_fake = self._get_outputs(net_D_output, real=False)
+        self.gen_losses['GAN'] = self.criteria['GAN'](output_fake, True, dis_update=False)
+        self.gen_losses['FeatureMatching'] = self.criteria['FeatureMatching'](
+            net_D_output['fake_features'], net_D_output['real_features'])
+        if self.net_G_module.use_style_encoder and net_G_output.get('mu') is not None:
+            self.gen_losses['GaussianKL'] = self.criteria['GaussianKL'](
+                net_G_output['mu'], net_G_output['logvar'])
+        else:
+            self.gen_losses['GaussianKL'] = torch.zeros((), device=self.device)
+        if hasattr(self.cfg.trainer, 'perceptual_loss'):
+            self.gen_losses['Perceptual'] = self.criteria['Perceptual'](
+                net_G_output['fake_images'], data['images'])
+        total_loss = torch.zeros((), device=self.device)
+        for key in self.criteria:
+            total_loss = total_loss + self.gen_losses[key] * self.weights[key]
+        self.gen_losses['total'] = total_loss
+        return total_loss
+
+    def dis_forward(self, data):
+        with torch.no_grad():
+            net_G_output = self.net_G(data)
+            net_G_output['fake_images'] = net_G_output['fake_images'].detach()
+        net_D_output = self.net_D(data, net_G_output)
+        self._time_before_loss()
+        output_fake = self._get_outputs(net_D_output, real=False)
+        output_real = self._get_outputs(net_D_output, real=True)
+        fake_loss = self.criteria['GAN'](output_fake, False, dis_update=True)
+        true_loss = self.criteria['GAN'](output_real, True, dis_update=True)
+        self.dis_losses['GAN/fake'] = fake_loss
+        self.dis_losses['GAN/true'] = true_loss
+        self.dis_losses['GAN'] = fake_loss + true_loss
+        total_loss = self.dis_losses['GAN'] * self.weights['GAN']
+        self.dis_losses['total'] = total_loss
+        return total_loss
+
+    def _get_visualizations(self, data):
+        self.recalculate_model_average_batch_norm_statistics(self.train_data_loader)
+        with torch.no_grad(), self.autocast():
+            dataset = getattr(self.train_data_loader, 'dataset', None)
+            segmap = data['label']
+            if dataset is not None and hasattr(dataset, 'get_label_lengths'):
+                labels = split_labels(data['label'], dataset.get_label_lengths())
+                segmap = labels.get('segmaps', labels.get('seg_maps', segmap))
+            segmap = tensor2label(segmap.float()).to(data['images'].device)
+            net_G_output = self.net_G(data, random_style=True)
+            vis_images = [data['images'][:, :3].float(), segmap,
+                          net_G_output['fake_images'][:, :3].float()]
+            if self.cfg.trainer.model_average:
+                avg_out = self.net_G.module.averaged_model(data, random_style=True)
+                vis_images.append(avg_out['fake_images'][:, :3].float())
+        return vis_images
+
+    def recalculate_model_average_batch_norm_statistics(self, data_loader):
+        if not self.cfg.trainer.model_average or data_loader is None:
+            return
+        n_iter = self.cfg.trainer.model_average_batch_norm_estimation_iteration
+        if n_iter == 0:
+            return
+        from imaginaire_amd.utils.model_average import (calibrate_batch_norm_momentum,
+                                                        reset_batch_norm)
+        with torch.no_grad(), self.autocast():
+            avg = self.net_G.module.averaged_model
+            avg.train()
+            avg.apply(reset_batch_norm)
+            for cal_it, cal_data in enumerate(data_loader):
+                if cal_it >= n_iter:
+                    break
+                cal_data = self._start_of_iteration(cal_data, 0)
+                avg.apply(calibrate_batch_norm_momentum)
+                avg(cal_data)
+
+    def write_metrics(self):
+        fids = self._compute_fid()
+        if fids is None:
+            return
+        if self.cfg.trainer.model_average:
+            regular_fid, average_fid = fids
+            self.regular_fid_meter.write(regular_fid)
+            self.average_fid_meter.write(average_fid)
+            meters = [self.regular_fid_meter, self.average_fid_meter]
+        else:
+            self.regular_fid_meter.write(fids)
+            meters = [self.regular_fid_meter]
+        for meter in meters:
+            meter.flush(self.current_iteration)
+
+    def _compute_fid(self):
+        if self.val_data_loader is None:
+            return None
+        self.net_G.eval()
+        net_G_for_evaluation = functools.partial(self.net_G, random_style=True)
+        regular_fid_path = self._get_save_path('regular_fid', 'npy')
+        preprocess = functools.partial(self._start_of_iteration, current_iteration=0)
+        with self.autocast():
+            regular_fid_value = compute_fid(regular_fid_path, self.val_data_loader,
+                                            net_G_for_evaluation, preprocess=preprocess)
+        print('Epoch {:05}, Iteration {:09}, Regular FID {}'.format(
+            self.current_epoch, self.current_iteration, regular_fid_value))
+        if self.cfg.trainer.model_average:
+            avg_net = functools.partial(self.net_G.module.averaged_model, random_style=True)
+            fid_path = self._get_save_path('average_fid', 'npy')
+            with self.autocast():
+                fid_value = compute_fid(fid_path, self.val_data_loader, avg_net,
+                                        preprocess=preprocess)
+            print('Epoch {:05}, Iteration {:09}, FID {}'.format(
+                self.current_epoch, self.current_iteration, fid_value))
+            self.net_G.train()
+            return regular_fid_value, fid_value
+        self.net_G.train()
+        return regular_fid_value
+
+    def _resize_data(self, data):
+        base = getattr(self.net_G, 'base', 32)
+        sy = math.floor(data['label'].size()[2] * 1.0 // base) * base
+        sx = math.floor(data['label'].size()[3] * 1.0 // base) * base
+        if (sy, sx) != tuple(data['label'].shape[2:]):
+            data['label'] = F.interpolate(data['label'], size=[sy, sx], mode='nearest')
+            if 'images' in data.keys():
+                data['images'] = F.interpolate(data['images'], size=[sy, sx], mode='bicubic')
+        return data

@@ -1,0 +1,155 @@
+"""Model / optimizer / scheduler / trainer factories (reference utils/trainer.py:24-306).
+
+Same flow as the reference: identical-seed weight init on every rank, then a
+rank-offset seed; G/D built from ``cfg.gen.type`` / ``cfg.dis.type``; optimizers
+from ``cfg.{gen,dis}_opt`` (adam → the fused multi-tensor HIP Adam when
+``fused_opt``); ``ModelAverage`` wrapping; data-parallel wrapping.
+
+MI355X mapping of the reference knobs:
+  * ``trainer.amp`` O1/O2 → bf16 autocast (no loss scaler), O0 → fp32;
+  * ``trainer.distributed_data_parallel`` 'pytorch' → our bucketed RCCL DDP
+    with backward overlap; 'apex' → the same without overlap (the apex
+    ``delay_allreduce`` semantics); 'torch' → stock torch DDP;
+  * SyncBN layers get a dedicated communicator (parallel/groups.py).
+"""
+import random
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+from torch.optim import SGD, Adam, RMSprop, lr_scheduler
+
+from imaginaire_amd.optimizers import Fromage, Madam, FusedAdam
+from imaginaire_amd.parallel import DistributedDataParallel, WrappedModel
+from imaginaire_amd.parallel.groups import assign_syncbn_group
+from imaginaire_amd.registry import import_module
+from imaginaire_amd.utils.distributed import get_rank, get_world_size
+from imaginaire_amd.utils.distributed import master_only_print as print
+from imaginaire_amd.utils.init_weight import weights_init
+from imaginaire_amd.utils.model_average import ModelAverage
+
+
+def set_random_seed(seed, by_rank=False):
+    if by_rank:
+        seed += get_rank()
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    if torch.cuda.is_available():
+        torch.cuda.manual_seed(seed)
+        torch.cuda.manual_seed_all(seed)
+
+
+def get_trainer(cfg, net_G, net_D=None, opt_G=None, opt_D=None, sch_G=None, sch_D=None,
+                train_data_loader=None, val_data_loader=None):
+    trainer_lib = import_module(cfg.trainer.type)
+    return trainer_lib.Trainer(cfg, net_G, net_D, opt_G, opt_D, sch_G, sch_D,
+                               train_data_loader, val_data_loader)
+
+
+def default_device():
+    if torch.cuda.is_available():
+        return torch.device('cuda', torch.cuda.current_device())
+    return torch.device('cpu')
+
+
+def get_model_optimizer_and_scheduler(cfg, seed=0, device=None):
+    device = device or default_device()
+    set_random_seed(seed, by_rank=False)
+    lib_G = import_module(cfg.gen.type)
+    lib_D = import_module(cfg.dis.type)
+    net_G = lib_G.Generator(cfg.gen, cfg.data)
+    net_D = lib_D.Discriminator(cfg.dis, cfg.data)
+    init_cfg = getattr(cfg.trainer, 'init', None)
+    init_type = getattr(init_cfg, 'type', 'xavier') if init_cfg is not None else 'xavier'
+    init_gain = getattr(init_cfg, 'gain', 0.02) if init_cfg is not None else 0.02
+    init_bias = getattr(init_cfg, 'bias', None) if init_cfg is not None else None
+    print('Initialize net_G and net_D weights using type: {} gain: {}'.format(init_type,
+                                                                             init_gain))
+    net_G.apply(weights_init(init_type, init_gain, init_bias))
+    net_D.apply(weights_init(init_type, init_gain, init_bias))
+    net_G = net_G.to(device)
+    net_D = net_D.to(device)
+    set_random_seed(seed, by_rank=True)
+    print('net_G parameter count: {:,}'.format(_calculate_model_size(net_G)))
+    print('net_D parameter count: {:,}'.format(_calculate_model_size(net_D)))
+    opt_G = get_optimizer(cfg.gen_opt, net_G)
+    opt_D = get_optimizer(cfg.dis_opt, net_D)
+    net_G, net_D, opt_G, opt_D = wrap_model_and_optimizer(cfg, net_G, net_D, opt_G, opt_D)
+    sch_G = get_scheduler(cfg.gen_opt, opt_G)
+    sch_D = get_scheduler(cfg.dis_opt, opt_D)
+    return net_G, net_D, opt_G, opt_D, sch_G, sch_D
+
+
+def wrap_model_and_optimizer(cfg, net_G, net_D, opt_G, opt_D):
+    if cfg.trainer.model_average:
+        net_G = ModelAverage(net_G, cfg.trainer.model_average_beta,
+                             cfg.trainer.model_average_start_iteration,
+                             cfg.trainer.model_average_remove_sn)
+    net_G_module = net_G.module if cfg.trainer.model_average else net_G
+    if hasattr(net_G_module, 'custom_init'):
+        net_G_module.custom_init()
+    net_G = _wrap_model(cfg, net_G)
+    net_D = _wrap_model(cfg, net_D)
+    return net_G, net_D, opt_G, opt_D
+
+
+def _calculate_model_size(model):
+    return sum(p.numel() for p in model.parameters() if p.requires_grad)
+
+
+def _wrap_model(cfg, model):
+    if dist.is_available() and dist.is_initialized() and get_world_size() > 1:
+        assign_syncbn_group(model)
+        ddp = getattr(cfg.trainer, 'distributed_data_parallel', 'pytorch')
+        bucket_mb = getattr(cfg.trainer, 'ddp_bucket_mb', 256)
+        comm = getattr(cfg.trainer, 'ddp_comm_dtype', None)
+        comm = torch.bfloat16 if comm in ('bf16', 'bfloat16') else None
+        if ddp == 'torch':
+            return torch.nn.parallel.DistributedDataParallel(
+                model, device_ids=[torch.cuda.current_device()] if torch.cuda.is_available()
+                else None, find_unused_parameters=True, broadcast_buffers=False)
+        return DistributedDataParallel(model, bucket_cap_mb=bucket_mb, comm_dtype=comm,
+                                       overlap=(ddp != 'apex'))
+    return WrappedModel(model)
+
+
+def get_scheduler(cfg_opt, opt):
+    if cfg_opt.lr_policy.type == 'step':
+        return lr_scheduler.StepLR(opt, step_size=cfg_opt.lr_policy.step_size,
+                                   gamma=cfg_opt.lr_policy.gamma)
+    if cfg_opt.lr_policy.type == 'constant':
+        return lr_scheduler.LambdaLR(opt, lambda x: 1)
+    raise NotImplementedError('Learning rate policy {} not implemented.'.format(
+        cfg_opt.lr_policy.type))
+
+
+def get_optimizer(cfg_opt, net):
+    if hasattr(net, 'get_param_groups'):
+        params = net.get_param_groups(cfg_opt)
+    else:
+        params = [p for p in net.parameters()]
+    return get_optimizer_for_params(cfg_opt, params)
+
+
+def get_optimizer_for_params(cfg_opt, params):
+    fused_opt = getattr(cfg_opt, 'fused_opt', True)
+    eps = getattr(cfg_opt, 'eps', 1e-8)
+    if cfg_opt.type == 'adam':
+        betas = (getattr(cfg_opt, 'adam_beta1', 0.0), getattr(cfg_opt, 'adam_beta2', 0.999))
+        if fused_opt:
+            return FusedAdam(params, lr=cfg_opt.lr, eps=eps, betas=betas)
+        return Adam(params, lr=cfg_opt.lr, eps=eps, betas=betas)
+    if cfg_opt.type == 'madam':
+        return Madam(params, lr=cfg_opt.lr, scale=getattr(cfg_opt, 'scale', 3.0),
+                     g_bound=getattr(cfg_opt, 'g_bound', None))
+    if cfg_opt.type == 'fromage':
+        return Fromage(params, lr=cfg_opt.lr)
+    if cfg_opt.type == 'rmsprop':
+        return RMSprop(params, lr=cfg_opt.lr, eps=eps,
+                       weight_decay=getattr(cfg_opt, 'weight_decay', 0))
+    if cfg_opt.type == 'sgd':
+        return SGD(params, lr=cfg_opt.lr, momentum=getattr(cfg_opt, 'momentum', 0),
+                   weight_decay=getattr(cfg_opt, 'weight_decay', 0))
+    raise NotImplementedError('Optimizer {} is not yet implemented.'.format(cfg_opt.type))

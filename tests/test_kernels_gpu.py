@@ -1,0 +1,181 @@
+"""Numerics of the gfx950 HIP kernels vs PyTorch fp32 references (GPU only)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_norm(x, mode, w, b, gamma, beta, slope, eps=1e-5):
+    xf = x.float()
+    if mode == 'batch':
+        y = F.batch_norm(xf, None, None, w, b, True, 0.0, eps)
+    elif mode == 'instance':
+        y = F.instance_norm(xf, weight=w, bias=b, eps=eps)
+    else:
+        y = xf
+    if gamma is not None:
+        g, bb = gamma.float(), beta.float()
+        if g.dim() == 2:
+            g, bb = g[:, :, None, None], bb[:, :, None, None]
+        y = y * (1 + g) + bb
+    return F.leaky_relu(y, slope) if slope != 1.0 else y
+
+
+@pytest.mark.parametrize('layout', ['cl', 'nchw'])
+@pytest.mark.parametrize('mode', ['batch', 'instance', 'none'])
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('mod', ['spatial', 'gb', 'bcast', None])
+def test_fused_norm_act(layout, mode, dtype, mod):
+    from imaginaire_amd.ops.norm import fused_norm_act
+    torch.manual_seed(0)
+    N, C, H, W = 2, 64, 12, 20
+    x = (torch.randn(N, C, H, W, device='cuda') * 2 + 0.5).to(dtype)
+    if layout == 'cl':
+        x = x.contiguous(memory_format=torch.channels_last)
+    w = torch.randn(C, device='cuda') * 0.5 + 1
+    b = torch.randn(C, device='cuda') * 0.1
+    gamma = beta = gb = None
+    if mod == 'spatial':
+        gamma = (torch.randn(N, C, H, W, device='cuda') * 0.3).to(dtype)
+        beta = (torch.randn(N, C, H, W, device='cuda') * 0.3).to(dtype)
+        if layout == 'cl':
+            gamma = gamma.contiguous(memory_format=torch.channels_last)
+            beta = beta.contiguous(memory_format=torch.channels_last)
+    elif mod == 'gb':
+        gb = (torch.randn(N, 2 * C, H, W, device='cuda') * 0.3).to(dtype)
+        if layout == 'cl':
+            gb = gb.contiguous(memory_format=torch.channels_last)
+    elif mod == 'bcast':
+        gamma = torch.randn(N, C, device='cuda') * 0.3
+        beta = torch.randn(N, C, device='cuda') * 0.3
+    tensors = [t for t in (x, w, b, gamma, beta, gb) if t is not None]
+    for t in tensors:
+        t.requires_grad_(True)
+    y = fused_norm_act(x, mode, w, b, gamma=gamma, beta=beta, gb=gb, training=True,
+                       momentum=0.0, slope=0.2)
+    g_gamma, g_beta = (gb[:, :C], gb[:, C:]) if gb is not None else (gamma, beta)
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().clone().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True)
+    gr = g_gamma.detach().float().requires_grad_(True) if g_gamma is not None else None
+    ber = g_beta.detach().float().requires_grad_(True) if g_beta is not None else None
+    yr = _ref_norm(xr, mode, wr, br, gr, ber, 0.2)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    assert torch.allclose(y.float(), yr, atol=tol * 5, rtol=tol), (y.float() - yr).abs().max()
+    go = torch.randn_like(yr)
+    y.backward(go.to(y.dtype))
+    yr.backward(go)
+    scale = lambda t: max(1.0, float(t.abs().max()))  # noqa: E731
+    assert torch.allclose(x.grad.float(), xr.grad, atol=tol * 5 * scale(xr.grad), rtol=tol * 5)
+    assert torch.allclose(w.grad, wr.grad, atol=tol * 20 * scale(wr.grad), rtol=tol * 5)
+    assert torch.allclose(b.grad, br.grad, atol=tol * 20 * scale(br.grad), rtol=tol * 5)
+    if gb is not None:
+        dgb = torch.cat([gr.grad, ber.grad], 1)
+        assert torch.allclose(gb.grad.float(), dgb, atol=tol * 5 * scale(dgb), rtol=tol * 5)
+    elif gamma is not None:
+        assert torch.allclose(gamma.grad.float(), gr.grad, atol=tol * 20 * scale(gr.grad),
+                              rtol=tol * 5)
+        assert torch.allclose(beta.grad.float(), ber.grad, atol=tol * 20 * scale(ber.grad),
+                              rtol=tol * 5)
+
+
+@pytest.mark.parametrize('layout', ['cl', 'nchw', 'linear'])
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_bias_act(layout, dtype):
+    from imaginaire_amd.ops.bias_act import bias_act
+    torch.manual_seed(1)
+    if layout == 'linear':
+        x = torch.randn(8, 96, device='cuda', dtype=dtype)
+    else:
+        x = torch.randn(2, 64, 9, 16, device='cuda', dtype=dtype)
+        if layout == 'cl':
+            x = x.contiguous(memory_format=torch.channels_last)
+    b = torch.randn(x.shape[1], device='cuda')
+    x.requires_grad_(True)
+    b.requires_grad_(True)
+    y = bias_act(x, b, 0.2)
+    xr = x.detach().float().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True)
+    shape = [1, -1] + [1] * (x.dim() - 2)
+    yr = F.leaky_relu(xr + br.reshape(shape), 0.2)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    assert torch.allclose(y.float(), yr, atol=tol, rtol=tol)
+    go = torch.randn_like(yr)
+    y.backward(go.to(dtype))
+    yr.backward(go)
+    assert torch.allclose(x.grad.float(), xr.grad, atol=tol * 2, rtol=tol * 2)
+    assert torch.allclose(b.grad, br.grad, atol=tol * 50, rtol=tol * 5)
+
+
+def test_partial_conv_renorm():
+    from imaginaire_amd.ops.partial_conv import partial_conv_renorm, _mask_stats_reference
+    torch.manual_seed(2)
+    raw = torch.randn(2, 16, 10, 12, device='cuda')
+    mask = (torch.rand(2, 1, 10, 12, device='cuda') > 0.3).float()
+    bias = torch.randn(16, device='cuda')
+    raw.requires_grad_(True)
+    out, upd = partial_conv_renorm(raw, mask, bias, 3, 1, 1, 1, 9.0)
+    ratio, update = _mask_stats_reference(mask, (3, 3), (1, 1), (1, 1), (1, 1), 9.0, 1e-6)
+    ref = (raw.detach() * ratio + bias.view(1, -1, 1, 1)) * update
+    assert torch.allclose(out, ref, atol=1e-5, rtol=1e-5)
+    assert torch.allclose(upd, update)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_flow_warp(dtype):
+    from imaginaire_amd.ops.flow_warp import flow_warp, flow_warp_reference
+    torch.manual_seed(3)
+    img = torch.randn(2, 3, 17, 23, device='cuda', dtype=dtype)
+    flow = (torch.randn(2, 2, 17, 23, device='cuda') * 4).to(dtype)
+    img.requires_grad_(True)
+    flow.requires_grad_(True)
+    out = flow_warp(img, flow)
+    ir = img.detach().float().requires_grad_(True)
+    fr = flow.detach().float().requires_grad_(True)
+    ref = flow_warp_reference(ir, fr)
+    tol = 3e-2 if dtype == torch.bfloat16 else 1e-4
+    assert torch.allclose(out.float(), ref, atol=tol, rtol=tol)
+    g = torch.randn_like(ref)
+    out.backward(g.to(dtype))
+    ref.backward(g)
+    assert torch.allclose(img.grad.float(), ir.grad, atol=tol * 5, rtol=tol * 5)
+    # flow gradient differs only at exact integer/border positions
+    close = (flow.grad.float() - fr.grad).abs() <= tol * 10 + tol * 10 * fr.grad.abs()
+    assert close.float().mean() > 0.99
+
+
+def test_multi_tensor_adam_and_ema():
+    from imaginaire_amd.optimizers.fused_adam import FusedAdam, _reference_adam
+    from imaginaire_amd.ops import _ext
+    torch.manual_seed(4)
+    shapes = [(37,), (128, 64), (3, 5, 7, 11), (1,), (70001,)]
+    ps = [torch.randn(s, device='cuda') for s in shapes]
+    refs = [p.detach().clone() for p in ps]
+    for p in ps:
+        p.requires_grad_(True)
+    opt = FusedAdam(ps, lr=1e-2, betas=(0.5, 0.999), eps=1e-8)
+    m = [torch.zeros_like(p) for p in refs]
+    v = [torch.zeros_like(p) for p in refs]
+    for step in range(1, 4):
+        grads = [torch.randn_like(p) for p in ps]
+        for p, g in zip(ps, grads):
+            p.grad = g.clone()
+        opt.step()
+        _reference_adam(refs, grads, m, v, 1e-2, 0.5, 0.999, 1e-8, step, 0.0, False)
+    for p, r in zip(ps, refs):
+        assert torch.allclose(p.detach(), r, atol=1e-6, rtol=1e-5)
+    # EMA with spectral-norm absorption
+    ws = [torch.randn(8, 3, 3, 3, device='cuda'), torch.randn(16, 40, device='cuda')]
+    us = [torch.nn.functional.normalize(torch.randn(w.shape[0], device='cuda'), dim=0) for w in ws]
+    vs = [torch.nn.functional.normalize(torch.randn(w[0].numel(), device='cuda'), dim=0)
+          for w in ws]
+    sig = _ext.ext().mt_sn_sigma(ws, us, vs)
+    ref_sig = torch.stack([torch.dot(u, w.reshape(w.shape[0], -1) @ vv)
+                           for w, u, vv in zip(ws, us, vs)])
+    assert torch.allclose(sig, ref_sig, atol=1e-4, rtol=1e-4)
+    ts = [torch.randn_like(w) for w in ws]
+    ts_ref = [t.clone() for t in ts]
+    _ext.ext().mt_ema(ts, ws, 0.9, sig)
+    for t, tr, w, s in zip(ts, ts_ref, ws, ref_sig):
+        assert torch.allclose(t, 0.9 * tr + 0.1 * w / s, atol=1e-5, rtol=1e-5)

@@ -1,0 +1,84 @@
+"""Training entry point (reference train.py:1-93).
+
+    python train.py --config configs/bench/spade_256x512_synthetic.yaml [--logdir D]
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 train.py --config ...
+
+One process per GPU; RCCL (``nccl``) process group on GPU, gloo on CPU hosts.
+"""
+import argparse
+import faulthandler
+import os
+import sys
+
+import torch
+
+faulthandler.enable()
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from imaginaire_amd.config import Config  # noqa: E402
+from imaginaire_amd.utils.cudnn import init_cudnn  # noqa: E402
+from imaginaire_amd.utils.dataset import get_train_and_val_dataloader  # noqa: E402
+from imaginaire_amd.utils.distributed import init_dist, get_world_size  # noqa: E402
+from imaginaire_amd.utils.distributed import master_only_print as print  # noqa: E402
+from imaginaire_amd.utils.logging import init_logging, make_logging_dir  # noqa: E402
+from imaginaire_amd.utils.trainer import (get_model_optimizer_and_scheduler, get_trainer,  # noqa
+                                          set_random_seed)
+
+
+def parse_args():
+    parser = argparse.ArgumentParser(description='Training')
+    parser.add_argument('--config', required=True, help='Path to the training config file.')
+    parser.add_argument('--logdir', help='Dir for saving logs and models.')
+    parser.add_argument('--checkpoint', default='', help='Checkpoint path.')
+    parser.add_argument('--seed', type=int, default=2, help='Random seed.')
+    parser.add_argument('--local_rank', '--local-rank', type=int,
+                        default=int(os.environ.get('LOCAL_RANK', 0)))
+    parser.add_argument('--single_gpu', action='store_true')
+    parser.add_argument('--num_workers', type=int)
+    parser.add_argument('--backend', default=None, help='nccl (RCCL) / gloo; default auto')
+    return parser.parse_args()
+
+
+def main():
+    args = parse_args()
+    set_random_seed(args.seed, by_rank=True)
+    cfg = Config(args.config)
+    if not args.single_gpu and int(os.environ.get('WORLD_SIZE', '1')) > 1:
+        cfg.local_rank = args.local_rank
+        init_dist(cfg.local_rank, backend=args.backend)
+    elif torch.cuda.is_available():
+        torch.cuda.set_device(args.local_rank)
+    if args.num_workers is not None:
+        cfg.data.num_workers = args.num_workers
+    cfg.date_uid, cfg.logdir = init_logging(args.config, args.logdir)
+    make_logging_dir(cfg.logdir)
+    init_cudnn(cfg.cudnn.deterministic, cfg.cudnn.benchmark)
+    train_data_loader, val_data_loader = get_train_and_val_dataloader(cfg, seed=args.seed)
+    net_G, net_D, opt_G, opt_D, sch_G, sch_D = get_model_optimizer_and_scheduler(cfg,
+                                                                                seed=args.seed)
+    trainer = get_trainer(cfg, net_G, net_D, opt_G, opt_D, sch_G, sch_D, train_data_loader,
+                          val_data_loader)
+    current_epoch, current_iteration = trainer.load_checkpoint(cfg, args.checkpoint)
+    for epoch in range(current_epoch, cfg.max_epoch):
+        print('Epoch {} ...'.format(epoch))
+        if hasattr(train_data_loader.sampler, 'set_epoch'):
+            train_data_loader.sampler.set_epoch(current_epoch)
+        trainer.start_of_epoch(current_epoch)
+        for it, data in enumerate(train_data_loader):
+            data = trainer.start_of_iteration(data, current_iteration)
+            for _ in range(cfg.trainer.dis_step):
+                trainer.dis_update(data)
+            for _ in range(cfg.trainer.gen_step):
+                trainer.gen_update(data)
+            current_iteration += 1
+            trainer.end_of_iteration(data, current_epoch, current_iteration)
+            if current_iteration >= cfg.max_iter:
+                print('Done with training!!!')
+                return
+        current_epoch += 1
+        trainer.end_of_epoch(data, current_epoch, current_iteration)
+    print('Done with training!!!')
+
+
+if __name__ == "__main__":
+    main()
