@@ -681,7 +681,9 @@ std::vector<at::Tensor> norm_bwd_reduce(const at::Tensor& x, const at::Tensor& d
   // broadcast modulation (per-(n,c) gamma/beta): pixel stride 0
   const bool bcast = mod && gm.sp == 0 && bt.sp == 0 && g.HW > 1;
   IAMD_CHECK(!mod || bcast || (dgm.ptr != nullptr && dbt.ptr != nullptr),
-             "norm_bwd_reduce: spatial modulation needs dgamma/dbeta outputs");
+             "norm_bwd_reduce: spatial modulation needs dgamma/dbeta outputs (gamma strides n/c/p=",
+             gm.sn, "/", gm.sc, "/", gm.sp, " beta p=", bt.sp, " HW=", g.HW, " dg=",
+             dgm.ptr != nullptr, " db=", dbt.ptr != nullptr, ")");
   const int vec = pick_vec(g, x.element_size(), {gm, bt, dgm, dbt});
   int P, chunk, tpr, nzc;
   reduce_plan(g, vec, P, chunk, tpr, nzc);

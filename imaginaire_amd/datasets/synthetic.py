@@ -35,10 +35,13 @@ def _input_types(cfg_data):
     return out
 
 
-def _crop_hw(cfg_data, is_inference=False):
-    split = getattr(cfg_data, 'val' if is_inference else 'train', None)
-    if split is None:
-        split = cfg_data.train
+def _crop_hw(cfg_data, is_inference=False, is_test=False):
+    names = ['test'] if is_test else (['val', 'train'] if is_inference else ['train'])
+    split = None
+    for n in names + ['train', 'val', 'test']:
+        split = getattr(cfg_data, n, None)
+        if split is not None:
+            break
     aug = getattr(split, 'augmentations', None)
     try:
         return get_crop_h_w(aug)
@@ -84,7 +87,7 @@ class Dataset(torch.utils.data.Dataset):
         self.is_inference = is_inference
         self.is_test = is_test
         self.types = _input_types(self.cfg_data)
-        self.h, self.w = _crop_hw(self.cfg_data, is_inference)
+        self.h, self.w = _crop_hw(self.cfg_data, is_inference, is_test)
         syn = getattr(self.cfg_data, 'synthetic', None)
         self.length = int(getattr(syn, 'num_samples', 64)) if syn is not None else 64
         self.seq_len = int(getattr(syn, 'sequence_length', 0)) if syn is not None else 0

@@ -54,10 +54,14 @@ def _update_running(running_mean, running_var, mean, var, count, factor):
 
 
 def _expand_mod(t, x):
+    """[N, C] → stride-0 [N, C, H, W] view (dtype converted BEFORE expanding so
+    the pixel stride stays 0 and the kernel sees a broadcast modulation)."""
     if t is None:
         return None
+    if t.dtype != x.dtype:
+        t = t.to(x.dtype)
     if t.dim() == 2:
-        return t[:, :, None, None].expand(-1, -1, x.shape[2], x.shape[3])
+        return t.contiguous()[:, :, None, None].expand(-1, -1, x.shape[2], x.shape[3])
     return t
 
 
@@ -85,8 +89,6 @@ class _FusedNormActFn(torch.autograd.Function):
             gamma_v, beta_v = gb[:, :C], gb[:, C:]
         else:
             gamma_v, beta_v = _expand_mod(gamma, x), _expand_mod(beta, x)
-            if gamma_v is not None and gamma_v.dtype != x.dtype:
-                gamma_v, beta_v = gamma_v.to(x.dtype), beta_v.to(x.dtype)
         wf = weight.float() if weight is not None else None
         bf = bias.float() if bias is not None else None
         per_instance = cfg.mode == 'instance'
@@ -148,12 +150,10 @@ class _FusedNormActFn(torch.autograd.Function):
             dgam_v, dbet_v = dgb[:, :C], dgb[:, C:]
         elif ctx.has_mod:
             gamma_v, beta_v = _expand_mod(gamma, x), _expand_mod(beta, x)
-            if gamma_v.dtype != x.dtype:
-                gamma_v, beta_v = gamma_v.to(x.dtype), beta_v.to(x.dtype)
             if ctx.mod_bcast:
                 dgam_v = dbet_v = None
             else:
-                dgam_v = torch.empty_like(gamma_v, memory_format=fmt) if gamma_v.dtype == x.dtype else None
+                dgam_v = torch.empty_like(gamma_v, memory_format=fmt)
                 dbet_v = torch.empty_like(beta_v, memory_format=fmt)
         else:
             gamma_v = beta_v = dgam_v = dbet_v = None
@@ -164,7 +164,8 @@ class _FusedNormActFn(torch.autograd.Function):
             dgamma = sums[2].to(ctx.mod_dtypes[0])
             dbeta = sums[3].to(ctx.mod_dtypes[1])
         elif ctx.has_mod and not ctx.has_gb:
-            dgamma, dbeta = dgam_v, dbet_v
+            dgamma = dgam_v.to(ctx.mod_dtypes[0])
+            dbeta = dbet_v.to(ctx.mod_dtypes[1])
         N, HW = x.shape[0], x.shape[2] * x.shape[3]
         dweight = S2.sum(0).to(weight.dtype) if weight is not None and ctx.needs_input_grad[1] else None
         dbias = S1.sum(0).to(weight.dtype if weight is not None else torch.float32) \
@@ -254,6 +255,10 @@ class _SyncStats(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dn, dmean_g, dvar_g):
         cnt, mean_l, var_l, n, mean_g = ctx.local
+        # the global statistics feed every rank's loss: sum their gradients
+        g = torch.stack([dmean_g.reshape(-1), dvar_g.reshape(-1)], 0).contiguous()
+        dist.all_reduce(g, group=ctx.group)
+        dmean_g, dvar_g = g[0].reshape(dmean_g.shape), g[1].reshape(dvar_g.shape)
         # d mean_g / d mean_l = cnt/n ; d var_g / d var_l = cnt/n ;
         # d var_g / d mean_l = 2 cnt (mean_l - mean_g) / n
         w = cnt / n

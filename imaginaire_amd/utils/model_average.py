@@ -28,6 +28,16 @@ def calibrate_batch_norm_momentum(m):
         m.momentum = 1.0 / float(m.num_batches_tracked + 1)
 
 
+def _drop_sn_load_hooks(m):
+    """``remove_spectral_norm`` leaves SN's load-state-dict pre-hook behind on
+    this PyTorch version, which then demands ``weight_orig`` keys; drop it."""
+    from torch.nn.utils.spectral_norm import SpectralNormLoadStateDictPreHook
+    for k, h in list(m._load_state_dict_pre_hooks.items()):
+        inner = getattr(h, 'hook', h)
+        if isinstance(inner, SpectralNormLoadStateDictPreHook):
+            del m._load_state_dict_pre_hooks[k]
+
+
 class ModelAverage(nn.Module):
     def __init__(self, module, beta=0.9999, start_iteration=1000, remove_sn=True):
         super().__init__()
@@ -44,6 +54,7 @@ class ModelAverage(nn.Module):
             def fn_remove_sn(m):
                 if hasattr(m, 'weight_orig'):
                     remove_spectral_norm(m)
+                    _drop_sn_load_hooks(m)
             self.averaged_model.apply(fn_remove_sn)
             self.dim = 0
         else:
@@ -60,6 +71,7 @@ class ModelAverage(nn.Module):
         tgt = self.averaged_model.state_dict(keep_vars=True)
         sn_t, sn_w, sn_u, sn_v = [], [], [], []
         plain = {}  # dtype -> (targets, sources)
+        ints_t, ints_s = [], []
         for key, t in tgt.items():
             if self.remove_sn and key.endswith('weight') and key + '_orig' in src:
                 sn_t.append(t.data)
@@ -69,11 +81,14 @@ class ModelAverage(nn.Module):
             else:
                 s = src[key]
                 if not t.is_floating_point():
+                    ints_t.append(t.data)
+                    ints_s.append(s.data)
                     continue
                 plain.setdefault(t.dtype, ([], []))
                 plain[t.dtype][0].append(t.data)
                 plain[t.dtype][1].append(s.data)
         self._plan = (sn_t, sn_w, sn_u, sn_v, plain)
+        self._ints = (ints_t, ints_s)
 
     @torch.no_grad()
     def update_average(self):
@@ -116,10 +131,8 @@ class ModelAverage(nn.Module):
                 else:
                     torch._foreach_lerp_(ts, ss, 1 - beta)
         # integer buffers (num_batches_tracked) are copied verbatim
-        src = self.module.state_dict()
-        for key, t in self.averaged_model.state_dict().items():
-            if not t.is_floating_point() and key in src:
-                t.copy_(src[key])
+        if self._ints[0]:
+            torch._foreach_copy_(self._ints[0], self._ints[1])
 
     def copy_t2s(self):
         target_dict = self.module.state_dict()

@@ -13,7 +13,7 @@ def _ref_norm(x, mode, w, b, gamma, beta, slope, eps=1e-5):
     elif mode == 'instance':
         y = F.instance_norm(xf, weight=w, bias=b, eps=eps)
     else:
-        y = xf
+        y = xf * w.view(1, -1, 1, 1) + b.view(1, -1, 1, 1)
     if gamma is not None:
         g, bb = gamma.float(), beta.float()
         if g.dim() == 2:
