@@ -96,6 +96,7 @@ class Dataset(torch.utils.data.Dataset):
         self.input_image = list(getattr(self.cfg_data, 'input_image', ['images']))
         self.num_classes = getattr(self.cfg_data, 'num_classes', 0)
         self.sample_class_idx = None
+        self.num_style_classes = int(getattr(self.cfg_data, 'num_style_classes', 0) or 0) or 1
 
     def __len__(self):
         return self.length
@@ -123,7 +124,7 @@ class Dataset(torch.utils.data.Dataset):
         for name, t in self.types.items():
             nc = t.num_channels
             interp = getattr(t, 'interpolator', 'BILINEAR')
-            if name in self.input_image or (not self.input_labels and name == 'images'):
+            if name in self.input_image or name.startswith('images'):
                 out[name] = smooth_field(nc, h, w, gen).clamp(-1, 1)
             elif interp == 'NEAREST' and nc > 1:
                 seg = voronoi_labels(h, w, nc, gen)
@@ -131,6 +132,11 @@ class Dataset(torch.utils.data.Dataset):
                 if getattr(t, 'use_dont_care', False):
                     onehot = torch.cat([onehot, torch.zeros(1, h, w)], 0)
                 out[name] = onehot
+            elif 'instance' in name:
+                # integer instance ids (cityscapes-style: class*1000 + k)
+                inst = voronoi_labels(h, w, 8, gen, num_sites=12)
+                base = seg if seg is not None else torch.zeros_like(inst)
+                out[name] = (base * 1000 + inst).float()[None]
             else:
                 if seg is not None and nc == 1:
                     out[name] = edge_map(seg)[None]
@@ -151,17 +157,26 @@ class Dataset(torch.utils.data.Dataset):
             data['label'] = torch.cat(labels, dim=-3)
         for n in self.input_image:
             if n in sample:
-                data['images'] = sample[n]
+                data['images' if n == 'images' or len(self.input_image) == 1 else n] = sample[n]
         for n, v in sample.items():
             if n not in self.input_labels and n not in self.input_image:
                 data[n] = v
-        if not self.paired and 'images' in data:
+        if not self.paired and 'images' in data and 'images_b' not in data:
             data['images_a'] = data['images']
             gen_b = torch.Generator().manual_seed(98765 + int(index))
             data['images_b'] = smooth_field(data['images'].shape[-3], self.h, self.w,
                                             gen_b).clamp(-1, 1)
         if self.num_classes:
             data['labels'] = torch.tensor(index % self.num_classes)
+        if 'images_content' in data and 'images_style' in data:
+            # few-shot unpaired contract (reference unpaired_few_shot_images.py):
+            # integer class ids of the content and style images.
+            ncls = max(1, int(getattr(self.cfg_data, 'num_style_classes', 0) or
+                              getattr(getattr(self.cfg, 'dis', None), 'num_classes', 1) or 1))
+            style_cls = self.sample_class_idx if self.sample_class_idx is not None else \
+                (index * 7 + 3) % ncls
+            data['labels_content'] = torch.tensor(index % ncls)
+            data['labels_style'] = torch.tensor(style_cls % ncls)
         data['key'] = {k: ['synthetic/%06d' % index] for k in self.types}
         data['original_h_w'] = torch.tensor([self.h, self.w])
         data['is_flipped'] = False

@@ -1,0 +1,34 @@
+"""UNIT discriminator: weight-shared multi-res patch (or residual) D per domain
+(reference discriminators/unit.py:12-99)."""
+from torch import nn
+
+from imaginaire_amd.discriminators.multires_patch import WeightSharedMultiResPatchDiscriminator
+from imaginaire_amd.discriminators.residual import ResDiscriminator
+from imaginaire_amd.discriminators.munit import _kw
+
+
+class Discriminator(nn.Module):
+    def __init__(self, dis_cfg, data_cfg):
+        super().__init__()
+        if getattr(dis_cfg, 'patch_dis', True):
+            kw = _kw(dis_cfg)
+            kw.pop('patch_dis', None)
+            self.discriminator_a = WeightSharedMultiResPatchDiscriminator(**kw)
+            self.discriminator_b = WeightSharedMultiResPatchDiscriminator(**kw)
+        else:
+            self.discriminator_a = ResDiscriminator(**_kw(dis_cfg))
+            self.discriminator_b = ResDiscriminator(**_kw(dis_cfg))
+
+    def forward(self, data, net_G_output, gan_recon=False, real=True):
+        out_ab, fea_ab, _ = self.discriminator_b(net_G_output['images_ab'])
+        out_ba, fea_ba, _ = self.discriminator_a(net_G_output['images_ba'])
+        output = dict(out_ba=out_ba, out_ab=out_ab, fea_ba=fea_ba, fea_ab=fea_ab)
+        if real:
+            out_a, fea_a, _ = self.discriminator_a(data['images_a'])
+            out_b, fea_b, _ = self.discriminator_b(data['images_b'])
+            output.update(dict(out_a=out_a, out_b=out_b, fea_a=fea_a, fea_b=fea_b))
+        if gan_recon:
+            out_aa, fea_aa, _ = self.discriminator_a(net_G_output['images_aa'])
+            out_bb, fea_bb, _ = self.discriminator_b(net_G_output['images_bb'])
+            output.update(dict(out_aa=out_aa, out_bb=out_bb, fea_aa=fea_aa, fea_bb=fea_bb))
+        return output

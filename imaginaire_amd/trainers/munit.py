@@ -1,0 +1,185 @@
+"""MUNIT trainer (reference trainers/munit.py:16-307).
+
+GAN (optionally on reconstructions) + image / style / content / cycle
+reconstruction + KL + (instance-normalised) perceptual; D: GAN, WGAN-GP
+gradient penalty (implemented here — the reference references it but never
+creates the criterion) and consistency regularisation (flip + random shift).
+"""
+import torch
+
+from imaginaire_amd.evaluation import compute_fid
+from imaginaire_amd.losses import GANLoss, GaussianKLLoss, PerceptualLoss
+from imaginaire_amd.losses.gp import GradientPenaltyLoss
+from imaginaire_amd.trainers.base import BaseTrainer
+from imaginaire_amd.utils.distributed import master_only_print as print
+from imaginaire_amd.utils.meters import Meter
+from imaginaire_amd.utils.misc import random_shift
+
+
+def _weights_from(cfg_loss_weight):
+    items = cfg_loss_weight.items() if isinstance(cfg_loss_weight, dict) else \
+        vars(cfg_loss_weight).items()
+    return {k: v for k, v in items if v > 0}
+
+
+class Trainer(BaseTrainer):
+    def __init__(self, cfg, net_G, net_D, opt_G, opt_D, sch_G, sch_D, train_data_loader,
+                 val_data_loader):
+        super().__init__(cfg, net_G, net_D, opt_G, opt_D, sch_G, sch_D, train_data_loader,
+                         val_data_loader)
+        self.gan_recon = getattr(cfg.trainer, 'gan_recon', False)
+        self.best_fid_a = None
+        self.best_fid_b = None
+
+    def _init_tensorboard(self):
+        self.meters = {}
+        for name in ['optim/gen_lr', 'optim/dis_lr', 'time/iteration', 'time/epoch']:
+            self.meters[name] = Meter(name)
+        self.metric_meters = {}
+        for name in ['FID_a', 'best_FID_a', 'FID_b', 'best_FID_b']:
+            self.metric_meters[name] = Meter(name)
+        self.image_meter = Meter('images')
+
+    def _init_loss(self, cfg):
+        self.criteria['gan'] = GANLoss(cfg.trainer.gan_mode)
+        self.criteria['kl'] = GaussianKLLoss()
+        self.criteria['image_recon'] = torch.nn.L1Loss()
+        self.criteria['content_recon'] = torch.nn.L1Loss()
+        self.criteria['style_recon'] = torch.nn.L1Loss()
+        if getattr(cfg.trainer.loss_weight, 'perceptual', 0) > 0:
+            self.criteria['perceptual'] = PerceptualLoss(
+                cfg=cfg, network=cfg.trainer.perceptual_mode,
+                layers=cfg.trainer.perceptual_layers, instance_normalized=True)
+        if getattr(cfg.trainer.loss_weight, 'gp', 0) > 0:
+            self.criteria['gp'] = GradientPenaltyLoss()
+        self.weights.update(_weights_from(cfg.trainer.loss_weight))
+
+    def gen_forward(self, data):
+        cycle_recon = 'cycle_recon' in self.weights
+        image_recon = 'image_recon' in self.weights
+        perceptual = 'perceptual' in self.weights
+        out = self.net_G(data, image_recon=image_recon, cycle_recon=cycle_recon,
+                         within_latent_recon=False)
+        dout = self.net_D(data, out, real=False, gan_recon=self.gan_recon)
+        self._time_before_loss()
+        gan = self.criteria['gan']
+        if self.gan_recon:
+            self.gen_losses['gan_a'] = 0.5 * (gan(dout['out_ba'], True, dis_update=False) +
+                                              gan(dout['out_aa'], True, dis_update=False))
+            self.gen_losses['gan_b'] = 0.5 * (gan(dout['out_ab'], True, dis_update=False) +
+                                              gan(dout['out_bb'], True, dis_update=False))
+        else:
+            self.gen_losses['gan_a'] = gan(dout['out_ba'], True, dis_update=False)
+            self.gen_losses['gan_b'] = gan(dout['out_ab'], True, dis_update=False)
+        self.gen_losses['gan'] = self.gen_losses['gan_a'] + self.gen_losses['gan_b']
+        if perceptual:
+            self.gen_losses['perceptual_a'] = self.criteria['perceptual'](out['images_ab'],
+                                                                          data['images_a'])
+            self.gen_losses['perceptual_b'] = self.criteria['perceptual'](out['images_ba'],
+                                                                          data['images_b'])
+            self.gen_losses['perceptual'] = self.gen_losses['perceptual_a'] + \
+                self.gen_losses['perceptual_b']
+        if image_recon:
+            self.gen_losses['image_recon'] = \
+                self.criteria['image_recon'](out['images_aa'], data['images_a']) + \
+                self.criteria['image_recon'](out['images_bb'], data['images_b'])
+        self.gen_losses['style_recon_a'] = self.criteria['style_recon'](out['style_ba'],
+                                                                        out['style_a_rand'])
+        self.gen_losses['style_recon_b'] = self.criteria['style_recon'](out['style_ab'],
+                                                                        out['style_b_rand'])
+        self.gen_losses['style_recon'] = self.gen_losses['style_recon_a'] + \
+            self.gen_losses['style_recon_b']
+        self.gen_losses['content_recon_a'] = self.criteria['content_recon'](
+            out['content_ab'], out['content_a'].detach())
+        self.gen_losses['content_recon_b'] = self.criteria['content_recon'](
+            out['content_ba'], out['content_b'].detach())
+        self.gen_losses['content_recon'] = self.gen_losses['content_recon_a'] + \
+            self.gen_losses['content_recon_b']
+        self.gen_losses['kl'] = self.criteria['kl'](out['style_a']) + \
+            self.criteria['kl'](out['style_b'])
+        if cycle_recon:
+            self.gen_losses['cycle_recon'] = \
+                self.criteria['image_recon'](out['images_aba'], data['images_a']) + \
+                self.criteria['image_recon'](out['images_bab'], data['images_b'])
+        return self._get_total_loss(gen_forward=True)
+
+    def dis_forward(self, data):
+        with torch.no_grad():
+            out = self.net_G(data, image_recon=self.gan_recon, latent_recon=False,
+                             cycle_recon=False, within_latent_recon=False)
+        out['images_ba'].requires_grad = True
+        out['images_ab'].requires_grad = True
+        dout = self.net_D(data, out, gan_recon=self.gan_recon)
+        self._time_before_loss()
+        gan = self.criteria['gan']
+        self.dis_losses['gan_a'] = gan(dout['out_a'], True) + gan(dout['out_ba'], False)
+        self.dis_losses['gan_b'] = gan(dout['out_b'], True) + gan(dout['out_ab'], False)
+        self.dis_losses['gan'] = self.dis_losses['gan_a'] + self.dis_losses['gan_b']
+        if 'gp' in self.weights:
+            gp = self.criteria['gp']
+            images_a_gp = gp.get_dis_inputs(data['images_a'], out['images_ba'])
+            images_b_gp = gp.get_dis_inputs(data['images_b'], out['images_ab'])
+            dout_gp = self.net_D(data, dict(images_ab=images_b_gp, images_ba=images_a_gp),
+                                 real=False)
+            self.dis_losses['gp_a'] = gp(images_a_gp, dout_gp['out_ba'])
+            self.dis_losses['gp_b'] = gp(images_b_gp, dout_gp['out_ab'])
+            self.dis_losses['gp'] = self.dis_losses['gp_a'] + self.dis_losses['gp_b']
+        self.dis_losses['consistency_reg'] = torch.zeros((), device=self.device)
+        if 'consistency_reg' in self.weights:
+            data_aug = {'images_a': random_shift(data['images_a'].flip(-1)),
+                        'images_b': random_shift(data['images_b'].flip(-1))}
+            out_aug = {'images_ab': random_shift(out['images_ab'].flip(-1)),
+                       'images_ba': random_shift(out['images_ba'].flip(-1))}
+            dout_aug = self.net_D(data_aug, out_aug)
+            for name in ['fea_ba', 'fea_ab', 'fea_a', 'fea_b']:
+                a, b = dout_aug[name], dout[name]
+                if isinstance(a, list):
+                    for x, y in zip(a, b):
+                        xs = x if isinstance(x, list) else [x]
+                        ys = y if isinstance(y, list) else [y]
+                        for xx, yy in zip(xs, ys):
+                            self.dis_losses['consistency_reg'] = \
+                                self.dis_losses['consistency_reg'] + \
+                                torch.pow(xx.float() - yy.float(), 2).mean()
+                else:
+                    self.dis_losses['consistency_reg'] = self.dis_losses['consistency_reg'] + \
+                        torch.pow(a.float() - b.float(), 2).mean()
+        return self._get_total_loss(gen_forward=False)
+
+    def _get_visualizations(self, data):
+        net = self.net_G.module.averaged_model if self.cfg.trainer.model_average else self.net_G
+        with torch.no_grad(), self.autocast():
+            out = net(data, random_style=False)
+            out_r = net(data)
+            return [data['images_a'], data['images_b'], out['images_aa'], out['images_bb'],
+                    out['images_ab'], out_r['images_ab'], out['images_ba'], out_r['images_ba'],
+                    out['images_aba'], out['images_bab']]
+
+    def write_metrics(self):
+        res = self._compute_fid()
+        if res is None:
+            return
+        cur_fid_a, cur_fid_b = res
+        self.best_fid_a = cur_fid_a if self.best_fid_a is None else min(self.best_fid_a,
+                                                                         cur_fid_a)
+        self.best_fid_b = cur_fid_b if self.best_fid_b is None else min(self.best_fid_b,
+                                                                         cur_fid_b)
+        self._write_to_meters({'FID_a': cur_fid_a, 'best_FID_a': self.best_fid_a,
+                               'FID_b': cur_fid_b, 'best_FID_b': self.best_fid_b},
+                              self.metric_meters)
+        self._flush_meters(self.metric_meters)
+
+    def _compute_fid(self):
+        if self.val_data_loader is None:
+            return None
+        self.net_G.eval()
+        net = self.net_G.module.averaged_model if self.cfg.trainer.model_average else self.net_G
+        with self.autocast():
+            fid_a = compute_fid(self._get_save_path('fid_a', 'npy'), self.val_data_loader, net,
+                                'images_a', 'images_ba')
+            fid_b = compute_fid(self._get_save_path('fid_b', 'npy'), self.val_data_loader, net,
+                                'images_b', 'images_ab')
+        print('Epoch {:05}, Iteration {:09}, FID a {}, FID b {}'.format(
+            self.current_epoch, self.current_iteration, fid_a, fid_b))
+        self.net_G.train()
+        return fid_a, fid_b

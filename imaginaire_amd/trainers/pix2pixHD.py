@@ -1,0 +1,104 @@
+"""pix2pixHD trainer (reference trainers/pix2pixHD.py:17-203): GAN + FM +
+perceptual; instance map → edge map pre-processing; feature clustering before
+every checkpoint when the instance encoder is enabled."""
+import functools
+
+import torch
+
+from imaginaire_amd.evaluation import compute_fid
+from imaginaire_amd.losses import FeatureMatchingLoss, GANLoss, PerceptualLoss
+from imaginaire_amd.model_utils.pix2pixHD import cluster_features, get_edges
+from imaginaire_amd.trainers.spade import Trainer as SPADETrainer
+from imaginaire_amd.utils.distributed import master_only_print as print
+
+
+class Trainer(SPADETrainer):
+    def _assign_criteria(self, name, criterion, weight):
+        self.criteria[name] = criterion
+        self.weights[name] = weight
+
+    def _init_loss(self, cfg):
+        loss_weight = cfg.trainer.loss_weight
+        self._assign_criteria('GAN', GANLoss(cfg.trainer.gan_mode), loss_weight.gan)
+        self._assign_criteria('FeatureMatching', FeatureMatchingLoss(),
+                              loss_weight.feature_matching)
+        if hasattr(cfg.trainer, 'perceptual_loss'):
+            self._assign_criteria('Perceptual', PerceptualLoss(
+                cfg=cfg, network=cfg.trainer.perceptual_loss.mode,
+                layers=cfg.trainer.perceptual_loss.layers,
+                weights=cfg.trainer.perceptual_loss.weights), loss_weight.perceptual)
+
+    def _start_of_iteration(self, data, current_iteration):
+        return self.pre_process(data)
+
+    def gen_forward(self, data):
+        net_G_output = self.net_G(data)
+        net_D_output = self.net_D(data, net_G_output)
+        self._time_before_loss()
+        output_fake = self._get_outputs(net_D_output, real=False)
+        self.gen_losses['GAN'] = self.criteria['GAN'](output_fake, True, dis_update=False)
+        self.gen_losses['FeatureMatching'] = self.criteria['FeatureMatching'](
+            net_D_output['fake_features'], net_D_output['real_features'])
+        if 'Perceptual' in self.criteria:
+            self.gen_losses['Perceptual'] = self.criteria['Perceptual'](
+                net_G_output['fake_images'], data['images'])
+        total_loss = torch.zeros((), device=self.device)
+        for key in self.criteria:
+            total_loss = total_loss + self.gen_losses[key] * self.weights[key]
+        self.gen_losses['total'] = total_loss
+        return total_loss
+
+    def dis_forward(self, data):
+        with torch.no_grad():
+            net_G_output = self.net_G(data)
+            net_G_output['fake_images'] = net_G_output['fake_images'].detach()
+        net_D_output = self.net_D(data, net_G_output)
+        self._time_before_loss()
+        output_fake = self._get_outputs(net_D_output, real=False)
+        output_real = self._get_outputs(net_D_output, real=True)
+        fake_loss = self.criteria['GAN'](output_fake, False, dis_update=True)
+        true_loss = self.criteria['GAN'](output_real, True, dis_update=True)
+        self.dis_losses['GAN'] = fake_loss + true_loss
+        total_loss = self.dis_losses['GAN'] * self.weights['GAN']
+        self.dis_losses['total'] = total_loss
+        return total_loss
+
+    def pre_process(self, data):
+        data = self.to_device(data)
+        net_G = self.net_G.module.module if self.cfg.trainer.model_average else \
+            self.net_G.module
+        if net_G.contain_instance_map:
+            inst_maps = data['label'][:, -1:]
+            edge_maps = get_edges(inst_maps)
+            data['instance_maps'] = inst_maps.clone()
+            label = data['label'].clone()
+            label[:, -1:] = edge_maps
+            data['label'] = label
+        return data
+
+    def _pre_save_checkpoint(self):
+        if hasattr(self.cfg.gen, 'enc') and self.val_data_loader is not None:
+            net_E = self.net_G.module.averaged_model.encoder if self.cfg.trainer.model_average \
+                else self.net_G.module.encoder
+            is_cityscapes = getattr(self.cfg.gen, 'is_cityscapes', False)
+            cluster_features(self.cfg, self.val_data_loader, net_E, self.pre_process,
+                             is_cityscapes)
+
+    def _compute_fid(self):
+        if self.val_data_loader is None:
+            return None
+        self.net_G.eval()
+        net_G_for_evaluation = functools.partial(self.net_G, random_style=True)
+        regular_fid_path = self._get_save_path('regular_fid', 'npy')
+        regular_fid_value = compute_fid(regular_fid_path, self.val_data_loader,
+                                        net_G_for_evaluation, preprocess=self.pre_process)
+        print('Epoch {:05}, Iteration {:09}, Regular FID {}'.format(
+            self.current_epoch, self.current_iteration, regular_fid_value))
+        if self.cfg.trainer.model_average:
+            avg = functools.partial(self.net_G.module.averaged_model, random_style=True)
+            fid_value = compute_fid(self._get_save_path('average_fid', 'npy'),
+                                    self.val_data_loader, avg, preprocess=self.pre_process)
+            self.net_G.train()
+            return regular_fid_value, fid_value
+        self.net_G.train()
+        return regular_fid_value

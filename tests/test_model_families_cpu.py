@@ -1,0 +1,33 @@
+"""One D+G training iteration of every image model family on CPU (synthetic
+data; mirrors the reference's tests/test_training.py / scripts/test_training.sh
+loop over configs/unit_test/*.yaml)."""
+import os
+
+import pytest
+import torch
+
+from imaginaire_amd.config import Config
+from imaginaire_amd.utils.dataset import get_train_and_val_dataloader
+from imaginaire_amd.utils.trainer import get_model_optimizer_and_scheduler, get_trainer
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FAMILIES = ['spade', 'pix2pixHD', 'munit', 'unit', 'funit', 'coco_funit']
+
+
+@pytest.mark.parametrize('name', FAMILIES)
+def test_family_one_iteration(tmp_path, name):
+    torch.manual_seed(0)
+    cfg = Config(os.path.join(ROOT, 'configs', 'unit_test', name + '.yaml'))
+    cfg.logdir = str(tmp_path)
+    train_loader, val_loader = get_train_and_val_dataloader(cfg)
+    nets = get_model_optimizer_and_scheduler(cfg, seed=0)
+    trainer = get_trainer(cfg, *nets, train_loader, val_loader)
+    data = trainer.start_of_iteration(next(iter(train_loader)), 0)
+    before = [p.detach().clone() for p in trainer.net_G_module.parameters()]
+    trainer.dis_update(data)
+    trainer.gen_update(data)
+    changed = sum(int(not torch.equal(a, b))
+                  for a, b in zip(before, trainer.net_G_module.parameters()))
+    assert changed > 0
+    for k, v in list(trainer.gen_losses.items()) + list(trainer.dis_losses.items()):
+        assert torch.isfinite(torch.as_tensor(v)).all(), (name, k)
