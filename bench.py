@@ -41,6 +41,7 @@ def parse():
     p.add_argument('--eager', action='store_true',
                    help='self-baseline: PyTorch reference ops instead of the HIP kernels')
     p.add_argument('--profile-phases', action='store_true')
+    p.add_argument('--verbose', action='store_true')
     return p.parse_args()
 
 
@@ -65,7 +66,8 @@ def main():
         init_dist(local_rank, backend='nccl')
     else:
         torch.cuda.set_device(local_rank)
-    torch.backends.cudnn.benchmark = True
+    from imaginaire_amd.utils.cudnn import init_cudnn
+    init_cudnn(False, True)
     device = torch.device('cuda', local_rank)
     cfg = Config(args.config)
     cfg.logdir = os.path.join('/tmp', 'imaginaire_amd_bench')
@@ -99,6 +101,8 @@ def main():
     t0 = time.perf_counter()
     for it in range(args.steps):
         step(args.warmup + it)
+        if rank == 0 and args.verbose:
+            print('[bench] step {} queued'.format(it), flush=True)
     barrier()
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], device=device, dtype=torch.float64)

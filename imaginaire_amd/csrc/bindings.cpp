@@ -44,6 +44,15 @@ void mt_ema(const std::vector<at::Tensor>& targets, const std::vector<at::Tensor
             double beta, const c10::optional<at::Tensor>& sigma);
 void mt_scale(const std::vector<at::Tensor>& xs, const at::Tensor& s);
 at::Tensor mt_sqnorm(const std::vector<at::Tensor>& xs);
+// correlation.hip (k6 correlation, k8 channelnorm)
+at::Tensor correlation_forward(const at::Tensor& input1, const at::Tensor& input2, int64_t pad,
+                               int64_t ks, int64_t md, int64_t s1, int64_t s2);
+std::vector<at::Tensor> correlation_backward(const at::Tensor& input1, const at::Tensor& input2,
+                                             const at::Tensor& grad_out, int64_t pad,
+                                             int64_t ks, int64_t md, int64_t s1, int64_t s2);
+at::Tensor channelnorm_forward(const at::Tensor& x);
+at::Tensor channelnorm_backward(const at::Tensor& x, const at::Tensor& out,
+                                const at::Tensor& grad_out);
 // flow_warp.hip (k9 warp, k7 resample2d)
 at::Tensor flow_warp_fwd(const at::Tensor& img, const at::Tensor& flow);
 std::vector<at::Tensor> flow_warp_bwd(const at::Tensor& img, const at::Tensor& flow,
@@ -71,4 +80,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("flow_warp_bwd", &iamd::flow_warp_bwd, "k9 backward");
   m.def("resample2d_forward", &iamd::resample2d_forward, "FlowNet2 Resample2d (k7)");
   m.def("resample2d_backward", &iamd::resample2d_backward, "k7 backward");
+  m.def("correlation_forward", &iamd::correlation_forward, "FlowNet correlation (k6)");
+  m.def("correlation_backward", &iamd::correlation_backward, "k6 backward");
+  m.def("channelnorm_forward", &iamd::channelnorm_forward, "channel L2 norm (k8)");
+  m.def("channelnorm_backward", &iamd::channelnorm_backward, "k8 backward");
 }

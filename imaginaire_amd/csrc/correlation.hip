@@ -1,0 +1,330 @@
+// k6 FlowNet cost-volume correlation and k8 channel-norm, gfx950.
+//
+// Semantics follow reference third_party/correlation/src/correlation_cuda_kernel.cu:73-334
+// (zero-padded inputs, output channel tc = (tj+R)*(2R+1) + (ti+R), value averaged over
+// kernel_size^2 * C) and third_party/channelnorm/src/channelnorm_kernel.cu:19-96
+// (L2 norm over channels, grad = g*x/(norm+1e-9)).
+//
+// MI355X design:
+//   * Inputs are NHWC (channels-last), the layout every conv in the framework produces,
+//     so a pixel's feature vector is one contiguous, 16-byte-vectorisable run.
+//   * The kernel_size==1 forward (the only configuration FlowNet2 uses: pad 20,
+//     max_disp 20, stride2 2 -> 21x21 = 441 displacements) is LDS-tiled: one workgroup
+//     owns 32 output pixels of one output row and one displacement row tj. It stages the
+//     32 first-image feature vectors and the (31*s1 + 2R*s2 + 1)-wide second-image strip
+//     through LDS in 32-channel chunks (rows padded to 33 floats -> conflict-free), and
+//     each lane accumulates up to 3 displacements for its pixel in fp32 registers.
+//     Every input element is read from HBM once per displacement row instead of once
+//     per displacement (21x fewer global reads than the per-pixel reference kernel).
+//   * Backward is gather-form (one lane per (pixel, channel); displacement loop with
+//     broadcast reads of grad_out) so it needs no atomics and is deterministic.
+//   * Output is written channels-last [N, oH, oW, D*D] so the FlowNetC concat +
+//     conv3_1 that consume it stay NHWC.
+#include "common.h"
+
+namespace iamd {
+namespace {
+
+constexpr int kTX = 32;       // output pixels per workgroup (one row segment)
+constexpr int kCC = 32;       // channel chunk staged through LDS
+constexpr int kLdsPad = kCC + 1;
+constexpr int kCorrThreads = 256;
+constexpr int kMaxDispPerLane = 3;  // ceil(D / (256/32)) for D <= 24
+
+template <typename T>
+__device__ __forceinline__ float ld_pad(const T* __restrict__ x, int n, int y, int xx, int c,
+                                        int H, int W, int C) {
+  if (y < 0 || y >= H || xx < 0 || xx >= W) return 0.f;
+  return to_f<T>(x[(((int64_t)n * H + y) * W + xx) * C + c]);
+}
+
+// Tiled forward for kernel_size == 1. grid = (ceil(oW/32), oH, N*D), block = 256.
+template <typename T>
+__global__ __launch_bounds__(kCorrThreads) void corr_fwd_k1(
+    const T* __restrict__ in1, const T* __restrict__ in2, T* __restrict__ out, int H, int W,
+    int C, int oH, int oW, int pad, int md, int s1, int s2, int R, int D) {
+  __shared__ float sA[kTX * kLdsPad];
+  extern __shared__ float sB[];  // [span][kLdsPad]
+  const int ox0 = blockIdx.x * kTX;
+  const int oy = blockIdx.y;
+  const int n = blockIdx.z / D;
+  const int tjr = blockIdx.z % D;  // tj + R
+  const int tid = threadIdx.x;
+  const int px = tid % kTX;
+  const int grp = tid / kTX;  // 8 groups of 32 lanes
+  const int ngrp = kCorrThreads / kTX;
+  const int span = (kTX - 1) * s1 + 2 * R * s2 + 1;
+  // padded-frame centre of the first output pixel of the tile
+  const int y1 = oy * s1 + md;
+  const int x1_0 = ox0 * s1 + md;
+  const int y2 = y1 + (tjr - R) * s2;
+  const int bx0 = x1_0 - R * s2;  // first second-image column (padded frame)
+
+  float acc[kMaxDispPerLane];
+#pragma unroll
+  for (int k = 0; k < kMaxDispPerLane; ++k) acc[k] = 0.f;
+
+  for (int c0 = 0; c0 < C; c0 += kCC) {
+    const int cc = min(kCC, C - c0);
+    __syncthreads();
+    for (int e = tid; e < kTX * kCC; e += kCorrThreads) {
+      int p = e / kCC, c = e % kCC;
+      float v = 0.f;
+      if (c < cc && ox0 + p < oW)
+        v = ld_pad(in1, n, y1 - pad, x1_0 + p * s1 - pad, c0 + c, H, W, C);
+      sA[p * kLdsPad + c] = v;
+    }
+    for (int e = tid; e < span * kCC; e += kCorrThreads) {
+      int p = e / kCC, c = e % kCC;
+      float v = 0.f;
+      if (c < cc) v = ld_pad(in2, n, y2 - pad, bx0 + p - pad, c0 + c, H, W, C);
+      sB[p * kLdsPad + c] = v;
+    }
+    __syncthreads();
+    for (int c = 0; c < cc; ++c) {
+      const float a = sA[px * kLdsPad + c];
+#pragma unroll
+      for (int k = 0; k < kMaxDispPerLane; ++k) {
+        const int tir = grp + k * ngrp;
+        if (tir < D) acc[k] += a * sB[(px * s1 + tir * s2) * kLdsPad + c];
+      }
+    }
+  }
+  const int ox = ox0 + px;
+  if (ox >= oW) return;
+  const float inv = 1.f / (float)C;
+  T* o = out + (((int64_t)n * oH + oy) * oW + ox) * (D * D);
+#pragma unroll
+  for (int k = 0; k < kMaxDispPerLane; ++k) {
+    const int tir = grp + k * ngrp;
+    if (tir < D) o[tjr * D + tir] = from_f<T>(acc[k] * inv);
+  }
+}
+
+// Generic forward (any kernel_size): one workgroup (one wave) per output pixel.
+template <typename T>
+__global__ __launch_bounds__(kWave) void corr_fwd_generic(
+    const T* __restrict__ in1, const T* __restrict__ in2, T* __restrict__ out, int H, int W,
+    int C, int oH, int oW, int pad, int ks, int md, int s1, int s2, int R, int D) {
+  const int ox = blockIdx.x, oy = blockIdx.y, n = blockIdx.z;
+  const int kr = (ks - 1) / 2;
+  const int y1 = oy * s1 + md, x1 = ox * s1 + md;
+  const float inv = 1.f / (float)(ks * ks * C);
+  T* o = out + (((int64_t)n * oH + oy) * oW + ox) * (D * D);
+  for (int tj = -R; tj <= R; ++tj) {
+    for (int ti = -R; ti <= R; ++ti) {
+      const int y2 = y1 + tj * s2, x2 = x1 + ti * s2;
+      float acc = 0.f;
+      for (int j = -kr; j <= kr; ++j)
+        for (int i = -kr; i <= kr; ++i)
+          for (int c = threadIdx.x; c < C; c += kWave)
+            acc += ld_pad(in1, n, y1 + j - pad, x1 + i - pad, c, H, W, C) *
+                   ld_pad(in2, n, y2 + j - pad, x2 + i - pad, c, H, W, C);
+      acc = wave_sum(acc);
+      if (threadIdx.x == 0) o[(tj + R) * D + (ti + R)] = from_f<T>(acc * inv);
+    }
+  }
+}
+
+// Backward w.r.t. both inputs, gather form. One lane per (n, y, x, c) of the
+// *unpadded* inputs; grad_out is channels-last [N, oH, oW, D*D] fp32.
+template <typename T>
+__global__ __launch_bounds__(256) void corr_bwd(
+    const T* __restrict__ in1, const T* __restrict__ in2, const float* __restrict__ gout,
+    float* __restrict__ g1, float* __restrict__ g2, int N, int H, int W, int C, int oH, int oW,
+    int pad, int ks, int md, int s1, int s2, int R, int D) {
+  const int64_t total = (int64_t)N * H * W * C;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int c = idx % C;
+  int64_t r = idx / C;
+  const int x = r % W;
+  r /= W;
+  const int y = r % H;
+  const int n = r / H;
+  const int kr = (ks - 1) / 2;
+  const int py = y + pad, px = x + pad;  // padded frame
+  const int DD = D * D;
+  const float inv = 1.f / (float)(ks * ks * C);
+  float a1 = 0.f, a2 = 0.f;
+  for (int j = -kr; j <= kr; ++j) {
+    for (int i = -kr; i <= kr; ++i) {
+      // grad_in1: this element is in1 at window offset (j,i) of centre (py-j, px-i)
+      {
+        const int cy = py - j, cx = px - i;
+        const int ty = cy - md, tx = cx - md;
+        if (ty >= 0 && tx >= 0 && ty % s1 == 0 && tx % s1 == 0) {
+          const int oy = ty / s1, ox = tx / s1;
+          if (oy < oH && ox < oW) {
+            const float* go = gout + (((int64_t)n * oH + oy) * oW + ox) * DD;
+            for (int tj = -R; tj <= R; ++tj)
+              for (int ti = -R; ti <= R; ++ti)
+                a1 += go[(tj + R) * D + ti + R] *
+                      ld_pad(in2, n, cy + tj * s2 + j - pad, cx + ti * s2 + i - pad, c, H, W, C);
+          }
+        }
+      }
+      // grad_in2: this element is in2 at window offset (j,i) of displaced centre
+      for (int tj = -R; tj <= R; ++tj) {
+        const int cy = py - tj * s2 - j;
+        const int ty = cy - md;
+        if (ty < 0 || ty % s1 != 0 || ty / s1 >= oH) continue;
+        const int oy = ty / s1;
+        for (int ti = -R; ti <= R; ++ti) {
+          const int cx = px - ti * s2 - i;
+          const int tx = cx - md;
+          if (tx < 0 || tx % s1 != 0 || tx / s1 >= oW) continue;
+          const int ox = tx / s1;
+          a2 += gout[(((int64_t)n * oH + oy) * oW + ox) * DD + (tj + R) * D + ti + R] *
+                ld_pad(in1, n, cy + j - pad, cx + i - pad, c, H, W, C);
+        }
+      }
+    }
+  }
+  g1[idx] = a1 * inv;
+  g2[idx] = a2 * inv;
+}
+
+// ---- k8 channel norm (generic 4-D strides, fp32 accumulate) -------------------
+template <typename T>
+__global__ void chnorm_fwd(const T* __restrict__ x, T* __restrict__ out, int N, int C, int H,
+                           int W, int64_t sn, int64_t sc, int64_t sh, int64_t sw) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)N * H * W) return;
+  const int xx = idx % W;
+  const int y = (idx / W) % H;
+  const int n = idx / ((int64_t)H * W);
+  const T* p = x + n * sn + y * sh + xx * sw;
+  float acc = 0.f;
+  for (int c = 0; c < C; ++c) {
+    float v = to_f<T>(p[c * sc]);
+    acc += v * v;
+  }
+  out[idx] = from_f<T>(sqrtf(acc));
+}
+
+template <typename T>
+__global__ void chnorm_bwd(const T* __restrict__ x, const T* __restrict__ nrm,
+                           const T* __restrict__ g, T* __restrict__ dx, int N, int C, int H,
+                           int W, int64_t sn, int64_t sc, int64_t sh, int64_t sw) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)N * H * W) return;
+  const int xx = idx % W;
+  const int y = (idx / W) % H;
+  const int n = idx / ((int64_t)H * W);
+  const int64_t off = n * sn + y * sh + xx * sw;
+  const float k = to_f<T>(g[idx]) / (to_f<T>(nrm[idx]) + 1e-9f);
+  for (int c = 0; c < C; ++c) dx[off + c * sc] = from_f<T>(to_f<T>(x[off + c * sc]) * k);
+}
+
+inline int corr_out_size(int in, int pad, int ks, int md, int s1) {
+  const int border = (ks - 1) / 2 + md;
+  const int padded = in + 2 * pad;
+  return (int)std::ceil((double)(padded - 2 * border) / (double)s1);
+}
+
+}  // namespace
+
+// in1, in2: [N, C, H, W] (any memory format; made channels-last internally)
+// returns [N, D*D, oH, oW] in channels-last memory format, dtype of the inputs.
+at::Tensor correlation_forward(const at::Tensor& input1, const at::Tensor& input2, int64_t pad,
+                               int64_t ks, int64_t md, int64_t s1, int64_t s2) {
+  IAMD_CHECK(input1.dim() == 4 && input1.sizes() == input2.sizes(), "correlation: shapes");
+  IAMD_CHECK(ks >= 1 && ks % 2 == 1 && s1 >= 1 && s2 >= 1, "correlation: bad params");
+  auto a = input1.contiguous(at::MemoryFormat::ChannelsLast);
+  auto b = input2.to(a.scalar_type()).contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = a.size(0), C = a.size(1), H = a.size(2), W = a.size(3);
+  const int R = md / s2, D = 2 * R + 1;
+  const int oH = corr_out_size(H, pad, ks, md, s1), oW = corr_out_size(W, pad, ks, md, s1);
+  IAMD_CHECK(oH > 0 && oW > 0, "correlation: empty output");
+  auto out = at::empty({N, D * D, oH, oW},
+                       a.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int ngrp = kCorrThreads / kTX;
+  IAMD_DISPATCH_FLOAT_TYPES(a.scalar_type(), "correlation_fwd", [&] {
+    auto pa = reinterpret_cast<const scalar_t*>(a.data_ptr());
+    auto pb = reinterpret_cast<const scalar_t*>(b.data_ptr());
+    auto po = reinterpret_cast<scalar_t*>(out.data_ptr());
+    const int span = (kTX - 1) * s1 + 2 * R * s2 + 1;
+    const size_t lds = (size_t)span * kLdsPad * sizeof(float);
+    if (ks == 1 && D <= ngrp * kMaxDispPerLane && lds <= 96 * 1024) {
+      dim3 grid(ceil_div(oW, kTX), oH, N * D);
+      hipLaunchKernelGGL((corr_fwd_k1<scalar_t>), grid, dim3(kCorrThreads), lds, stream(), pa,
+                         pb, po, H, W, C, oH, oW, (int)pad, (int)md, (int)s1, (int)s2, R, D);
+    } else {
+      dim3 grid(oW, oH, N);
+      hipLaunchKernelGGL((corr_fwd_generic<scalar_t>), grid, dim3(kWave), 0, stream(), pa, pb,
+                         po, H, W, C, oH, oW, (int)pad, (int)ks, (int)md, (int)s1, (int)s2, R,
+                         D);
+    }
+  });
+  IAMD_LAUNCH_CHECK();
+  return out;
+}
+
+// returns {grad_input1, grad_input2} fp32, channels-last [N, C, H, W]
+std::vector<at::Tensor> correlation_backward(const at::Tensor& input1, const at::Tensor& input2,
+                                             const at::Tensor& grad_out, int64_t pad,
+                                             int64_t ks, int64_t md, int64_t s1, int64_t s2) {
+  auto a = input1.contiguous(at::MemoryFormat::ChannelsLast);
+  auto b = input2.to(a.scalar_type()).contiguous(at::MemoryFormat::ChannelsLast);
+  auto g = grad_out.to(at::kFloat).contiguous(at::MemoryFormat::ChannelsLast);
+  const int N = a.size(0), C = a.size(1), H = a.size(2), W = a.size(3);
+  const int R = md / s2, D = 2 * R + 1;
+  const int oH = corr_out_size(H, pad, ks, md, s1), oW = corr_out_size(W, pad, ks, md, s1);
+  IAMD_CHECK(g.size(0) == N && g.size(1) == D * D && g.size(2) == oH && g.size(3) == oW,
+             "correlation_backward: grad_out shape");
+  auto fopt = a.options().dtype(at::kFloat).memory_format(at::MemoryFormat::ChannelsLast);
+  auto g1 = at::empty({N, C, H, W}, fopt);
+  auto g2 = at::empty({N, C, H, W}, fopt);
+  const int64_t total = (int64_t)N * H * W * C;
+  if (total == 0) return {g1, g2};
+  IAMD_DISPATCH_FLOAT_TYPES(a.scalar_type(), "correlation_bwd", [&] {
+    hipLaunchKernelGGL((corr_bwd<scalar_t>), dim3(ceil_div(total, 256)), dim3(256), 0, stream(),
+                       reinterpret_cast<const scalar_t*>(a.data_ptr()),
+                       reinterpret_cast<const scalar_t*>(b.data_ptr()), g.data_ptr<float>(),
+                       g1.data_ptr<float>(), g2.data_ptr<float>(), N, H, W, C, oH, oW, (int)pad,
+                       (int)ks, (int)md, (int)s1, (int)s2, R, D);
+  });
+  IAMD_LAUNCH_CHECK();
+  return {g1, g2};
+}
+
+// x: [N, C, H, W] any strides -> [N, 1, H, W]
+at::Tensor channelnorm_forward(const at::Tensor& x) {
+  IAMD_CHECK(x.dim() == 4, "channelnorm: 4-D input");
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  auto out = at::empty({N, 1, H, W}, x.options());
+  const int64_t total = (int64_t)N * H * W;
+  if (total == 0) return out;
+  IAMD_DISPATCH_FLOAT_TYPES(x.scalar_type(), "channelnorm_fwd", [&] {
+    hipLaunchKernelGGL((chnorm_fwd<scalar_t>), dim3(ceil_div(total, 256)), dim3(256), 0, stream(),
+                       reinterpret_cast<const scalar_t*>(x.data_ptr()),
+                       reinterpret_cast<scalar_t*>(out.data_ptr()), N, C, H, W, x.stride(0),
+                       x.stride(1), x.stride(2), x.stride(3));
+  });
+  IAMD_LAUNCH_CHECK();
+  return out;
+}
+
+at::Tensor channelnorm_backward(const at::Tensor& x, const at::Tensor& out,
+                                const at::Tensor& grad_out) {
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  auto nrm = out.to(x.scalar_type()).contiguous();
+  auto g = grad_out.to(x.scalar_type()).contiguous();
+  auto dx = at::empty_strided(x.sizes(), x.strides(), x.options());
+  const int64_t total = (int64_t)N * H * W;
+  if (total == 0) return dx;
+  IAMD_CHECK(x.is_non_overlapping_and_dense(), "channelnorm_backward: dense input");
+  IAMD_DISPATCH_FLOAT_TYPES(x.scalar_type(), "channelnorm_bwd", [&] {
+    hipLaunchKernelGGL((chnorm_bwd<scalar_t>), dim3(ceil_div(total, 256)), dim3(256), 0, stream(),
+                       reinterpret_cast<const scalar_t*>(x.data_ptr()),
+                       reinterpret_cast<const scalar_t*>(nrm.data_ptr()),
+                       reinterpret_cast<const scalar_t*>(g.data_ptr()),
+                       reinterpret_cast<scalar_t*>(dx.data_ptr()), N, C, H, W, x.stride(0),
+                       x.stride(1), x.stride(2), x.stride(3));
+  });
+  IAMD_LAUNCH_CHECK();
+  return dx;
+}
+
+}  // namespace iamd

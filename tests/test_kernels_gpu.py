@@ -58,8 +58,9 @@ def test_fused_norm_act(layout, mode, dtype, mod):
     xr = x.detach().float().requires_grad_(True)
     wr = w.detach().clone().requires_grad_(True)
     br = b.detach().clone().requires_grad_(True)
-    gr = g_gamma.detach().float().requires_grad_(True) if g_gamma is not None else None
-    ber = g_beta.detach().float().requires_grad_(True) if g_beta is not None else None
+    # the op applies the modulation in the activation dtype: round like it does
+    gr = g_gamma.detach().to(dtype).float().requires_grad_(True) if g_gamma is not None else None
+    ber = g_beta.detach().to(dtype).float().requires_grad_(True) if g_beta is not None else None
     yr = _ref_norm(xr, mode, wr, br, gr, ber, 0.2)
     tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
     assert torch.allclose(y.float(), yr, atol=tol * 5, rtol=tol), (y.float() - yr).abs().max()
@@ -179,3 +180,50 @@ def test_multi_tensor_adam_and_ema():
     _ext.ext().mt_ema(ts, ws, 0.9, sig)
     for t, tr, w, s in zip(ts, ts_ref, ws, ref_sig):
         assert torch.allclose(t, 0.9 * tr + 0.1 * w / s, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('params', [(20, 1, 20, 1, 2), (4, 1, 4, 1, 1), (3, 3, 2, 2, 1)])
+def test_correlation(dtype, params):
+    from imaginaire_amd.ops.flownet_ops import _CorrelationFn, correlation_reference
+    torch.manual_seed(3)
+    N, C, H, W = 2, 40, 13, 37
+    a = torch.randn(N, C, H, W, device='cuda').to(dtype).contiguous(
+        memory_format=torch.channels_last).requires_grad_(True)
+    b = torch.randn(N, C, H, W, device='cuda').to(dtype).requires_grad_(True)
+    out = _CorrelationFn.apply(a, b, *params)
+    ar = a.detach().float().requires_grad_(True)
+    br = b.detach().float().requires_grad_(True)
+    ref = correlation_reference(ar, br, *params)
+    assert out.shape == ref.shape
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    assert torch.allclose(out.float(), ref, atol=tol, rtol=tol), (out.float() - ref).abs().max()
+    go = torch.randn_like(ref)
+    out.backward(go.to(dtype))
+    ref.backward(go)
+    assert torch.allclose(a.grad.float(), ar.grad, atol=tol, rtol=tol * 5)
+    assert torch.allclose(b.grad.float(), br.grad, atol=tol, rtol=tol * 5)
+
+
+@pytest.mark.parametrize('layout', ['cl', 'nchw'])
+def test_channelnorm_resample2d(layout):
+    from imaginaire_amd.ops.flownet_ops import (_ChannelNormFn, _Resample2dFn,
+                                                channelnorm_reference, resample2d_reference)
+    torch.manual_seed(4)
+    x = torch.randn(2, 5, 17, 23, device='cuda')
+    if layout == 'cl':
+        x = x.contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    y = _ChannelNormFn.apply(x)
+    xr = x.detach().clone().requires_grad_(True)
+    yr = channelnorm_reference(xr)
+    assert torch.allclose(y, yr, atol=1e-5)
+    go = torch.randn_like(yr)
+    y.backward(go)
+    yr.backward(go)
+    assert torch.allclose(x.grad, xr.grad, atol=1e-4)
+    img = torch.randn(2, 3, 17, 23, device='cuda', requires_grad=True)
+    flow = (torch.randn(2, 2, 17, 23, device='cuda') * 3).requires_grad_(True)
+    o = _Resample2dFn.apply(img, flow, 1)
+    o_ref = resample2d_reference(img.detach(), flow.detach(), 1)
+    assert torch.allclose(o, o_ref, atol=1e-5)
