@@ -90,7 +90,20 @@ class Dataset(torch.utils.data.Dataset):
         self.h, self.w = _crop_hw(self.cfg_data, is_inference, is_test)
         syn = getattr(self.cfg_data, 'synthetic', None)
         self.length = int(getattr(syn, 'num_samples', 64)) if syn is not None else 64
-        self.seq_len = int(getattr(syn, 'sequence_length', 0)) if syn is not None else 0
+        # video datasets (paired_videos / paired_few_shot_videos contract)
+        self.is_video = 'video' in str(getattr(self.cfg_data, 'type', '')) or \
+            hasattr(self.cfg_data, 'num_frames_G') or \
+            int(getattr(syn, 'sequence_length', 0) or 0) > 0
+        self.sequence_length_max = int(getattr(syn, 'max_sequence_length', 8) or 8) \
+            if syn is not None else 8
+        train = getattr(self.cfg_data, 'train', None)
+        self.seq_len = int(getattr(syn, 'sequence_length', 0) or 0) if syn is not None else 0
+        if self.is_video and not self.seq_len:
+            self.seq_len = int(getattr(train, 'initial_sequence_length', 1) or 1) \
+                if not is_inference else 1
+        self.sequence_length = self.seq_len
+        self.few_shot = 'few_shot' in str(getattr(self.cfg_data, 'type', ''))
+        self.few_shot_K = int(getattr(self.cfg_data, 'initial_few_shot_K', 1) or 1)
         self.paired = getattr(self.cfg_data, 'paired', True)
         self.input_labels = list(getattr(self.cfg_data, 'input_labels', []))
         self.input_image = list(getattr(self.cfg_data, 'input_image', ['images']))
@@ -114,6 +127,12 @@ class Dataset(torch.utils.data.Dataset):
     def set_inference_sequence_idx(self, *args):
         self.inference_sequence_idx = args
 
+    def set_sequence_length(self, sequence_length):
+        """Frames per training sample (vid2vid curriculum); 0 = whole sequence."""
+        self.sequence_length = min(int(sequence_length) or self.sequence_length_max,
+                                   self.sequence_length_max)
+        self.seq_len = self.sequence_length
+
     def set_sample_class_idx(self, class_idx):
         self.sample_class_idx = class_idx
 
@@ -124,7 +143,14 @@ class Dataset(torch.utils.data.Dataset):
         for name, t in self.types.items():
             nc = t.num_channels
             interp = getattr(t, 'interpolator', 'BILINEAR')
-            if name in self.input_image or name.startswith('images'):
+            if name == 'unprojections':
+                continue
+            if name == 'flow':
+                # external flow (px) + occlusion mask, wc-vid2vid fork contract
+                f = smooth_field(2, h, w, gen) * 2.0
+                m = (smooth_field(1, h, w, gen) + 1) / 2
+                out[name] = torch.cat([f, m], 0)
+            elif name in self.input_image or name.startswith('images'):
                 out[name] = smooth_field(nc, h, w, gen).clamp(-1, 1)
             elif interp == 'NEAREST' and nc > 1:
                 seg = voronoi_labels(h, w, nc, gen)
@@ -151,6 +177,10 @@ class Dataset(torch.utils.data.Dataset):
             sample = {k: torch.stack([f[k] for f in frames]) for k in frames[0]}
         else:
             sample = self._frame(gen)
+        few_shot = None
+        if self.few_shot:
+            shots = [self._frame(gen) for _ in range(self.few_shot_K)]
+            few_shot = {k: torch.stack([f[k] for f in shots]) for k in shots[0]}
         data = {}
         labels = [sample[n] for n in self.input_labels if n in sample]
         if labels:
@@ -161,6 +191,11 @@ class Dataset(torch.utils.data.Dataset):
         for n, v in sample.items():
             if n not in self.input_labels and n not in self.input_image:
                 data[n] = v
+        if few_shot is not None:
+            shot_labels = [few_shot[n] for n in self.input_labels if n in few_shot]
+            if shot_labels:
+                data['few_shot_label'] = torch.cat(shot_labels, dim=-3)
+            data['few_shot_images'] = few_shot[self.input_image[0]]
         if not self.paired and 'images' in data and 'images_b' not in data:
             data['images_a'] = data['images']
             gen_b = torch.Generator().manual_seed(98765 + int(index))

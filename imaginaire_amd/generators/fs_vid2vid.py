@@ -328,7 +328,8 @@ class WeightGenerator(nn.Module):
         if hasattr(hyper_cfg, 'attention'):
             self.num_downsample_atn = get_and_setattr(hyper_cfg.attention, 'num_downsamples', 2)
             if data_cfg.initial_few_shot_K > 1:
-                self.attention_module = AttentionModule(hyper_cfg, data_cfg, conv_2d_block, nf)
+                self.attention_module = AttentionModule(hyper_cfg.attention, data_cfg,
+                                                        conv_2d_block, nf)
         else:
             self.num_downsample_atn = 0
 
@@ -501,7 +502,10 @@ class AttentionModule(nn.Module):
         super().__init__()
         self.initial_few_shot_K = data_cfg.initial_few_shot_K
         num_input_channels = data_cfg.num_input_channels
-        num_filters = getattr(atn_cfg, 'num_filters', 32)
+        # the reference reads num_filters from the hyper cfg (default 32), which only
+        # matches the key/query towers when the generator also uses 32 filters; the
+        # towers' first layer must produce num_filters_each_layer[0] channels.
+        num_filters = num_filters_each_layer[0]
         self.num_downsample_atn = getattr(atn_cfg, 'num_downsamples', 2)
         self.atn_query_first = conv_2d_block(num_input_channels, num_filters)
         self.atn_key_first = conv_2d_block(num_input_channels, num_filters)

@@ -6,10 +6,10 @@ ROOT=$(pwd)
 mkdir -p gpurun_out/prof
 step() {  # name, timeout, cmd...
   local name=$1 t=$2; shift 2
-  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  timeout -k 10 "$t" "$@" > "$ROOT/gpurun_out/$name.log" 2>&1
   local rc=$?
   echo "[profile_round] $name rc=$rc"
-  tail -12 "gpurun_out/$name.log"
+  tail -12 "$ROOT/gpurun_out/$name.log"
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
 if [ -z "$SKIP_PROBE" ]; then
@@ -17,7 +17,11 @@ if [ -z "$SKIP_PROBE" ]; then
   step probe_bench 400 python scripts/probe/conv_find_probe.py bench
 fi
 cd /tmp && export TMPDIR=/tmp
-step rocprof 900 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/prof" -o bench -- \
+rm -rf /tmp/iamd_prof
+step rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/iamd_prof -o bench -- \
   python3 "$ROOT/bench.py" ${BENCH_ARGS:---steps 3 --warmup 2 --verbose}
 cd "$ROOT"
-find gpurun_out/prof -name '*stats*' | head -20
+# keep only the (small) summary tables; the full trace stays on the box
+find /tmp/iamd_prof -name '*stats*.csv' -exec cp {} gpurun_out/prof/ \;
+python3 scripts/gpu/summarize_kernels.py gpurun_out/prof > gpurun_out/prof/top_kernels.txt || true
+head -60 gpurun_out/prof/top_kernels.txt

@@ -11,7 +11,8 @@ from imaginaire_amd.utils.dataset import get_train_and_val_dataloader
 from imaginaire_amd.utils.trainer import get_model_optimizer_and_scheduler, get_trainer
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-FAMILIES = ['spade', 'pix2pixHD', 'munit', 'unit', 'funit', 'coco_funit']
+FAMILIES = ['spade', 'pix2pixHD', 'munit', 'unit', 'funit', 'coco_funit', 'vid2vid_street',
+            'fs_vid2vid_face', 'wc_vid2vid']
 
 
 @pytest.mark.parametrize('name', FAMILIES)
@@ -22,6 +23,7 @@ def test_family_one_iteration(tmp_path, name):
     train_loader, val_loader = get_train_and_val_dataloader(cfg)
     nets = get_model_optimizer_and_scheduler(cfg, seed=0)
     trainer = get_trainer(cfg, *nets, train_loader, val_loader)
+    trainer.start_of_epoch(0)
     data = trainer.start_of_iteration(next(iter(train_loader)), 0)
     before = [p.detach().clone() for p in trainer.net_G_module.parameters()]
     trainer.dis_update(data)
