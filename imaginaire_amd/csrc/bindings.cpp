@@ -60,10 +60,12 @@ std::vector<at::Tensor> flow_warp_bwd(const at::Tensor& img, const at::Tensor& f
 at::Tensor resample2d_forward(const at::Tensor& in1, const at::Tensor& flow, int64_t ks);
 std::vector<at::Tensor> resample2d_backward(const at::Tensor& in1, const at::Tensor& flow,
                                             const at::Tensor& dout, int64_t ks);
+void register_lmdb(pybind11::module_& m);
 }  // namespace iamd
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "imaginaire_amd gfx950 HIP kernels";
+  iamd::register_lmdb(m);
   m.def("norm_stats", &iamd::norm_stats, "per-(group,channel) statistics (k1)");
   m.def("norm_apply", &iamd::norm_apply, "norm + SPADE modulation + activation (k1 fwd)");
   m.def("norm_bwd_reduce", &iamd::norm_bwd_reduce, "k1 backward reduction");

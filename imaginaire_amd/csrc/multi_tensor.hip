@@ -30,6 +30,9 @@ struct TensorEntry {
   void* p[5];
   int64_t numel;
   int64_t cols;  // numel / size(0): row length when viewed as a matrix (spectral norm)
+  // channels-last 4-D weights: memory column (kh, kw, ci) -> logical column (ci, kh, kw)
+  int64_t cl_cin;  // 0 = memory order == logical order
+  int64_t cl_khw;
 };
 
 struct Table {
@@ -64,6 +67,16 @@ Table& get_table(const std::vector<std::vector<at::Tensor>>& lists, const at::De
     ents[i].numel = lists[0][i].numel();
     ents[i].cols = lists[0][i].dim() > 0 && lists[0][i].size(0) > 0
                        ? ents[i].numel / lists[0][i].size(0) : 1;
+    const at::Tensor& t0 = lists[0][i];
+    const bool cl = t0.dim() == 4 && !t0.is_contiguous() &&
+                    t0.is_contiguous(at::MemoryFormat::ChannelsLast);
+    ents[i].cl_cin = cl ? t0.size(1) : 0;
+    ents[i].cl_khw = cl ? t0.size(2) * t0.size(3) : 0;
+    // every parallel operand of the same rank must share the layout of list 0
+    for (size_t k = 1; k < lists.size(); ++k)
+      if (lists[k][i].dim() == t0.dim())
+        IAMD_CHECK(lists[k][i].strides() == t0.strides(),
+                   "multi-tensor: operand layouts differ (strides must match)");
     const int64_t nch = (ents[i].numel + kChunk - 1) / kChunk;
     for (int64_t c = 0; c < nch; ++c) {
       bm.push_back((int32_t)i);
@@ -172,7 +185,9 @@ sn_sigma_kernel(const TensorEntry* __restrict__ ents, const int* __restrict__ bl
   const int64_t end = min(e.numel, start + (int64_t)kChunk);
   float acc = 0.f;
   for (int64_t i = start + threadIdx.x; i < end; i += kThreads) {
-    const int64_t r = i / ncol, c = i - r * ncol;
+    const int64_t r = i / ncol;
+    int64_t c = i - r * ncol;
+    if (e.cl_cin) c = (c % e.cl_cin) * e.cl_khw + c / e.cl_cin;
     acc = fmaf(u[r] * W[i], v[c], acc);
   }
   acc = wave_sum(acc);
@@ -246,7 +261,7 @@ sqnorm_kernel(const TensorEntry* __restrict__ ents, const int* __restrict__ bloc
 void check_same_dtype(const std::vector<at::Tensor>& l, at::ScalarType st, const char* what) {
   for (auto& t : l) {
     IAMD_CHECK(t.scalar_type() == st, what, ": dtype mismatch");
-    IAMD_CHECK(t.is_contiguous(), what, ": tensors must be contiguous");
+    IAMD_CHECK(t.is_non_overlapping_and_dense(), what, ": tensors must be dense");
   }
 }
 

@@ -18,6 +18,8 @@ SPADE MI355X specifics (SpatiallyAdaptiveNorm):
 from types import SimpleNamespace
 
 import torch
+
+from imaginaire_amd.ops import conv as nhwc_conv
 from torch import nn
 from torch.nn import functional as F
 
@@ -305,7 +307,8 @@ class SpatiallyAdaptiveNorm(nn.Module):
             cb = self.betas[i].layers.conv
             w = torch.cat([get_weight(cg), get_weight(cb)], 0)
             b = torch.cat([cg.bias, cb.bias], 0) if cg.bias is not None else None
-            return F.conv2d(hidden, w, b, cg.stride, cg.padding, cg.dilation, cg.groups)
+            return nhwc_conv.conv2d(hidden, w, b, cg.stride, cg.padding, cg.dilation, cg.groups,
+                                    cg.padding_mode)
         return self.mlps[i](label_map)
 
     def forward(self, x, *cond_inputs, act_slope=1.0, **kwargs):

@@ -81,8 +81,9 @@ class WeightDemodulation(nn.Module):
         _, _, *ws = weight.shape
         weight = weight.reshape(b * self.conv.out_channels, *ws)
         bias = self.conv.bias.repeat(b) if self.conv.bias is not None else None
-        x = torch.nn.functional.conv2d(x, weight, bias, self.conv.stride, self.conv.padding,
-                                       self.conv.dilation, groups=b)
+        from imaginaire_amd.ops.conv import conv2d as _conv2d
+        x = _conv2d(x, weight, bias, self.conv.stride, self.conv.padding, self.conv.dilation,
+                    groups=b)
         x = x.reshape(-1, self.conv.out_channels, x.shape[2], x.shape[3])
         if self.adaptive_bias:
             x = x + self.fc_beta(y)[:, :, None, None]

@@ -53,6 +53,13 @@ class _Bucket(object):
         self.comm = None
 
 
+def _grad_view(flat, off, p):
+    """Bucket slice viewed with the parameter's own strides (channels-last
+    conv weights stay channels-last), so fused optimizers can walk param and
+    grad storage in the same order."""
+    return flat[off:off + p.numel()].as_strided(p.size(), p.stride())
+
+
 class DistributedDataParallel(nn.Module):
     def __init__(self, module, process_group=None, bucket_cap_mb=256, first_bucket_mb=16,
                  broadcast_buffers=False, comm_dtype=None, overlap=True, **unused):
@@ -118,7 +125,7 @@ class DistributedDataParallel(nn.Module):
         for bi, b in enumerate(self.buckets):
             for p, off in zip(b.params, b.offsets):
                 self._param_bucket[p] = (bi, off)
-                p.grad = b.flat[off:off + p.numel()].view_as(p)
+                p.grad = _grad_view(b.flat, off, p)
                 if self.overlap:
                     self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
 
@@ -136,7 +143,7 @@ class DistributedDataParallel(nn.Module):
             b.flat.zero_()
             for p, off in zip(b.params, b.offsets):
                 if p.grad is None or p.grad.data_ptr() != b.flat.data_ptr() + off * 4:
-                    p.grad = b.flat[off:off + p.numel()].view_as(p)
+                    p.grad = _grad_view(b.flat, off, p)
 
     def _on_grad(self, p):
         if not self._active:

@@ -71,6 +71,12 @@ def get_model_optimizer_and_scheduler(cfg, seed=0, device=None):
     net_D.apply(weights_init(init_type, init_gain, init_bias))
     net_G = net_G.to(device)
     net_D = net_D.to(device)
+    if torch.device(device).type == 'cuda':
+        # packed NHWC conv weights: MIOpen's fast NHWC solvers need both operands
+        # channels-last (see ops/conv.py); optimizer state / EMA / DDP bucket views
+        # all follow the parameter strides.
+        net_G = net_G.to(memory_format=torch.channels_last)
+        net_D = net_D.to(memory_format=torch.channels_last)
     set_random_seed(seed, by_rank=True)
     print('net_G parameter count: {:,}'.format(_calculate_model_size(net_G)))
     print('net_D parameter count: {:,}'.format(_calculate_model_size(net_D)))

@@ -13,7 +13,7 @@ tail -5 gpurun_out/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 ok_or_stop $? smoke
 tail -2 gpurun_out/smoke.log
-if [ -n "$BENCH_ARGS" ] || [ -z "$NO_BENCH" ]; then
+if [ -z "$NO_BENCH" ]; then
   timeout -k 10 ${BENCH_TIMEOUT:-900} python bench.py ${BENCH_ARGS:---steps 10 --warmup 5} > gpurun_out/bench.json 2> gpurun_out/bench.err
   ok_or_stop $? bench
   cat gpurun_out/bench.json; tail -5 gpurun_out/bench.err

@@ -146,12 +146,17 @@ def test_flow_warp(dtype):
     assert close.float().mean() > 0.99
 
 
-def test_multi_tensor_adam_and_ema():
+@pytest.mark.parametrize('layout', ['contiguous', 'channels_last'])
+def test_multi_tensor_adam_and_ema(layout):
     from imaginaire_amd.optimizers.fused_adam import FusedAdam, _reference_adam
     from imaginaire_amd.ops import _ext
     torch.manual_seed(4)
+    cl = layout == 'channels_last'
+
+    def fmt(t):
+        return t.contiguous(memory_format=torch.channels_last) if cl and t.dim() == 4 else t
     shapes = [(37,), (128, 64), (3, 5, 7, 11), (1,), (70001,)]
-    ps = [torch.randn(s, device='cuda') for s in shapes]
+    ps = [fmt(torch.randn(s, device='cuda')) for s in shapes]
     refs = [p.detach().clone() for p in ps]
     for p in ps:
         p.requires_grad_(True)
@@ -159,7 +164,7 @@ def test_multi_tensor_adam_and_ema():
     m = [torch.zeros_like(p) for p in refs]
     v = [torch.zeros_like(p) for p in refs]
     for step in range(1, 4):
-        grads = [torch.randn_like(p) for p in ps]
+        grads = [fmt(torch.randn_like(p)) for p in ps]
         for p, g in zip(ps, grads):
             p.grad = g.clone()
         opt.step()
@@ -167,7 +172,8 @@ def test_multi_tensor_adam_and_ema():
     for p, r in zip(ps, refs):
         assert torch.allclose(p.detach(), r, atol=1e-6, rtol=1e-5)
     # EMA with spectral-norm absorption
-    ws = [torch.randn(8, 3, 3, 3, device='cuda'), torch.randn(16, 40, device='cuda')]
+    ws = [fmt(torch.randn(8, 3, 3, 3, device='cuda')), torch.randn(16, 40, device='cuda'),
+          fmt(torch.randn(32, 16, 5, 5, device='cuda'))]
     us = [torch.nn.functional.normalize(torch.randn(w.shape[0], device='cuda'), dim=0) for w in ws]
     vs = [torch.nn.functional.normalize(torch.randn(w[0].numel(), device='cuda'), dim=0)
           for w in ws]
@@ -175,7 +181,7 @@ def test_multi_tensor_adam_and_ema():
     ref_sig = torch.stack([torch.dot(u, w.reshape(w.shape[0], -1) @ vv)
                            for w, u, vv in zip(ws, us, vs)])
     assert torch.allclose(sig, ref_sig, atol=1e-4, rtol=1e-4)
-    ts = [torch.randn_like(w) for w in ws]
+    ts = [fmt(torch.randn_like(w)) for w in ws]
     ts_ref = [t.clone() for t in ts]
     _ext.ext().mt_ema(ts, ws, 0.9, sig)
     for t, tr, w, s in zip(ts, ts_ref, ws, ref_sig):
