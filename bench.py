@@ -98,6 +98,12 @@ def main():
         torch.cuda.synchronize()
 
     barrier()
+    if args.verbose:
+        try:  # phase marker for scripts/gpu/summarize_kernels.py (steady-state split)
+            from imaginaire_amd.ops import _ext
+            _ext.ext().profile_marker(1)
+        except Exception:  # noqa: BLE001
+            pass
     t0 = time.perf_counter()
     for it in range(args.steps):
         step(args.warmup + it)

@@ -113,6 +113,7 @@ class Augmentor(object):
         self.keypoint_data_types = keypoint_data_types or []
         self.crop_h = self.crop_w = None
         self.resize_h = self.resize_w = None
+        self.original_h = self.original_w = None
         self.resize_smallest_side = None
         self.max_time_step = 1
         self.ops = self._build_augmentation_ops()

@@ -23,5 +23,5 @@ step rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/ia
 cd "$ROOT"
 # keep only the (small) summary tables; the full trace stays on the box
 find /tmp/iamd_prof -name '*stats*.csv' -exec cp {} gpurun_out/prof/ \;
-python3 scripts/gpu/summarize_kernels.py gpurun_out/prof > gpurun_out/prof/top_kernels.txt || true
+python3 scripts/gpu/summarize_kernels.py /tmp/iamd_prof > gpurun_out/prof/top_kernels.txt || true
 head -60 gpurun_out/prof/top_kernels.txt

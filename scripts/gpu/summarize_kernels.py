@@ -28,13 +28,52 @@ def family(name):
     return 'other'
 
 
-def main(root):
-    files = [f for f in glob.glob(os.path.join(root, '**', '*kernel_stats*.csv'), recursive=True)]
-    rows = []
-    for f in files:
+MARKER = 'iamd_profile_marker_kernel'
+
+
+def steady_rows(root):
+    """Per-kernel totals from the kernel trace, counting only dispatches that
+    start after the last profile marker (= the timed steady-state region)."""
+    traces = glob.glob(os.path.join(root, '**', '*kernel_trace*.csv'), recursive=True)
+    if not traces:
+        return None, 0.0
+    recs = []
+    for f in traces:
         with open(f) as fh:
-            for r in csv.DictReader(fh):
-                rows.append(r)
+            rd = csv.DictReader(fh)
+            kn = next(k for k in rd.fieldnames if 'Kernel_Name' in k)
+            ks = next(k for k in rd.fieldnames if 'Start_Timestamp' in k)
+            ke = next(k for k in rd.fieldnames if 'End_Timestamp' in k)
+            for r in rd:
+                recs.append((int(r[ks]), int(r[ke]), r[kn]))
+    marks = [s for s, _, n in recs if MARKER in n]
+    if not marks:
+        return None, 0.0
+    t0 = max(marks)
+    agg = {}
+    t_end = t0
+    for s, e, n in recs:
+        if s >= t0 and MARKER not in n:
+            a = agg.setdefault(n, [0, 0.0])
+            a[0] += 1
+            a[1] += e - s
+            t_end = max(t_end, e)
+    rows = [{'Name': n, 'Calls': str(c), 'TotalDurationNs': str(d)} for n, (c, d) in agg.items()]
+    return rows, (t_end - t0) / 1e6
+
+
+def main(root):
+    rows, span_ms = steady_rows(root)
+    if rows:
+        print('STEADY STATE (after last profile marker): wall span %.1f ms' % span_ms)
+    else:
+        files = glob.glob(os.path.join(root, '**', '*kernel_stats*.csv'), recursive=True)
+        rows = []
+        for f in files:
+            with open(f) as fh:
+                for r in csv.DictReader(fh):
+                    rows.append(r)
+        print('WHOLE RUN (no marker found)')
     if not rows:
         print('no kernel stats found under', root)
         return
