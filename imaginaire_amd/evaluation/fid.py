@@ -70,19 +70,31 @@ def get_inception_mean_cov(data_loader, key_real, key_fake, generator, sample_si
     else:
         y = get_activations(data_loader, key_real, key_fake, generator, sample_size, preprocess)
     if is_master():
+        if y.shape[0] < 2:  # covariance of a single sample is undefined
+            return np.mean(y, axis=0), np.zeros((y.shape[1], y.shape[1]))
         return np.mean(y, axis=0), np.cov(y, rowvar=False)
     return None, None
 
 
-def _sqrtm_trace_gpu(sigma1, sigma2):
-    dev = torch.device('cuda', torch.cuda.current_device())
+def _sqrtm_trace(sigma1, sigma2, eps=1e-6):
+    """tr(sqrt(S1 S2)) via two symmetric eigendecompositions in fp64:
+    sqrt(S1) S2 sqrt(S1) is symmetric PSD with the same eigenvalues as S1 S2,
+    so no non-symmetric sqrtm (and no complex round-off) is needed."""
+    dev = torch.device('cuda', torch.cuda.current_device()) if torch.cuda.is_available() \
+        else torch.device('cpu')
     s1 = torch.as_tensor(sigma1, dtype=torch.float64, device=dev)
     s2 = torch.as_tensor(sigma2, dtype=torch.float64, device=dev)
-    w, v = torch.linalg.eigh((s1 + s1.T) / 2)
-    root1 = (v * w.clamp_min(0).sqrt()) @ v.T
-    m = root1 @ s2 @ root1
-    ev = torch.linalg.eigvalsh((m + m.T) / 2)
-    return float(ev.clamp_min(0).sqrt().sum().item())
+    eye = torch.eye(s1.shape[0], dtype=torch.float64, device=dev)
+    for jitter in (0.0, eps, eps * 1e3):
+        try:
+            w, v = torch.linalg.eigh((s1 + s1.T) / 2 + jitter * eye)
+            root1 = (v * w.clamp_min(0).sqrt()) @ v.T
+            m = root1 @ (s2 + jitter * eye) @ root1
+            ev = torch.linalg.eigvalsh((m + m.T) / 2)
+            return float(ev.clamp_min(0).sqrt().sum().item())
+        except RuntimeError:  # ill-conditioned (e.g. tiny sample sets): add jitter
+            continue
+    raise RuntimeError('FID: covariance eigendecomposition failed')
 
 
 def calculate_frechet_distance(mu1, sigma1, mu2, sigma2, eps=1e-6):
@@ -93,15 +105,9 @@ def calculate_frechet_distance(mu1, sigma1, mu2, sigma2, eps=1e-6):
     assert mu1.shape == mu2.shape, 'Training and test mean vectors have different lengths'
     assert sigma1.shape == sigma2.shape, 'Training and test covariances have different dimensions'
     diff = mu1 - mu2
-    if torch.cuda.is_available():
-        tr_covmean = _sqrtm_trace_gpu(sigma1, sigma2)
-    else:
-        from scipy import linalg
-        covmean, _ = linalg.sqrtm(sigma1.dot(sigma2), disp=False)
-        if not np.isfinite(covmean).all():
-            offset = np.eye(sigma1.shape[0]) * eps
-            covmean = linalg.sqrtm((sigma1 + offset).dot(sigma2 + offset))
-        if np.iscomplexobj(covmean):
-            covmean = covmean.real
-        tr_covmean = np.trace(covmean)
+    if not (np.isfinite(mu1).all() and np.isfinite(mu2).all() and np.isfinite(sigma1).all()
+            and np.isfinite(sigma2).all()):
+        print('FID: non-finite activation statistics (diverged generator?); returning nan')
+        return float('nan')
+    tr_covmean = _sqrtm_trace(sigma1, sigma2)
     return float(diff.dot(diff) + np.trace(sigma1) + np.trace(sigma2) - 2 * tr_covmean)

@@ -1,0 +1,28 @@
+"""train -> checkpoint -> inference.py / evaluate.py CLIs on CPU (spade unit config)."""
+import glob
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def test_inference_and_evaluate_cli(tmp_path):
+    from imaginaire_amd.config import Config
+    from imaginaire_amd.utils.dataset import get_train_and_val_dataloader
+    from imaginaire_amd.utils.trainer import get_model_optimizer_and_scheduler, get_trainer
+    cfg_path = os.path.join(ROOT, 'configs', 'unit_test', 'spade.yaml')
+    cfg = Config(cfg_path)
+    cfg.logdir = str(tmp_path / 'train')
+    tl, vl = get_train_and_val_dataloader(cfg)
+    trainer = get_trainer(cfg, *get_model_optimizer_and_scheduler(cfg, seed=0), tl, vl)
+    ckpt = trainer.save_checkpoint(0, 1)
+    assert os.path.exists(ckpt)
+    import inference
+    out = tmp_path / 'out'
+    inference.main(['--config', cfg_path, '--checkpoint', ckpt, '--output_dir', str(out),
+                    '--single_gpu', '--logdir', str(tmp_path / 'inf'), '--num_workers', '0'])
+    assert len(glob.glob(str(out / '**' / '*.jpg'), recursive=True)) > 0
+    import evaluate
+    evaluate.main(['--config', cfg_path, '--checkpoint_logdir', cfg.logdir, '--single_gpu',
+                   '--logdir', str(tmp_path / 'eval'), '--num_workers', '0'])
