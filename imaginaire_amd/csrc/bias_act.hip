@@ -110,12 +110,23 @@ bias_act_bwd_nchw(const T* __restrict__ out, const T* __restrict__ dy, T* __rest
   }
 }
 
-__global__ void col_sum(const float* __restrict__ partial, int P, int C, float* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// Column sums of a [P, C] fp32 matrix: block = 64 columns x 8 row-groups
+// (coalesced along C), row-groups combined through LDS.
+constexpr int kColRows = 8;
+__global__ void __launch_bounds__(64 * kColRows)
+col_sum(const float* __restrict__ partial, int P, int C, float* __restrict__ out) {
+  __shared__ float sh[kColRows][64];
+  const int lane = threadIdx.x, row = threadIdx.y;
+  const int c = blockIdx.x * 64 + lane;
   float t = 0.f;
-  for (int p = 0; p < P; ++p) t += partial[(int64_t)p * C + c];
-  out[c] = t;
+  if (c < C)
+    for (int p = row; p < P; p += kColRows) t += partial[(int64_t)p * C + c];
+  sh[row][lane] = t;
+  __syncthreads();
+  if (row == 0 && c < C) {
+    for (int k = 1; k < kColRows; ++k) t += sh[k][lane];
+    out[c] = t;
+  }
 }
 
 bool is_cl(const at::Tensor& x) {
@@ -228,7 +239,7 @@ std::vector<at::Tensor> bias_act_bwd(const at::Tensor& out, const at::Tensor& dy
   });
   IAMD_LAUNCH_CHECK();
   auto db = at::empty({C}, fopt);
-  hipLaunchKernelGGL(col_sum, dim3(ceil_div(C, 256)), dim3(256), 0, stream(),
+  hipLaunchKernelGGL(col_sum, dim3(ceil_div(C, 64)), dim3(64, kColRows), 0, stream(),
                      partial.data_ptr<float>(), P, C, db.data_ptr<float>());
   IAMD_LAUNCH_CHECK();
   return {dx, db};

@@ -162,24 +162,39 @@ stats_partial_nchw(const T* __restrict__ x, int C, int HW, int P, int chunk,
 
 // Merge partials [N][P][C] -> per-group (count, mean, var) and fold the
 // per-channel affine (a, b) into scale/shift. G = N (instance) or 1 (batch).
-__global__ void stats_finalize(const float* __restrict__ pcnt, const float* __restrict__ pmean,
-                               const float* __restrict__ pm2, int N, int P, int C, int per_instance,
-                               float eps, const float* __restrict__ weight,
-                               const float* __restrict__ bias, float* __restrict__ out_cnt,
-                               float* __restrict__ out_mean, float* __restrict__ out_var,
-                               float* __restrict__ out_scale, float* __restrict__ out_shift) {
-  const int G = per_instance ? N : 1;
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= G * C) return;
-  const int g = idx / C, c = idx % C;
-  float n_a = 0.f, mean_a = 0.f, m2_a = 0.f;
+// Parallel merge: block = 64 channels (one wave across channels -> coalesced
+// partial reads) x kFinRows row-groups, each row-group Chan-merges a strided
+// subset of the N*P partial rows, then the row-groups merge through LDS.
+// Grid = (ceil(C/64), G). Replaces a one-thread-per-channel serial merge.
+constexpr int kFinRows = 8;
+__global__ void __launch_bounds__(64 * kFinRows)
+stats_finalize(const float* __restrict__ pcnt, const float* __restrict__ pmean,
+               const float* __restrict__ pm2, int N, int P, int C, int per_instance,
+               float eps, const float* __restrict__ weight,
+               const float* __restrict__ bias, float* __restrict__ out_cnt,
+               float* __restrict__ out_mean, float* __restrict__ out_var,
+               float* __restrict__ out_scale, float* __restrict__ out_shift) {
+  __shared__ float sh_n[kFinRows][64], sh_mean[kFinRows][64], sh_m2[kFinRows][64];
+  const int lane = threadIdx.x, row = threadIdx.y;
+  const int c = blockIdx.x * 64 + lane;
+  const int g = blockIdx.y;
   const int n_lo = per_instance ? g : 0, n_hi = per_instance ? g + 1 : N;
-  for (int n = n_lo; n < n_hi; ++n) {
-    for (int p = 0; p < P; ++p) {
-      const int64_t o = ((int64_t)n * P + p) * C + c;
+  const int rows = (n_hi - n_lo) * P;
+  float n_a = 0.f, mean_a = 0.f, m2_a = 0.f;
+  if (c < C) {
+    for (int r = row; r < rows; r += kFinRows) {
+      const int64_t o = ((int64_t)(n_lo * P + r)) * C + c;
       chan_merge(n_a, mean_a, m2_a, pcnt[o], pmean[o], pm2[o]);
     }
   }
+  sh_n[row][lane] = n_a;
+  sh_mean[row][lane] = mean_a;
+  sh_m2[row][lane] = m2_a;
+  __syncthreads();
+  if (row != 0 || c >= C) return;
+  for (int k = 1; k < kFinRows; ++k)
+    chan_merge(n_a, mean_a, m2_a, sh_n[k][lane], sh_mean[k][lane], sh_m2[k][lane]);
+  const int idx = g * C + c;
   const float var = n_a > 0.f ? m2_a / n_a : 0.f;
   out_cnt[idx] = n_a;
   out_mean[idx] = mean_a;
@@ -404,16 +419,23 @@ bwd_reduce(const T* __restrict__ x, const T* __restrict__ dout, int N, int C, in
 }
 
 // Sum partials over the chunk axis: [N][P][C] -> [N][C].
-__global__ void sum_partials(const float* __restrict__ ps, int Q, int64_t qstride, int N, int P,
-                             int C, float* __restrict__ out) {
-  // ps: Q planes of [N][P][C] (plane stride qstride) -> out: Q planes of [N][C]
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= N * C) return;
-  const int n = idx / C, c = idx % C;
-  for (int q = 0; q < Q; ++q) {
-    float t = 0.f;
-    for (int p = 0; p < P; ++p) t += ps[q * qstride + ((int64_t)n * P + p) * C + c];
-    out[(int64_t)q * N * C + idx] = t;
+// ps: Q planes of [N][P][C] (plane stride qstride) -> out: Q planes of [N][C].
+// Block = 64 channels x kFinRows partial-row groups; grid = (ceil(C/64), N, Q).
+__global__ void __launch_bounds__(64 * kFinRows)
+sum_partials(const float* __restrict__ ps, int Q, int64_t qstride, int N, int P, int C,
+             float* __restrict__ out) {
+  __shared__ float sh[kFinRows][64];
+  const int lane = threadIdx.x, row = threadIdx.y;
+  const int c = blockIdx.x * 64 + lane;
+  const int n = blockIdx.y, q = blockIdx.z;
+  float t = 0.f;
+  if (c < C)
+    for (int p = row; p < P; p += kFinRows) t += ps[q * qstride + ((int64_t)n * P + p) * C + c];
+  sh[row][lane] = t;
+  __syncthreads();
+  if (row == 0 && c < C) {
+    for (int k = 1; k < kFinRows; ++k) t += sh[k][lane];
+    out[(int64_t)q * N * C + (int64_t)n * C + c] = t;
   }
 }
 
@@ -605,8 +627,7 @@ std::vector<at::Tensor> norm_stats(const at::Tensor& x, bool per_instance, doubl
   at::Tensor wf, bf;
   if (weight.has_value() && weight->defined()) { wf = weight->contiguous().to(at::kFloat); wp = wf.data_ptr<float>(); }
   if (bias.has_value() && bias->defined()) { bf = bias->contiguous().to(at::kFloat); bp = bf.data_ptr<float>(); }
-  const int nthreads = 256;
-  hipLaunchKernelGGL(stats_finalize, dim3(ceil_div((int64_t)G * g.C, nthreads)), dim3(nthreads), 0,
+  hipLaunchKernelGGL(stats_finalize, dim3(ceil_div(g.C, 64), G), dim3(64, kFinRows), 0,
                      stream(), pcnt.data_ptr<float>(), pmean.data_ptr<float>(),
                      pm2.data_ptr<float>(), g.N, P, g.C, per_instance ? 1 : 0, (float)eps, wp, bp,
                      cnt.data_ptr<float>(), mean.data_ptr<float>(), var.data_ptr<float>(),
@@ -728,7 +749,7 @@ std::vector<at::Tensor> norm_bwd_reduce(const at::Tensor& x, const at::Tensor& d
   });
   IAMD_LAUNCH_CHECK();
   auto sums = at::empty({Q, g.N, g.C}, fopt);
-  hipLaunchKernelGGL(sum_partials, dim3(ceil_div((int64_t)g.N * g.C, 256)), dim3(256), 0, stream(),
+  hipLaunchKernelGGL(sum_partials, dim3(ceil_div(g.C, 64), g.N, Q), dim3(64, kFinRows), 0, stream(),
                      ps1, Q, qs, g.N, P, g.C, sums.data_ptr<float>());
   IAMD_LAUNCH_CHECK();
   // (S1, S2[, S3 = dgamma, S4 = dbeta for broadcast modulation]), each [N, C]
