@@ -22,6 +22,7 @@ import time
 import torch
 from torch import nn
 
+from imaginaire_amd.utils import trace
 from imaginaire_amd.utils.distributed import is_master, master_only
 from imaginaire_amd.utils.distributed import master_only_print as print
 from imaginaire_amd.utils.io import save_pilimage_in_jpeg
@@ -357,22 +358,26 @@ class BaseTrainer(object):
         requires_grad(self.net_G_module, True)
         requires_grad(self.net_D, False)
         self.forw_time = self._sync()
-        with self.autocast():
+        with trace.phase('gen/forward'), self.autocast():
             total_loss = self.gen_forward(data)
         if total_loss is None:
             return
         self.back_time = self._sync()
-        _ddp_call(self.net_G, 'begin')
-        total_loss.backward()
-        _ddp_call(self.net_G, 'finish')
+        with trace.phase('gen/backward'):
+            _ddp_call(self.net_G, 'begin')
+            total_loss.backward()
+            _ddp_call(self.net_G, 'finish')
         if hasattr(self.cfg.gen_opt, 'clip_grad_norm'):
             nn.utils.clip_grad_norm_(self.net_G_module.parameters(),
                                      self.cfg.gen_opt.clip_grad_norm)
         self.step_time = self._sync()
-        self.opt_G.step()
+        with trace.phase('gen/step'):
+            if self._step_ok(total_loss):
+                self.opt_G.step()
         self.avg_time = self._sync()
         if self.cfg.trainer.model_average:
-            self.net_G.module.update_average()
+            with trace.phase('gen/ema'):
+                self.net_G.module.update_average()
         self._detach_losses()
         self._time_before_leave_gen()
 
@@ -384,18 +389,33 @@ class BaseTrainer(object):
         requires_grad(self.net_G_module, False)
         requires_grad(self.net_D, True)
         self.forw_time = self._sync()
-        with self.autocast():
+        with trace.phase('dis/forward'), self.autocast():
             total_loss = self.dis_forward(data)
         if total_loss is None:
             return
         self.back_time = self._sync()
-        _ddp_call(self.net_D, 'begin')
-        total_loss.backward()
-        _ddp_call(self.net_D, 'finish')
+        with trace.phase('dis/backward'):
+            _ddp_call(self.net_D, 'begin')
+            total_loss.backward()
+            _ddp_call(self.net_D, 'finish')
         self.step_time = self._sync()
-        self.opt_D.step()
+        with trace.phase('dis/step'):
+            if self._step_ok(total_loss):
+                self.opt_D.step()
         self._detach_losses()
         self._time_before_leave_dis()
+
+    def _step_ok(self, total_loss):
+        """Optional non-finite-loss guard (``trainer.skip_nonfinite_steps``): the
+        bf16 counterpart of apex's dynamic-loss-scale overflow skip. Costs one
+        device->host sync per update, so it is off by default."""
+        if not getattr(self.cfg.trainer, 'skip_nonfinite_steps', False):
+            return True
+        ok = bool(torch.isfinite(total_loss.detach()).all())
+        if not ok:
+            print('Non-finite loss at iteration {}; skipping the optimizer step.'.format(
+                self.current_iteration))
+        return ok
 
     def dis_forward(self, data):
         raise NotImplementedError
