@@ -42,6 +42,9 @@ def parse():
                    help='self-baseline: PyTorch reference ops instead of the HIP kernels')
     p.add_argument('--profile-phases', action='store_true')
     p.add_argument('--verbose', action='store_true')
+    p.add_argument('--torch-profile', action='store_true',
+                   help='after warm-up, profile one step on the host (torch.profiler, CPU '
+                        'activities) and print the top operators to stderr')
     return p.parse_args()
 
 
@@ -73,6 +76,8 @@ def main():
     cfg.logdir = os.path.join('/tmp', 'imaginaire_amd_bench')
     if args.batch:
         cfg.data.train.batch_size = args.batch
+    if args.profile_phases:
+        cfg.speed_benchmark = True  # synchronised per-phase timers in the trainer
     bs = cfg.data.train.batch_size
     net_G, net_D, opt_G, opt_D, sch_G, sch_D = get_model_optimizer_and_scheduler(cfg, seed=0)
     trainer = get_trainer(cfg, net_G, net_D, opt_G, opt_D, sch_G, sch_D,
@@ -92,12 +97,23 @@ def main():
         if rank == 0:
             print('[bench] warmup {} done'.format(it), flush=True)
 
+    if args.torch_profile and rank == 0:
+        from torch.profiler import ProfilerActivity, profile
+        torch.cuda.synchronize()
+        with profile(activities=[ProfilerActivity.CPU], with_stack=False) as prof:
+            step(args.warmup)
+            torch.cuda.synchronize()
+        print(prof.key_averages().table(sort_by='self_cpu_time_total', row_limit=45),
+              flush=True)
+
     def barrier():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
 
     barrier()
+    if args.profile_phases:
+        trainer._reset_speed_accumulators()
     if args.verbose:
         try:  # phase marker for scripts/gpu/summarize_kernels.py (steady-state split)
             from imaginaire_amd.ops import _ext
@@ -115,6 +131,12 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    if args.profile_phases and rank == 0:
+        n = args.steps
+        for k in ('gen_forw', 'gen_loss', 'gen_back', 'gen_step', 'gen_avg', 'dis_forw',
+                  'dis_loss', 'dis_back', 'dis_step'):
+            print('[bench] phase %-9s %8.1f ms/step' % (
+                k, getattr(trainer, 'accu_%s_iter_time' % k) / n * 1e3), flush=True)
     ms_per_step = elapsed / args.steps * 1e3
     value = world * bs * args.steps / elapsed
     mem_gb = torch.cuda.max_memory_allocated(device) / 2 ** 30
