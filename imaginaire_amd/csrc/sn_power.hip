@@ -1,0 +1,246 @@
+// k5b: batched spectral-norm power iteration for every SN layer of a network.
+//
+// PyTorch's spectral_norm runs, per layer and per forward, two GEMVs + two
+// normalisations + a dot (plus a weight reshape copy for channels-last
+// convs) — ~10 tiny launches per layer, ~4000 per SPADE forward, and under
+// autocast the GEMVs go through bf16 hipBLASLt with a host-side heuristic
+// query each call. Here ONE set of 4 launches covers all L layers, in fp32:
+//
+//   K1 colsum : t_l  = W_l^T u_l                 (column-parallel, coalesced)
+//   K2 tnorm  : |t_l|^2                           (one block per layer)
+//   K3 rows   : s_l  = W_l (t_l / max(|t_l|,eps)) (one wave per row)
+//   K4 final  : u_l <- s_l / max(|s_l|,eps), v_l <- t_l / max(|t_l|,eps),
+//               sigma_l = u_l . s_l               (one block per layer)
+//
+// With update=false (eval) K1/K2 are skipped and K3 uses v_l directly:
+// sigma_l = u_l . (W_l v_l), u/v untouched — exactly torch's semantics.
+// Weights may be channels-last: memory column (kh,kw,ci) maps to logical
+// column (ci,kh,kw) so u/v keep the reference (logical) order.
+#include "common.h"
+
+#include <mutex>
+#include <unordered_map>
+
+namespace iamd {
+namespace {
+
+constexpr int kT = 256;
+constexpr int kColTile = 256;     // columns per K1 block
+constexpr int kRowsPerSplit = 64; // rows per K1 block
+constexpr int kRowsPerBlock = 4;  // rows (waves) per K3 block
+
+struct SnEntry {
+  const float* W;
+  float* u;
+  float* v;
+  float* t;  // workspace [w]
+  float* s;  // workspace [h]
+  int64_t h, w;
+  int64_t cl_cin, cl_khw;  // channels-last mapping (0 = none)
+};
+
+__device__ __forceinline__ int64_t logical_col(const SnEntry& e, int64_t c) {
+  return e.cl_cin ? (c % e.cl_cin) * e.cl_khw + c / e.cl_cin : c;
+}
+
+__device__ float block_sum(float v, float* sh) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float s = 0.f;
+  if (threadIdx.x == 0)
+    for (int k = 0; k < kT / 64; ++k) s += sh[k];
+  __syncthreads();
+  if (threadIdx.x == 0) sh[0] = s;
+  __syncthreads();
+  s = sh[0];
+  __syncthreads();
+  return s;
+}
+
+// blocks: {layer, col_tile, row_split}
+__global__ void __launch_bounds__(kT) sn_colsum(const SnEntry* __restrict__ ents,
+                                                 const int* __restrict__ blocks) {
+  const int* bm = blocks + 3 * blockIdx.x;
+  const SnEntry e = ents[bm[0]];
+  const int64_t c = (int64_t)bm[1] * kColTile + threadIdx.x;
+  if (c >= e.w) return;
+  const int64_t r0 = (int64_t)bm[2] * kRowsPerSplit;
+  const int64_t r1 = min(e.h, r0 + kRowsPerSplit);
+  float acc = 0.f;
+  for (int64_t r = r0; r < r1; ++r) acc = fmaf(e.W[r * e.w + c], e.u[r], acc);
+  atomicAdd(e.t + logical_col(e, c), acc);
+}
+
+// one block per layer: sums of squares of t -> scal[l*4 + 0]
+__global__ void __launch_bounds__(kT) sn_tnorm(const SnEntry* __restrict__ ents,
+                                                float* __restrict__ scal) {
+  __shared__ float sh[kT / 64];
+  const SnEntry e = ents[blockIdx.x];
+  float acc = 0.f;
+  for (int64_t c = threadIdx.x; c < e.w; c += kT) acc = fmaf(e.t[c], e.t[c], acc);
+  acc = block_sum(acc, sh);
+  if (threadIdx.x == 0) scal[4 * blockIdx.x] = acc;
+}
+
+// blocks: {layer, first_row}; one wave per row. Input vector: t/|t| (update) or v.
+__global__ void __launch_bounds__(64 * kRowsPerBlock) sn_rows(const SnEntry* __restrict__ ents,
+                                                               const int* __restrict__ blocks,
+                                                               const float* __restrict__ scal,
+                                                               int update, float eps) {
+  const int* bm = blocks + 2 * blockIdx.x;
+  const SnEntry e = ents[bm[0]];
+  const int64_t r = (int64_t)bm[1] + (threadIdx.x >> 6);
+  if (r >= e.h) return;
+  const int lane = threadIdx.x & 63;
+  const float* x = update ? e.t : e.v;
+  const float k = update ? 1.f / fmaxf(sqrtf(scal[4 * bm[0]]), eps) : 1.f;
+  const float* row = e.W + r * e.w;
+  float acc = 0.f;
+  for (int64_t c = lane; c < e.w; c += 64) acc = fmaf(row[c], x[logical_col(e, c)], acc);
+  acc = wave_sum(acc);
+  if (lane == 0) e.s[r] = acc * k;
+}
+
+// one block per layer: finalize u, v, sigma
+__global__ void __launch_bounds__(kT) sn_final(const SnEntry* __restrict__ ents,
+                                                float* __restrict__ scal,
+                                                float* __restrict__ sigma, int update,
+                                                float eps) {
+  __shared__ float sh[kT / 64];
+  const SnEntry e = ents[blockIdx.x];
+  if (update) {
+    float acc = 0.f;
+    for (int64_t r = threadIdx.x; r < e.h; r += kT) acc = fmaf(e.s[r], e.s[r], acc);
+    const float ss = block_sum(acc, sh);
+    const float inv_s = 1.f / fmaxf(sqrtf(ss), eps);
+    const float inv_t = 1.f / fmaxf(sqrtf(scal[4 * blockIdx.x]), eps);
+    for (int64_t r = threadIdx.x; r < e.h; r += kT) e.u[r] = e.s[r] * inv_s;
+    for (int64_t c = threadIdx.x; c < e.w; c += kT) e.v[c] = e.t[c] * inv_t;
+    if (threadIdx.x == 0) {
+      scal[4 * blockIdx.x + 1] = ss;
+      sigma[blockIdx.x] = ss * inv_s;  // u . s = |s|^2 / max(|s|, eps)
+    }
+  } else {
+    float acc = 0.f;
+    for (int64_t r = threadIdx.x; r < e.h; r += kT) acc = fmaf(e.u[r], e.s[r], acc);
+    const float d = block_sum(acc, sh);
+    if (threadIdx.x == 0) sigma[blockIdx.x] = d;
+  }
+}
+
+struct SnPlan {
+  at::Tensor ents;         // device SnEntry[L]
+  at::Tensor col_blocks;   // device int3
+  at::Tensor row_blocks;   // device int2
+  at::Tensor t_ws, s_ws;   // fp32 workspaces (flat)
+  int n_col_blocks, n_row_blocks, L;
+};
+
+std::mutex g_sn_mu;
+std::unordered_map<uint64_t, SnPlan> g_sn_cache;
+
+SnPlan& get_plan(const std::vector<at::Tensor>& W, const std::vector<at::Tensor>& U,
+                 const std::vector<at::Tensor>& V) {
+  uint64_t hsh = 0x51ed270b0b6e3a6dULL;
+  for (size_t i = 0; i < W.size(); ++i) {
+    hsh ^= reinterpret_cast<uint64_t>(W[i].data_ptr()) + 0x9e3779b97f4a7c15ULL + (hsh << 6);
+    hsh ^= reinterpret_cast<uint64_t>(U[i].data_ptr()) + (hsh >> 2);
+    hsh ^= reinterpret_cast<uint64_t>(V[i].data_ptr()) * 31 + (uint64_t)W[i].numel();
+  }
+  std::lock_guard<std::mutex> lk(g_sn_mu);
+  auto it = g_sn_cache.find(hsh);
+  if (it != g_sn_cache.end()) return it->second;
+  const int L = (int)W.size();
+  int64_t tot_w = 0, tot_h = 0;
+  for (int i = 0; i < L; ++i) {
+    tot_h += W[i].size(0);
+    tot_w += W[i].numel() / W[i].size(0);
+  }
+  SnPlan p;
+  auto fopt = W[0].options().dtype(at::kFloat);
+  p.t_ws = at::zeros({tot_w}, fopt);
+  p.s_ws = at::zeros({tot_h}, fopt);
+  std::vector<SnEntry> ents(L);
+  std::vector<int32_t> cb, rb;
+  int64_t ow = 0, oh = 0;
+  for (int i = 0; i < L; ++i) {
+    const at::Tensor& w = W[i];
+    IAMD_CHECK(w.scalar_type() == at::kFloat && w.is_non_overlapping_and_dense(),
+               "mt_sn_power: weights must be dense fp32");
+    IAMD_CHECK(U[i].is_contiguous() && V[i].is_contiguous(), "mt_sn_power: u/v contiguous");
+    SnEntry& e = ents[i];
+    e.W = w.data_ptr<float>();
+    e.u = U[i].data_ptr<float>();
+    e.v = V[i].data_ptr<float>();
+    e.h = w.size(0);
+    e.w = w.numel() / e.h;
+    IAMD_CHECK(U[i].numel() == e.h && V[i].numel() == e.w, "mt_sn_power: u/v sizes");
+    const bool cl = w.dim() == 4 && !w.is_contiguous() &&
+                    w.is_contiguous(at::MemoryFormat::ChannelsLast);
+    IAMD_CHECK(cl || w.is_contiguous(), "mt_sn_power: weight must be contiguous or CL");
+    e.cl_cin = cl ? w.size(1) : 0;
+    e.cl_khw = cl ? w.size(2) * w.size(3) : 0;
+    e.t = p.t_ws.data_ptr<float>() + ow;
+    e.s = p.s_ws.data_ptr<float>() + oh;
+    ow += e.w;
+    oh += e.h;
+    const int ntile = (int)((e.w + kColTile - 1) / kColTile);
+    const int nsplit = (int)((e.h + kRowsPerSplit - 1) / kRowsPerSplit);
+    for (int a = 0; a < ntile; ++a)
+      for (int b = 0; b < nsplit; ++b) {
+        cb.push_back(i);
+        cb.push_back(a);
+        cb.push_back(b);
+      }
+    for (int64_t r = 0; r < e.h; r += kRowsPerBlock) {
+      rb.push_back(i);
+      rb.push_back((int32_t)r);
+    }
+  }
+  auto pin = at::TensorOptions().dtype(at::kByte).pinned_memory(true);
+  auto dev = W[0].device();
+  auto stage = [&](const void* src, size_t bytes) {
+    auto h = at::empty({(int64_t)bytes}, pin);
+    memcpy(h.data_ptr(), src, bytes);
+    return h.to(dev, /*non_blocking=*/true);
+  };
+  p.ents = stage(ents.data(), ents.size() * sizeof(SnEntry));
+  p.col_blocks = stage(cb.data(), cb.size() * sizeof(int32_t)).view(at::kInt);
+  p.row_blocks = stage(rb.data(), rb.size() * sizeof(int32_t)).view(at::kInt);
+  p.n_col_blocks = (int)(cb.size() / 3);
+  p.n_row_blocks = (int)(rb.size() / 2);
+  p.L = L;
+  if (g_sn_cache.size() > 64) g_sn_cache.clear();
+  return g_sn_cache.emplace(hsh, std::move(p)).first->second;
+}
+
+}  // namespace
+
+// Returns sigma [L] (fp32). update=true runs one power iteration (u, v updated in place).
+at::Tensor mt_sn_power(const std::vector<at::Tensor>& weights, const std::vector<at::Tensor>& us,
+                       const std::vector<at::Tensor>& vs, bool update, double eps) {
+  IAMD_CHECK(!weights.empty() && weights.size() == us.size() && us.size() == vs.size(),
+             "mt_sn_power: list sizes");
+  SnPlan& p = get_plan(weights, us, vs);
+  auto fopt = weights[0].options().dtype(at::kFloat);
+  auto sigma = at::empty({p.L}, fopt);
+  auto scal = at::empty({p.L, 4}, fopt);
+  const auto* ents = reinterpret_cast<const SnEntry*>(p.ents.data_ptr());
+  hipStream_t st = stream();
+  if (update) {
+    IAMD_HIP_CHECK(hipMemsetAsync(p.t_ws.data_ptr(), 0, p.t_ws.numel() * sizeof(float), st));
+    hipLaunchKernelGGL(sn_colsum, dim3(p.n_col_blocks), dim3(kT), 0, st, ents,
+                       p.col_blocks.data_ptr<int>());
+    hipLaunchKernelGGL(sn_tnorm, dim3(p.L), dim3(kT), 0, st, ents, scal.data_ptr<float>());
+  }
+  hipLaunchKernelGGL(sn_rows, dim3(p.n_row_blocks), dim3(64 * kRowsPerBlock), 0, st, ents,
+                     p.row_blocks.data_ptr<int>(), scal.data_ptr<float>(), update ? 1 : 0,
+                     (float)eps);
+  hipLaunchKernelGGL(sn_final, dim3(p.L), dim3(kT), 0, st, ents, scal.data_ptr<float>(),
+                     sigma.data_ptr<float>(), update ? 1 : 0, (float)eps);
+  IAMD_LAUNCH_CHECK();
+  return sigma;
+}
+
+}  // namespace iamd

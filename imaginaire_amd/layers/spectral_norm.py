@@ -1,0 +1,145 @@
+"""Spectral normalisation, MI355X execution (reference layers/weight_norm.py:84-85,
+which wraps ``torch.nn.utils.spectral_norm``).
+
+Same parametrisation and state-dict layout as PyTorch's ``spectral_norm``
+(``weight_orig`` / ``weight_u`` / ``weight_v``, the same hooks), so
+checkpoints interchange with the reference. Two changes in how it runs:
+
+* **fp32, outside autocast.** Under bf16 autocast PyTorch's power iteration
+  runs its GEMVs in bf16 through hipBLASLt (with a host-side heuristic query
+  per call) — numerically worse and measured as the dominant host cost of a
+  SPADE forward on MI355X (profiles/spade_step_phases_mi355x.txt).
+* **Batched per network.** ``install_batched_spectral_norm(net)`` registers a
+  forward pre-hook on the network that runs ONE power iteration for every SN
+  layer of the network with the k5b HIP kernels (``mt_sn_power``: 4 launches
+  in total instead of ~10 per layer) and hands each layer its σ; the layer
+  then forms ``W / σ`` with an autograd function whose backward is exactly
+  the gradient of PyTorch's ``W / (uᵀ W v)`` (u, v constant). A layer called
+  again within the same network forward (weight sharing) falls back to its
+  own power iteration — again the reference's behaviour.
+"""
+import torch
+from torch.nn.utils.spectral_norm import (SpectralNorm as _TorchSN,
+                                          SpectralNormLoadStateDictPreHook,
+                                          SpectralNormStateDictHook)
+import torch.nn.functional as F
+
+from imaginaire_amd.ops import _ext
+
+
+class _SNScale(torch.autograd.Function):
+    """W / σ with σ = uᵀ W v (u, v constants): dW = G/σ − (⟨G, W⟩/σ²) u vᵀ."""
+
+    @staticmethod
+    def forward(ctx, weight, u, v, sigma):
+        ctx.save_for_backward(weight, u, v, sigma)
+        return weight / sigma
+
+    @staticmethod
+    def backward(ctx, grad):
+        weight, u, v, sigma = ctx.saved_tensors
+        g = grad.float()
+        dot = (g * weight).sum()
+        outer = torch.outer(u, v).view(weight.shape)
+        dw = g / sigma - (dot / (sigma * sigma)) * outer
+        return dw.to(weight.dtype), None, None, None
+
+
+class SpectralNorm(_TorchSN):
+    def compute_weight(self, module, do_power_iteration):
+        batched = getattr(self, '_batched', None)
+        if batched is not None:
+            self._batched = None  # consumed: a second call this forward iterates itself
+            weight = getattr(module, self.name + '_orig')
+            u, v, sigma = batched
+            return _SNScale.apply(weight, u, v, sigma)
+        dev = getattr(module, self.name + '_orig').device.type
+        with torch.autocast(device_type=dev, enabled=False):
+            return super().compute_weight(module, do_power_iteration)
+
+    @classmethod
+    def apply(cls, module, name, n_power_iterations, dim, eps):
+        for hook in module._forward_pre_hooks.values():
+            if isinstance(hook, _TorchSN) and hook.name == name:
+                raise RuntimeError('Cannot register two spectral_norm hooks on the same '
+                                   'parameter {}'.format(name))
+        fn = cls(name, n_power_iterations, dim, eps)
+        weight = module._parameters[name]
+        with torch.no_grad():
+            weight_mat = fn.reshape_weight_to_matrix(weight)
+            h, w = weight_mat.size()
+            u = F.normalize(weight.new_empty(h).normal_(0, 1), dim=0, eps=fn.eps)
+            v = F.normalize(weight.new_empty(w).normal_(0, 1), dim=0, eps=fn.eps)
+        delattr(module, fn.name)
+        module.register_parameter(fn.name + '_orig', weight)
+        setattr(module, fn.name, weight.data)
+        module.register_buffer(fn.name + '_u', u)
+        module.register_buffer(fn.name + '_v', v)
+        module.register_forward_pre_hook(fn)
+        module._register_state_dict_hook(SpectralNormStateDictHook(fn))
+        module._register_load_state_dict_pre_hook(SpectralNormLoadStateDictPreHook(fn))
+        return fn
+
+
+def spectral_norm(module, name='weight', n_power_iterations=1, eps=1e-12, dim=None):
+    """Drop-in for ``torch.nn.utils.spectral_norm`` using :class:`SpectralNorm`."""
+    if dim is None:
+        dim = 1 if isinstance(module, (torch.nn.ConvTranspose1d, torch.nn.ConvTranspose2d,
+                                       torch.nn.ConvTranspose3d)) else 0
+    SpectralNorm.apply(module, name, n_power_iterations, dim, eps)
+    return module
+
+
+class _SNGroup:
+    """Forward pre-hook of a network: one batched power iteration for all of
+    its (dim-0, single-iteration) SN layers."""
+
+    def __init__(self, net):
+        self.entries = self._collect(net)
+
+    @staticmethod
+    def _collect(net):
+        entries = []
+        for m in net.modules():
+            for hook in m._forward_pre_hooks.values():
+                if isinstance(hook, SpectralNorm) and hook.dim == 0 and \
+                        hook.n_power_iterations == 1:
+                    entries.append((m, hook))
+        return entries
+
+    def __call__(self, net, inputs):
+        ends = (self.entries[0], self.entries[-1]) if self.entries else ()
+        if not all(hasattr(m, h.name + '_orig') for m, h in ends):
+            self.entries = self._collect(net)  # SN removed/added since (e.g. EMA copy)
+        if not self.entries:
+            return
+        w0 = getattr(self.entries[0][0], self.entries[0][1].name + '_orig')
+        if not _ext.use_native(w0):
+            return
+        ws, us, vs = [], [], []
+        for m, h in self.entries:
+            ws.append(getattr(m, h.name + '_orig'))
+            us.append(getattr(m, h.name + '_u'))
+            vs.append(getattr(m, h.name + '_v'))
+        if any(w.dtype != torch.float32 for w in ws):
+            return
+        with torch.no_grad():
+            sigma = _ext.ext().mt_sn_power(ws, us, vs, bool(net.training),
+                                           float(self.entries[0][1].eps))
+            # snapshots of u, v for the backward (the next forward updates them in place)
+            u_all = torch.cat(us)
+            v_all = torch.cat(vs)
+        ou = ov = 0
+        for i, (m, h) in enumerate(self.entries):
+            nu, nv = us[i].numel(), vs[i].numel()
+            h._batched = (u_all[ou:ou + nu], v_all[ov:ov + nv], sigma[i])
+            ou += nu
+            ov += nv
+
+
+def install_batched_spectral_norm(net):
+    """Register the batched SN pre-hook on ``net``; returns the number of layers covered."""
+    group = _SNGroup(net)
+    if group.entries:
+        net.register_forward_pre_hook(group)
+    return len(group.entries)

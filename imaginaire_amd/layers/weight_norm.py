@@ -9,10 +9,11 @@ import functools
 
 import torch
 from torch import nn
-from torch.nn.utils import spectral_norm, weight_norm
+from torch.nn.utils import weight_norm
 from torch.nn.utils.spectral_norm import SpectralNorm as _TorchSN
 
 from .conv import LinearBlock
+from .spectral_norm import spectral_norm
 
 
 from torch.nn.utils.weight_norm import WeightNorm as _TorchWN

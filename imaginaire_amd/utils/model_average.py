@@ -38,6 +38,15 @@ def _drop_sn_load_hooks(m):
             del m._load_state_dict_pre_hooks[k]
 
 
+def _drop_sn_group_hooks(net):
+    """The deep-copied EMA network has no SN layers left: drop the batched-SN
+    pre-hook it inherited from the source network."""
+    from imaginaire_amd.layers.spectral_norm import _SNGroup
+    for k, h in list(net._forward_pre_hooks.items()):
+        if isinstance(h, _SNGroup):
+            del net._forward_pre_hooks[k]
+
+
 class ModelAverage(nn.Module):
     def __init__(self, module, beta=0.9999, start_iteration=1000, remove_sn=True):
         super().__init__()
@@ -56,6 +65,7 @@ class ModelAverage(nn.Module):
                     remove_spectral_norm(m)
                     _drop_sn_load_hooks(m)
             self.averaged_model.apply(fn_remove_sn)
+            _drop_sn_group_hooks(self.averaged_model)
             self.dim = 0
         else:
             self.averaged_model.eval()

@@ -233,3 +233,35 @@ def test_channelnorm_resample2d(layout):
     o = _Resample2dFn.apply(img, flow, 1)
     o_ref = resample2d_reference(img.detach(), flow.detach(), 1)
     assert torch.allclose(o, o_ref, atol=1e-5)
+
+
+@pytest.mark.parametrize('training', [True, False])
+def test_batched_spectral_norm_matches_torch(training):
+    """k5b batched power iteration + _SNScale autograd == torch.nn.utils.spectral_norm (fp32)."""
+    import copy
+    from torch import nn
+    from imaginaire_amd.layers.spectral_norm import install_batched_spectral_norm, spectral_norm
+    torch.manual_seed(5)
+
+    def make(sn):
+        return nn.Sequential(sn(nn.Conv2d(6, 16, 3, padding=1)), nn.LeakyReLU(0.2),
+                             sn(nn.Conv2d(16, 8, 5, padding=2)), nn.Flatten(),
+                             sn(nn.Linear(8 * 6 * 6, 10)))
+    ref = make(torch.nn.utils.spectral_norm).cuda()
+    net = make(spectral_norm).cuda()
+    net.load_state_dict(ref.state_dict())
+    net = net.to(memory_format=torch.channels_last)
+    assert install_batched_spectral_norm(net) == 3
+    ref.train(training)
+    net.train(training)
+    x = torch.randn(4, 6, 6, 6, device='cuda')
+    y_ref = ref(x)
+    y = net(x.contiguous(memory_format=torch.channels_last))
+    assert torch.allclose(y, y_ref, atol=1e-4, rtol=1e-4), (y - y_ref).abs().max()
+    g = torch.randn_like(y)
+    y_ref.backward(g)
+    y.backward(g)
+    for (n, p), (_, pr) in zip(net.named_parameters(), ref.named_parameters()):
+        assert torch.allclose(p.grad, pr.grad, atol=1e-4, rtol=1e-3), n
+    for (n, b), (_, br) in zip(net.named_buffers(), ref.named_buffers()):
+        assert torch.allclose(b, br, atol=1e-5, rtol=1e-4), n
