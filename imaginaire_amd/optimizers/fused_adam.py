@@ -55,13 +55,16 @@ class FusedAdam(Optimizer):
             if isinstance(lr, torch.Tensor):
                 lr = float(lr)
             native = _ext.use_native(params[0]) and all(
-                p.dtype == torch.float32 and p.is_contiguous() for p in params)
+                p.dtype == torch.float32 and p.is_non_overlapping_and_dense() for p in params)
             if native:
                 gdt = grads[0].dtype
-                gl = [g if (g.dtype == gdt and g.is_contiguous()) else g.contiguous().to(gdt)
-                      for g in grads]
                 if gdt not in (torch.float32, torch.bfloat16):
-                    gl = [g.float() for g in gl]
+                    gdt = torch.float32
+                # grads must walk memory in the same order as their params
+                # (channels-last conv weights): re-lay out only mismatching ones
+                gl = [g if (g.dtype == gdt and g.stride() == p.stride())
+                      else torch.empty_like(p, dtype=gdt).copy_(g)
+                      for g, p in zip(grads, params)]
                 _ext.ext().mt_adam(params, gl, m, v, [], lr, beta1, beta2, eps, int(step), wd,
                                    bool(adamw), 1.0)
             else:
