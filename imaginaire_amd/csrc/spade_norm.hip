@@ -167,6 +167,41 @@ stats_partial_nchw(const T* __restrict__ x, int C, int HW, int P, int chunk,
 // subset of the N*P partial rows, then the row-groups merge through LDS.
 // Grid = (ceil(C/64), G). Replaces a one-thread-per-channel serial merge.
 constexpr int kFinRows = 8;
+// Stage 1 of the partial merge (latency hiding): grid (ceil(C/64), G, RS); each
+// block Chan-merges its slice of the N*P partial rows of group g into one
+// (count, mean, M2) row of tmp [G][RS][C]. Stage 2 (stats_finalize) merges RS.
+__global__ void __launch_bounds__(64 * kFinRows)
+stats_merge_rows(const float* __restrict__ pcnt, const float* __restrict__ pmean,
+                 const float* __restrict__ pm2, int N, int P, int C, int per_instance, int RS,
+                 float* __restrict__ tcnt, float* __restrict__ tmean, float* __restrict__ tm2) {
+  __shared__ float sh_n[kFinRows][64], sh_mean[kFinRows][64], sh_m2[kFinRows][64];
+  const int lane = threadIdx.x, row = threadIdx.y;
+  const int c = blockIdx.x * 64 + lane;
+  const int g = blockIdx.y, rs = blockIdx.z;
+  const int n_lo = per_instance ? g : 0, n_hi = per_instance ? g + 1 : N;
+  const int rows = (n_hi - n_lo) * P;
+  const int per = (rows + RS - 1) / RS;
+  const int r0 = rs * per, r1 = min(rows, r0 + per);
+  float n_a = 0.f, mean_a = 0.f, m2_a = 0.f;
+  if (c < C) {
+    for (int r = r0 + row; r < r1; r += kFinRows) {
+      const int64_t o = ((int64_t)(n_lo * P + r)) * C + c;
+      chan_merge(n_a, mean_a, m2_a, pcnt[o], pmean[o], pm2[o]);
+    }
+  }
+  sh_n[row][lane] = n_a;
+  sh_mean[row][lane] = mean_a;
+  sh_m2[row][lane] = m2_a;
+  __syncthreads();
+  if (row != 0 || c >= C) return;
+  for (int k = 1; k < kFinRows; ++k)
+    chan_merge(n_a, mean_a, m2_a, sh_n[k][lane], sh_mean[k][lane], sh_m2[k][lane]);
+  const int64_t o = ((int64_t)g * RS + rs) * C + c;
+  tcnt[o] = n_a;
+  tmean[o] = mean_a;
+  tm2[o] = m2_a;
+}
+
 __global__ void __launch_bounds__(64 * kFinRows)
 stats_finalize(const float* __restrict__ pcnt, const float* __restrict__ pmean,
                const float* __restrict__ pm2, int N, int P, int C, int per_instance,
@@ -422,20 +457,25 @@ bwd_reduce(const T* __restrict__ x, const T* __restrict__ dout, int N, int C, in
 // ps: Q planes of [N][P][C] (plane stride qstride) -> out: Q planes of [N][C].
 // Block = 64 channels x kFinRows partial-row groups; grid = (ceil(C/64), N, Q).
 __global__ void __launch_bounds__(64 * kFinRows)
-sum_partials(const float* __restrict__ ps, int Q, int64_t qstride, int N, int P, int C,
+sum_partials(const float* __restrict__ ps, int Q, int64_t qstride, int N, int P, int C, int RS,
              float* __restrict__ out) {
+  // grid (ceil(C/64), N, Q*RS): RS row-splits per (n, q) accumulate into a zeroed out
   __shared__ float sh[kFinRows][64];
   const int lane = threadIdx.x, row = threadIdx.y;
   const int c = blockIdx.x * 64 + lane;
-  const int n = blockIdx.y, q = blockIdx.z;
+  const int n = blockIdx.y, q = blockIdx.z / RS, rs = blockIdx.z % RS;
+  const int per = (P + RS - 1) / RS;
+  const int p0 = rs * per, p1 = min(P, p0 + per);
   float t = 0.f;
   if (c < C)
-    for (int p = row; p < P; p += kFinRows) t += ps[q * qstride + ((int64_t)n * P + p) * C + c];
+    for (int p = p0 + row; p < p1; p += kFinRows)
+      t += ps[q * qstride + ((int64_t)n * P + p) * C + c];
   sh[row][lane] = t;
   __syncthreads();
   if (row == 0 && c < C) {
     for (int k = 1; k < kFinRows; ++k) t += sh[k][lane];
-    out[(int64_t)q * N * C + (int64_t)n * C + c] = t;
+    float* o = out + (int64_t)q * N * C + (int64_t)n * C + c;
+    if (RS == 1) *o = t; else atomicAdd(o, t);
   }
 }
 
@@ -627,11 +667,31 @@ std::vector<at::Tensor> norm_stats(const at::Tensor& x, bool per_instance, doubl
   at::Tensor wf, bf;
   if (weight.has_value() && weight->defined()) { wf = weight->contiguous().to(at::kFloat); wp = wf.data_ptr<float>(); }
   if (bias.has_value() && bias->defined()) { bf = bias->contiguous().to(at::kFloat); bp = bf.data_ptr<float>(); }
+  // two-stage merge: RS row-splits per group keep many CUs busy on the N*P partial rows
+  const int rows = (per_instance ? 1 : g.N) * P;
+  const int RS = std::max(1, std::min(32, rows / 16));
+  const float* mc = pcnt.data_ptr<float>();
+  const float* mm = pmean.data_ptr<float>();
+  const float* m2p = pm2.data_ptr<float>();
+  int fN = g.N, fP = P;
+  at::Tensor tc, tmn, tm2;
+  if (RS > 1) {
+    tc = at::empty({G, RS, g.C}, fopt);
+    tmn = at::empty({G, RS, g.C}, fopt);
+    tm2 = at::empty({G, RS, g.C}, fopt);
+    hipLaunchKernelGGL(stats_merge_rows, dim3(ceil_div(g.C, 64), G, RS), dim3(64, kFinRows), 0,
+                       stream(), mc, mm, m2p, g.N, P, g.C, per_instance ? 1 : 0, RS,
+                       tc.data_ptr<float>(), tmn.data_ptr<float>(), tm2.data_ptr<float>());
+    mc = tc.data_ptr<float>();
+    mm = tmn.data_ptr<float>();
+    m2p = tm2.data_ptr<float>();
+    fN = G;
+    fP = RS;
+  }
   hipLaunchKernelGGL(stats_finalize, dim3(ceil_div(g.C, 64), G), dim3(64, kFinRows), 0,
-                     stream(), pcnt.data_ptr<float>(), pmean.data_ptr<float>(),
-                     pm2.data_ptr<float>(), g.N, P, g.C, per_instance ? 1 : 0, (float)eps, wp, bp,
-                     cnt.data_ptr<float>(), mean.data_ptr<float>(), var.data_ptr<float>(),
-                     partial_only ? nullptr : scale.data_ptr<float>(),
+                     stream(), mc, mm, m2p, fN, fP, g.C, (per_instance || RS > 1) ? 1 : 0,
+                     (float)eps, wp, bp, cnt.data_ptr<float>(), mean.data_ptr<float>(),
+                     var.data_ptr<float>(), partial_only ? nullptr : scale.data_ptr<float>(),
                      partial_only ? nullptr : shift.data_ptr<float>());
   IAMD_LAUNCH_CHECK();
   return {cnt, mean, var, scale, shift};
@@ -748,9 +808,12 @@ std::vector<at::Tensor> norm_bwd_reduce(const at::Tensor& x, const at::Tensor& d
     }
   });
   IAMD_LAUNCH_CHECK();
-  auto sums = at::empty({Q, g.N, g.C}, fopt);
-  hipLaunchKernelGGL(sum_partials, dim3(ceil_div(g.C, 64), g.N, Q), dim3(64, kFinRows), 0, stream(),
-                     ps1, Q, qs, g.N, P, g.C, sums.data_ptr<float>());
+  // atomics across row-splits reorder fp32 sums: single split in deterministic mode
+  const int RSs = at::globalContext().deterministicAlgorithms()
+                      ? 1 : std::max(1, std::min(16, P / 16));
+  auto sums = RSs > 1 ? at::zeros({Q, g.N, g.C}, fopt) : at::empty({Q, g.N, g.C}, fopt);
+  hipLaunchKernelGGL(sum_partials, dim3(ceil_div(g.C, 64), g.N, Q * RSs), dim3(64, kFinRows), 0,
+                     stream(), ps1, Q, qs, g.N, P, g.C, RSs, sums.data_ptr<float>());
   IAMD_LAUNCH_CHECK();
   // (S1, S2[, S3 = dgamma, S4 = dbeta for broadcast modulation]), each [N, C]
   std::vector<at::Tensor> out;
