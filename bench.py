@@ -42,6 +42,11 @@ def parse():
                    help='self-baseline: PyTorch reference ops instead of the HIP kernels')
     p.add_argument('--profile-phases', action='store_true')
     p.add_argument('--verbose', action='store_true')
+    p.add_argument('--backend', default='nccl',
+                   help='process-group backend for N>1 (nccl = RCCL over xGMI; gloo for '
+                        'single-GPU multi-rank rehearsals with --share-gpu)')
+    p.add_argument('--share-gpu', action='store_true',
+                   help='testing only: every rank uses cuda:0 (rehearse the DDP path on one GPU)')
     p.add_argument('--torch-profile', action='store_true',
                    help='after warm-up, profile one step on the host (torch.profiler, CPU '
                         'activities) and print the top operators to stderr')
@@ -60,13 +65,15 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    if args.share_gpu:
+        local_rank = 0
     from imaginaire_amd.config import Config
     from imaginaire_amd.utils.distributed import init_dist
     from imaginaire_amd.utils.trainer import get_model_optimizer_and_scheduler, get_trainer
     from imaginaire_amd.datasets.synthetic import DeviceBatchSource
 
     if world > 1:
-        init_dist(local_rank, backend='nccl')
+        init_dist(local_rank, backend=args.backend)
     else:
         torch.cuda.set_device(local_rank)
     from imaginaire_amd.utils.cudnn import init_cudnn
