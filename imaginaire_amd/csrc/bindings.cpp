@@ -62,6 +62,8 @@ std::vector<at::Tensor> resample2d_backward(const at::Tensor& in1, const at::Ten
                                             const at::Tensor& dout, int64_t ks);
 void register_lmdb(pybind11::module_& m);
 void profile_marker(int64_t tag);
+std::vector<at::Tensor> mt_sn_scale_cast(const std::vector<at::Tensor>& weights,
+                                         const at::Tensor& sigma);
 at::Tensor mt_sn_power(const std::vector<at::Tensor>& weights, const std::vector<at::Tensor>& us,
                        const std::vector<at::Tensor>& vs, bool update, double eps);
 }  // namespace iamd
@@ -70,6 +72,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "imaginaire_amd gfx950 HIP kernels";
   iamd::register_lmdb(m);
   m.def("mt_sn_power", &iamd::mt_sn_power, "batched spectral-norm power iteration (k5b)");
+  m.def("mt_sn_scale_cast", &iamd::mt_sn_scale_cast, "batched W/sigma -> bf16 (k5c)");
   m.def("profile_marker", &iamd::profile_marker, "named no-op kernel for trace phase splits");
   m.def("norm_stats", &iamd::norm_stats, "per-(group,channel) statistics (k1)");
   m.def("norm_apply", &iamd::norm_apply, "norm + SPADE modulation + activation (k1 fwd)");

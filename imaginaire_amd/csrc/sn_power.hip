@@ -244,3 +244,103 @@ at::Tensor mt_sn_power(const std::vector<at::Tensor>& weights, const std::vector
 }
 
 }  // namespace iamd
+
+// ---------------------------------------------------------------------------
+// k5c: W_l / sigma_l for every SN layer, written straight into ONE flat bf16
+// buffer (the autocast compute dtype). Replaces a per-layer fp32 divide plus
+// autocast's per-layer fp32->bf16 cast (two launches and two fp32 passes per
+// layer per forward) with one launch. Layer l's output is a view at offset
+// off_l with W_l's strides (channels-last stays channels-last).
+// ---------------------------------------------------------------------------
+namespace iamd {
+namespace {
+
+constexpr int kScChunk = 256 * 8 * 8;
+
+struct ScEntry {
+  const float* W;
+  int64_t numel;
+  int64_t off;
+};
+
+__global__ void __launch_bounds__(kT) sn_scale_cast(const ScEntry* __restrict__ ents,
+                                                     const int* __restrict__ blocks,
+                                                     const float* __restrict__ sigma,
+                                                     __hip_bfloat16* __restrict__ out) {
+  const int t = blocks[2 * blockIdx.x], chunk = blocks[2 * blockIdx.x + 1];
+  const ScEntry e = ents[t];
+  const float inv = 1.f / sigma[t];
+  const int64_t start = (int64_t)chunk * kScChunk;
+  const int64_t end = min(e.numel, start + (int64_t)kScChunk);
+  __hip_bfloat16* o = out + e.off;
+  for (int64_t i = start + threadIdx.x; i < end; i += kT) o[i] = __float2bfloat16(e.W[i] * inv);
+}
+
+struct ScPlan {
+  at::Tensor ents, blocks;
+  int nblocks;
+  int64_t total;
+  std::vector<int64_t> offs;
+};
+std::mutex g_sc_mu;
+std::unordered_map<uint64_t, ScPlan> g_sc_cache;
+
+ScPlan& get_sc_plan(const std::vector<at::Tensor>& W) {
+  uint64_t h = 0x2545F4914F6CDD1DULL;
+  for (auto& w : W) h ^= reinterpret_cast<uint64_t>(w.data_ptr()) + 0x9e3779b97f4a7c15ULL +
+                        (h << 6) + (h >> 2) + (uint64_t)w.numel();
+  std::lock_guard<std::mutex> lk(g_sc_mu);
+  auto it = g_sc_cache.find(h);
+  if (it != g_sc_cache.end()) return it->second;
+  ScPlan p;
+  std::vector<ScEntry> ents;
+  std::vector<int32_t> bm;
+  int64_t off = 0;
+  for (size_t i = 0; i < W.size(); ++i) {
+    IAMD_CHECK(W[i].scalar_type() == at::kFloat && W[i].is_non_overlapping_and_dense(),
+               "mt_sn_scale_cast: weights must be dense fp32");
+    ents.push_back({W[i].data_ptr<float>(), W[i].numel(), off});
+    p.offs.push_back(off);
+    const int64_t nch = (W[i].numel() + kScChunk - 1) / kScChunk;
+    for (int64_t c = 0; c < nch; ++c) {
+      bm.push_back((int32_t)i);
+      bm.push_back((int32_t)c);
+    }
+    off += (W[i].numel() + 7) / 8 * 8;  // 16-byte aligned views
+  }
+  p.total = off;
+  auto pin = at::TensorOptions().dtype(at::kByte).pinned_memory(true);
+  auto dev = W[0].device();
+  auto he = at::empty({(int64_t)(ents.size() * sizeof(ScEntry))}, pin);
+  memcpy(he.data_ptr(), ents.data(), ents.size() * sizeof(ScEntry));
+  auto hb = at::empty({(int64_t)(bm.size() * sizeof(int32_t))}, pin);
+  memcpy(hb.data_ptr(), bm.data(), bm.size() * sizeof(int32_t));
+  p.ents = he.to(dev, true);
+  p.blocks = hb.to(dev, true).view(at::kInt);
+  p.nblocks = (int)(bm.size() / 2);
+  if (g_sc_cache.size() > 64) g_sc_cache.clear();
+  return g_sc_cache.emplace(h, std::move(p)).first->second;
+}
+
+}  // namespace
+
+std::vector<at::Tensor> mt_sn_scale_cast(const std::vector<at::Tensor>& weights,
+                                         const at::Tensor& sigma) {
+  IAMD_CHECK(!weights.empty() && sigma.numel() == (int64_t)weights.size() &&
+                 sigma.scalar_type() == at::kFloat,
+             "mt_sn_scale_cast: sigma must be fp32 [L]");
+  ScPlan& p = get_sc_plan(weights);
+  auto flat = at::empty({p.total}, weights[0].options().dtype(at::kBFloat16));
+  hipLaunchKernelGGL(sn_scale_cast, dim3(p.nblocks), dim3(kT), 0, stream(),
+                     reinterpret_cast<const ScEntry*>(p.ents.data_ptr()),
+                     p.blocks.data_ptr<int>(), sigma.data_ptr<float>(),
+                     reinterpret_cast<__hip_bfloat16*>(flat.data_ptr()));
+  IAMD_LAUNCH_CHECK();
+  std::vector<at::Tensor> out;
+  out.reserve(weights.size());
+  for (size_t i = 0; i < weights.size(); ++i)
+    out.push_back(flat.as_strided(weights[i].sizes(), weights[i].strides(), p.offs[i]));
+  return out;
+}
+
+}  // namespace iamd

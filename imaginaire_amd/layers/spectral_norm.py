@@ -14,7 +14,9 @@ checkpoints interchange with the reference. Two changes in how it runs:
   layer of the network with the k5b HIP kernels (``mt_sn_power``: 4 launches
   in total instead of ~10 per layer) and hands each layer its σ; the layer
   then forms ``W / σ`` with an autograd function whose backward is exactly
-  the gradient of PyTorch's ``W / (uᵀ W v)`` (u, v constant). A layer called
+  the gradient of PyTorch's ``W / (uᵀ W v)`` (u, v constant). Under bf16
+  autocast the bf16 ``W / σ`` of every layer is written by one k5c launch
+  (``mt_sn_scale_cast``) into a single flat buffer. A layer called
   again within the same network forward (weight sharing) falls back to its
   own power iteration — again the reference's behaviour.
 """
@@ -45,13 +47,34 @@ class _SNScale(torch.autograd.Function):
         return dw.to(weight.dtype), None, None, None
 
 
+class _SNScaleCast(torch.autograd.Function):
+    """As :class:`_SNScale`, but the forward value — ``bf16(W / σ)`` — was already
+    produced for every layer at once by the k5c kernel (``mt_sn_scale_cast``),
+    so autocast's per-layer divide + cast disappear from the forward."""
+
+    @staticmethod
+    def forward(ctx, weight, u, v, sigma, w16):
+        ctx.save_for_backward(weight, u, v, sigma)
+        return w16
+
+    @staticmethod
+    def backward(ctx, grad):
+        return _SNScale.backward(ctx, grad) + (None,)
+
+
+def _autocast_bf16(dev):
+    return torch.is_autocast_enabled(dev) and torch.get_autocast_dtype(dev) == torch.bfloat16
+
+
 class SpectralNorm(_TorchSN):
     def compute_weight(self, module, do_power_iteration):
         batched = getattr(self, '_batched', None)
         if batched is not None:
             self._batched = None  # consumed: a second call this forward iterates itself
             weight = getattr(module, self.name + '_orig')
-            u, v, sigma = batched
+            u, v, sigma, w16 = batched
+            if w16 is not None and _autocast_bf16(weight.device.type):
+                return _SNScaleCast.apply(weight, u, v, sigma, w16)
             return _SNScale.apply(weight, u, v, sigma)
         dev = getattr(module, self.name + '_orig').device.type
         with torch.autocast(device_type=dev, enabled=False):
@@ -129,10 +152,12 @@ class _SNGroup:
             # snapshots of u, v for the backward (the next forward updates them in place)
             u_all = torch.cat(us)
             v_all = torch.cat(vs)
+            w16 = (_ext.ext().mt_sn_scale_cast(ws, sigma)
+                   if _autocast_bf16(w0.device.type) else [None] * len(ws))
         ou = ov = 0
         for i, (m, h) in enumerate(self.entries):
             nu, nv = us[i].numel(), vs[i].numel()
-            h._batched = (u_all[ou:ou + nu], v_all[ov:ov + nv], sigma[i])
+            h._batched = (u_all[ou:ou + nu], v_all[ov:ov + nv], sigma[i], w16[i])
             ou += nu
             ov += nv
 

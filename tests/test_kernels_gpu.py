@@ -265,3 +265,41 @@ def test_batched_spectral_norm_matches_torch(training):
         assert torch.allclose(p.grad, pr.grad, atol=1e-4, rtol=1e-3), n
     for (n, b), (_, br) in zip(net.named_buffers(), ref.named_buffers()):
         assert torch.allclose(b, br, atol=1e-5, rtol=1e-4), n
+
+
+@pytest.mark.gpu
+def test_sn_scale_cast_under_bf16_autocast():
+    """k5c: bf16(W/σ) for all layers in one launch; grads match fp32 torch SN under autocast."""
+    from torch import nn
+    from imaginaire_amd.layers.spectral_norm import install_batched_spectral_norm, spectral_norm
+    torch.manual_seed(6)
+    # direct kernel check, including a channels-last weight and an odd numel
+    ws = [torch.randn(16, 6, 3, 3, device='cuda').contiguous(memory_format=torch.channels_last),
+          torch.randn(7, 13, device='cuda'), torch.randn(300, 40, device='cuda')]
+    sigma = torch.rand(3, device='cuda') + 0.5
+    from imaginaire_amd.ops import _ext
+    outs = _ext.ext().mt_sn_scale_cast(ws, sigma)
+    for w, s, o in zip(ws, sigma, outs):
+        assert o.dtype == torch.bfloat16 and o.shape == w.shape and o.stride() == w.stride()
+        torch.testing.assert_close(o.float(), (w / s).bfloat16().float(), atol=0, rtol=0)
+
+    def make(sn):
+        return nn.Sequential(sn(nn.Conv2d(6, 16, 3, padding=1)), nn.LeakyReLU(0.2),
+                             sn(nn.Conv2d(16, 8, 5, padding=2)), nn.Flatten(),
+                             sn(nn.Linear(8 * 6 * 6, 10)))
+    ref = make(torch.nn.utils.spectral_norm).cuda()
+    net = make(spectral_norm).cuda()
+    net.load_state_dict(ref.state_dict())
+    net = net.to(memory_format=torch.channels_last)
+    assert install_batched_spectral_norm(net) == 3
+    x = torch.randn(4, 6, 6, 6, device='cuda')
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        y_ref = ref(x)
+        y = net(x.contiguous(memory_format=torch.channels_last))
+    assert y.dtype == torch.bfloat16
+    torch.testing.assert_close(y.float(), y_ref.float(), atol=3e-2, rtol=3e-2)
+    g = torch.randn_like(y)
+    y_ref.backward(g)
+    y.backward(g)
+    for (n, p), (_, pr) in zip(net.named_parameters(), ref.named_parameters()):
+        torch.testing.assert_close(p.grad, pr.grad, atol=3e-2, rtol=3e-2, msg=n)
