@@ -152,6 +152,14 @@ class Dataset(torch.utils.data.Dataset):
                 out[name] = torch.cat([f, m], 0)
             elif name in self.input_image or name.startswith('images'):
                 out[name] = smooth_field(nc, h, w, gen).clamp(-1, 1)
+            elif 'densepose' in name:
+                # IUV map as decoded from the 8-bit PNG: U, V in [0, 1], part index I/255
+                parts = voronoi_labels(h, w, 25, gen).float() / 255.0
+                uv = (smooth_field(2, h, w, gen) + 1) / 2
+                out[name] = torch.cat([uv, parts[None]], 0)
+            elif 'instance' in name and nc == 3:
+                ids = voronoi_labels(h, w, 4, gen).float() / 255.0
+                out[name] = ids[None].repeat(3, 1, 1)
             elif interp == 'NEAREST' and nc > 1:
                 seg = voronoi_labels(h, w, nc, gen)
                 onehot = F.one_hot(seg, nc).permute(2, 0, 1).float()

@@ -10,6 +10,8 @@ exercise). Set ``IMAGINAIRE_AMD_EAGER=1`` to force the reference path on GPU
 import importlib
 import os
 
+import torch
+
 _EXT = None
 _ERR = None
 
@@ -53,3 +55,17 @@ def ext():
     if e is None:
         raise RuntimeError('imaginaire_amd._C not available: {}'.format(_ERR))
     return e
+
+
+def is_dense(t):
+    """Python mirror of ``at::Tensor::is_non_overlapping_and_dense`` (not bound in torch):
+    the elements exactly fill ``numel`` contiguous slots in some dimension order."""
+    if t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last)):
+        return True
+    dims = sorted((st, sz) for sz, st in zip(t.shape, t.stride()) if sz != 1)
+    expect = 1
+    for st, sz in dims:
+        if st != expect:
+            return False
+        expect *= sz
+    return True

@@ -55,7 +55,7 @@ class FusedAdam(Optimizer):
             if isinstance(lr, torch.Tensor):
                 lr = float(lr)
             native = _ext.use_native(params[0]) and all(
-                p.dtype == torch.float32 and p.is_non_overlapping_and_dense() for p in params)
+                p.dtype == torch.float32 and _ext.is_dense(p) for p in params)
             if native:
                 gdt = grads[0].dtype
                 if gdt not in (torch.float32, torch.bfloat16):

@@ -146,3 +146,12 @@ def test_unpaired_images_from_folder(tmp_path):
     ds = Dataset(cfg, is_inference=True)
     assert len(ds) == 8
     assert ds[3]['images'].shape == (3, 32, 48)
+
+
+def test_is_dense_mirror():
+    import torch
+    from imaginaire_amd.ops._ext import is_dense
+    a = torch.randn(2, 3, 4, 5)
+    assert is_dense(a) and is_dense(a.contiguous(memory_format=torch.channels_last))
+    assert is_dense(torch.nn.Parameter(a)) and is_dense(a.permute(3, 1, 0, 2))
+    assert not is_dense(a[:, :2]) and not is_dense(a[..., ::2])

@@ -12,7 +12,7 @@ from imaginaire_amd.utils.trainer import get_model_optimizer_and_scheduler, get_
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FAMILIES = ['spade', 'pix2pixHD', 'munit', 'unit', 'funit', 'coco_funit', 'vid2vid_street',
-            'fs_vid2vid_face', 'wc_vid2vid']
+            'fs_vid2vid_face', 'wc_vid2vid', 'munit_patch', 'vid2vid_pose', 'fs_vid2vid_pose']
 
 
 @pytest.mark.parametrize('name', FAMILIES)

@@ -25,7 +25,7 @@ from imaginaire_amd.utils.trainer import (get_model_optimizer_and_scheduler, get
                                           set_random_seed)
 
 
-def parse_args():
+def parse_args(argv=None):
     parser = argparse.ArgumentParser(description='Training')
     parser.add_argument('--config', required=True, help='Path to the training config file.')
     parser.add_argument('--logdir', help='Dir for saving logs and models.')
@@ -36,11 +36,11 @@ def parse_args():
     parser.add_argument('--single_gpu', action='store_true')
     parser.add_argument('--num_workers', type=int)
     parser.add_argument('--backend', default=None, help='nccl (RCCL) / gloo; default auto')
-    return parser.parse_args()
+    return parser.parse_args(argv)
 
 
-def main():
-    args = parse_args()
+def main(argv=None):
+    args = parse_args(argv)
     set_random_seed(args.seed, by_rank=True)
     cfg = Config(args.config)
     if not args.single_gpu and int(os.environ.get('WORLD_SIZE', '1')) > 1:
