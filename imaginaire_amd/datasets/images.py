@@ -2,6 +2,8 @@
 the class of an image is the first path component of its sequence name."""
 import random
 
+import torch
+
 from imaginaire_amd.datasets.base import BaseDataset
 
 
@@ -41,6 +43,12 @@ def load_unpaired(dataset, per_type):
         lmdbs[t] = dataset.lmdbs[t][k['lmdb_idx']]
     data = dataset.load_from_dataset(keys, lmdbs)
     data = dataset.apply_ops(data, dataset.pre_aug_ops)
+    # size of the first image type before augmentation (the content image for FUNIT):
+    # generators' ``keep_original_size`` inference resizes back to it
+    first = next((t for t in dataset.image_data_types if t in data), None)
+    orig_hw = None
+    if first is not None and hasattr(data[first][0], 'shape'):
+        orig_hw = tuple(int(v) for v in data[first][0].shape[:2])
     data, is_flipped = dataset.perform_augmentation(data, paired=False)
     data = dataset.apply_ops(data, dataset.post_aug_ops)
     data = dataset.apply_ops(data, dataset.full_data_post_aug_ops, full_data=True)
@@ -49,6 +57,8 @@ def load_unpaired(dataset, per_type):
         data[t] = data[t][0]
     data['is_flipped'] = is_flipped
     data['key'] = per_type
+    if orig_hw is not None:
+        data['original_h_w'] = torch.IntTensor(orig_hw)
     return data
 
 

@@ -31,10 +31,15 @@ class Dataset(BaseDataset):
     def _sample_keys(self, index):
         content = self.mapping['images_content']
         if self.is_inference:
-            cls = self.sample_class_idx or 0
+            if self.sample_class_idx is None:
+                # no class selected (plain ``inference.py``): walk every style image once
+                style = self.mapping['images_style'][index % len(self.mapping['images_style'])]
+                cls = style['class_idx']
+            else:
+                cls = self.sample_class_idx
+                style = self.mapping_class['images_style'][cls][index]
             ci = ((index + self.content_offset * cls) * self.content_interval) % len(content)
-            return {'images_content': content[ci],
-                    'images_style': self.mapping_class['images_style'][cls][index]}
+            return {'images_content': content[ci], 'images_style': style}
         return {'images_content': random.choice(content),
                 'images_style': random.choice(self.mapping['images_style'])}
 

@@ -9,6 +9,7 @@ from torch import nn
 
 from imaginaire_amd.generators.unit import _kw
 from imaginaire_amd.layers import Conv2dBlock, LinearBlock, Res2dBlock, UpRes2dBlock
+from imaginaire_amd.generators.unit import _names
 
 
 class Generator(nn.Module):
@@ -30,8 +31,7 @@ class Generator(nn.Module):
         if keep_original_size:
             height, width = int(data['original_h_w'][0][0]), int(data['original_h_w'][0][1])
             output_images = torch.nn.functional.interpolate(output_images, size=[height, width])
-        key = data['key']
-        file_names = key['images_content'][0] if isinstance(key, dict) else key
+        file_names = _names(data, 'images_content')
         return output_images, file_names
 
 

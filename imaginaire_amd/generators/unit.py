@@ -58,6 +58,17 @@ def _name(data, key):
     return str(entry)
 
 
+def _names(data, key):
+    """Per-sample output names ``sequence/filename`` for a collated batch."""
+    k = data.get('key', {})
+    entry = k.get(key, k) if isinstance(k, dict) else k
+    if isinstance(entry, dict) and 'sequence_name' in entry:
+        return ['%s/%s' % (s, f) for s, f in zip(entry['sequence_name'], entry['filename'])]
+    if isinstance(entry, (list, tuple)):
+        return [str(e) for e in entry]
+    return [str(entry)]
+
+
 class AutoEncoder(nn.Module):
     def __init__(self, num_filters=64, max_num_filters=256, num_res_blocks=4,
                  num_downsamples_content=2, num_image_channels=3, content_norm_type='instance',

@@ -60,6 +60,15 @@ def _grad_view(flat, off, p):
     return flat[off:off + p.numel()].as_strided(p.size(), p.stride())
 
 
+def _comm_device(group, tensors):
+    if dist.get_backend(group) == 'gloo':
+        return torch.device('cpu')
+    for t in tensors:
+        if t.device.type == 'cuda':
+            return t.device
+    return torch.device('cuda', torch.cuda.current_device())
+
+
 class DistributedDataParallel(nn.Module):
     def __init__(self, module, process_group=None, bucket_cap_mb=256, first_bucket_mb=16,
                  broadcast_buffers=False, comm_dtype=None, overlap=True, **unused):
@@ -80,13 +89,21 @@ class DistributedDataParallel(nn.Module):
     # -- construction ------------------------------------------------------
     @torch.no_grad()
     def _broadcast_state(self):
-        tensors = [p.data for p in self.module.parameters()] + \
-            [b for b in self.module.buffers()]
+        self._broadcast_tensors([p.data for p in self.module.parameters()] +
+                                [b for b in self.module.buffers()])
+
+    @torch.no_grad()
+    def _broadcast_tensors(self, tensors):
+        if not tensors:
+            return
+        # one flat broadcast per dtype, staged on the backend's device (RCCL needs HIP memory;
+        # a stray CPU buffer must not break construction)
+        comm_dev = _comm_device(self.process_group, tensors)
         by_dtype = {}
         for t in tensors:
             by_dtype.setdefault(t.dtype, []).append(t)
         for ts in by_dtype.values():
-            flat = torch.cat([t.reshape(-1) for t in ts])
+            flat = torch.cat([t.reshape(-1).to(comm_dev) for t in ts])
             dist.broadcast(flat, src=self._global_src(), group=self.process_group)
             off = 0
             for t in ts:
@@ -196,8 +213,7 @@ class DistributedDataParallel(nn.Module):
     def sync_buffers(self):
         if self.world <= 1:
             return
-        for buf in self.module.buffers():
-            dist.broadcast(buf, src=self._global_src(), group=self.process_group)
+        self._broadcast_tensors(list(self.module.buffers()))
 
     def forward(self, *args, **kwargs):
         if self.broadcast_buffers and self.world > 1 and self.training:

@@ -113,7 +113,7 @@ class Trainer(BaseTrainer):
             if dataset is not None and hasattr(dataset, 'get_label_lengths'):
                 labels = split_labels(data['label'], dataset.get_label_lengths())
                 segmap = labels.get('segmaps', labels.get('seg_maps', segmap))
-            segmap = tensor2label(segmap.float()).to(data['images'].device)
+            segmap = torch.stack(tensor2label(segmap.float(), output_normalized_tensor=True))
             net_G_output = self.net_G(data, random_style=True)
             vis_images = [data['images'][:, :3].float(), segmap,
                           net_G_output['fake_images'][:, :3].float()]

@@ -55,7 +55,11 @@ class ModelAverage(nn.Module):
         self.beta = beta
         self.remove_sn = remove_sn
         self.start_iteration = start_iteration
-        self.register_buffer('num_updates_tracked', torch.tensor(0, dtype=torch.long))
+        # on the module's device: DDP broadcasts every buffer over RCCL at construction
+        dev = next(module.parameters()).device if any(True for _ in module.parameters()) \
+            else torch.device('cpu')
+        self.register_buffer('num_updates_tracked',
+                             torch.tensor(0, dtype=torch.long, device=dev))
         requires_grad(self.averaged_model, False)
         if self.remove_sn:
             self.copy_s2t()

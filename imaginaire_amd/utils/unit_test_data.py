@@ -22,6 +22,7 @@ skipped (the fork never reads unprojections, generators/wc_vid2vid.py:147).
 the built LMDBs: synthetic dataset types are replaced with the real dataset
 class of the same family.
 """
+import copy
 import json
 import math
 import os
@@ -232,6 +233,15 @@ def lmdb_config(cfg_path, lmdb_root, out_path, max_iter=None):
     """Write ``out_path``: ``cfg_path`` with every split reading ``lmdb_root``."""
     with open(cfg_path) as f:
         cfg = yaml.safe_load(f)
+    if 'test_data' not in cfg and 'val' in cfg['data']:
+        # inference reads ``test_data``: derive it from the validation split
+        td = copy.deepcopy(cfg['data'])
+        td['test'] = copy.deepcopy(td['val'])
+        td['test']['batch_size'] = 1
+        td['paired'] = _layout(td) == 'paired'
+        for split in ('train', 'val'):
+            td.pop(split, None)
+        cfg['test_data'] = td
     for key in ('data', 'test_data'):
         d = cfg.get(key)
         if not d:
@@ -246,6 +256,7 @@ def lmdb_config(cfg_path, lmdb_root, out_path, max_iter=None):
         d.pop('synthetic', None)
     if max_iter is not None:
         cfg['max_iter'] = int(max_iter)
+        cfg['snapshot_save_iter'] = int(max_iter)  # leave a checkpoint for inference tests
     with open(out_path, 'w') as f:
         yaml.safe_dump(cfg, f, sort_keys=False)
     return out_path

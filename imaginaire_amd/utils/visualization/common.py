@@ -117,21 +117,34 @@ class Colorize(object):
         return color_image
 
 
-def tensor2label(segmap, n_label=None, imtype=np.uint8, colorize=True, output_normalized_tensor=False):
-    """One-hot (or index) label tensor → colour image tensor in [-1, 1]."""
+def tensor2label(segmap, n_label=None, imtype=np.uint8, colorize=True,
+                 output_normalized_tensor=False):
+    """One-hot (or index) label map → colour image (common.py:110-153).
+
+    [C,H,W] → HxWx3 ``imtype`` array (HxW indices when ``colorize=False``); batched
+    [N,C,H,W] / [N,T,C,H,W] inputs and lists give lists. ``output_normalized_tensor``
+    returns a [3,H,W] float tensor in [-1, 1] on the input's device instead.
+    """
+    if segmap is None:
+        return None
+    if isinstance(segmap, list):
+        return [tensor2label(x, n_label, imtype, colorize, output_normalized_tensor)
+                for x in segmap]
     if segmap.dim() == 5 or segmap.dim() == 4:
-        return torch.stack([tensor2label(segmap[i], n_label, imtype, colorize,
-                                         output_normalized_tensor) for i in range(segmap.size(0))])
-    segmap = segmap.float().cpu()
+        return [tensor2label(segmap[i], n_label, imtype, colorize, output_normalized_tensor)
+                for i in range(segmap.size(0))]
+    device = segmap.device
+    segmap = segmap.detach().float().cpu()
     if n_label is None:
         n_label = segmap.size(0)
     if segmap.size(0) > 1:
         segmap = segmap.max(0, keepdim=True)[1]
+    if output_normalized_tensor:
+        out = Colorize(max(n_label, 2))(segmap).float() / 255.0
+        return (out * 2 - 1).to(device)
     if colorize:
-        segmap = Colorize(max(n_label, 2))(segmap)
-        out = segmap.float() / 255.0
-        return out * 2 - 1
-    return segmap.float()
+        return np.transpose(Colorize(max(n_label, 2))(segmap).numpy(), (1, 2, 0)).astype(imtype)
+    return segmap.numpy().astype(imtype)
 
 
 def tensor2flow(tensor, imtype=np.uint8):

@@ -155,3 +155,12 @@ def test_is_dense_mirror():
     assert is_dense(a) and is_dense(a.contiguous(memory_format=torch.channels_last))
     assert is_dense(torch.nn.Parameter(a)) and is_dense(a.permute(3, 1, 0, 2))
     assert not is_dense(a[:, :2]) and not is_dense(a[..., ::2])
+
+
+def test_model_average_buffers_follow_module_device():
+    """Every ModelAverage buffer lives on the wrapped module's device (DDP broadcasts them)."""
+    import torch
+    from imaginaire_amd.utils.model_average import ModelAverage
+    net = torch.nn.Sequential(torch.nn.Linear(3, 3)).to('meta')
+    ma = ModelAverage(net, 0.9, 0, remove_sn=False)
+    assert all(b.device.type == 'meta' for b in ma.buffers())

@@ -103,3 +103,19 @@ def test_syncbn_matches_global_batchnorm():
     assert np.allclose(res[0][3], bn.running_mean.detach().numpy(), atol=1e-6)
     # weight grad is local per rank (DDP averages it); sum over ranks == global
     assert np.allclose(res[0][4] + res[1][4], bn.weight.grad.numpy(), atol=1e-4)
+
+
+def test_train_py_two_ranks_gloo(tmp_path):
+    """train.py under torch.distributed.run with 2 gloo ranks: the whole trainer path
+    (ModelAverage + native DDP + SyncBN groups + batched SN) on the SPADE unit config."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMP_NUM_THREADS='2')
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
+           '--master-addr', '127.0.0.1', '--master-port', str(_free_port()), 'train.py',
+           '--config', 'configs/unit_test/spade.yaml', '--backend', 'gloo',
+           '--logdir', str(tmp_path)]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert 'Done with training' in r.stdout
