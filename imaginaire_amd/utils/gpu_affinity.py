@@ -45,8 +45,46 @@ def _gpu_numa_node(gpu_id):
         return None
 
 
-def set_affinity(gpu_id):
-    """Pin this process to the CPUs local to ``gpu_id``; returns the CPU set used."""
+def systemGetDriverVersion():  # noqa: N802 (reference name)
+    """Kernel driver version (amdgpu module / KFD) as a string, '' if unknown."""
+    for path in ('/sys/module/amdgpu/version', '/sys/class/kfd/kfd/topology/system_properties'):
+        try:
+            with open(path) as f:
+                return f.read().strip().splitlines()[0]
+        except (OSError, IndexError):
+            continue
+    return ''
+
+
+def deviceGetCount():  # noqa: N802
+    """Number of visible GPUs (without initialising the HIP runtime)."""
+    import torch
+    return torch.cuda.device_count()
+
+
+class device(object):  # noqa: N801
+    """Per-GPU handle exposing name and local CPU list (reference gpu_affinity.py:24-46)."""
+
+    def __init__(self, device_idx):
+        self.idx = device_idx
+
+    def getName(self):  # noqa: N802
+        import torch
+        return torch.cuda.get_device_name(self.idx)
+
+    def getCpuAffinity(self):  # noqa: N802
+        node = _gpu_numa_node(self.idx)
+        cpus = _cpus_of_numa_node(node) if node is not None else None
+        if not cpus:
+            cpus = os.sched_getaffinity(0) if hasattr(os, 'sched_getaffinity') else set()
+        return sorted(cpus)
+
+
+def set_affinity(gpu_id=None):
+    """Pin this process to the CPUs local to ``gpu_id`` (default: $LOCAL_RANK); returns the
+    CPU set used."""
+    if gpu_id is None:
+        gpu_id = int(os.getenv('LOCAL_RANK', 0))
     node = _gpu_numa_node(gpu_id)
     cpus = _cpus_of_numa_node(node) if node is not None else None
     if not cpus or not hasattr(os, 'sched_setaffinity'):

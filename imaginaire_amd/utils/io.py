@@ -27,6 +27,22 @@ def save_intermediate_training_results(visualization_images, logdir, current_epo
     save_image_grid(visualization_images, output_filename, nrow=1)
 
 
+def get_confirm_token(response):
+    """Google-Drive large-file confirmation token from the response cookies (io.py:62-75)."""
+    for key, value in response.cookies.items():
+        if key.startswith('download_warning'):
+            return value
+    return None
+
+
+def save_response_content(response, destination, chunk_size=32768):
+    """Stream a ``requests`` response body to ``destination`` (io.py:78-90)."""
+    with open(destination, 'wb') as f:
+        for chunk in response.iter_content(chunk_size):
+            if chunk:
+                f.write(chunk)
+
+
 def download_file_from_google_drive(file_id, destination):
     try:
         import requests
@@ -35,16 +51,10 @@ def download_file_from_google_drive(file_id, destination):
     url = "https://docs.google.com/uc?export=download"
     session = requests.Session()
     response = session.get(url, params={'id': file_id}, stream=True)
-    token = None
-    for key, value in response.cookies.items():
-        if key.startswith('download_warning'):
-            token = value
+    token = get_confirm_token(response)
     if token:
         response = session.get(url, params={'id': file_id, 'confirm': token}, stream=True)
-    with open(destination, "wb") as f:
-        for chunk in response.iter_content(32768):
-            if chunk:
-                f.write(chunk)
+    save_response_content(response, destination)
 
 
 def get_checkpoint(checkpoint_path, url='', allow_download=False):

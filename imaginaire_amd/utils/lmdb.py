@@ -27,6 +27,14 @@ def check_and_add(filepath, key, filepaths, keys, remove_missing=False):
     return os.path.getsize(filepath)
 
 
+def write_entry(txn, key, filepath):
+    """Put the raw bytes of ``filepath`` under ``key`` into a transaction-like object with a
+    ``put(bytes, bytes)`` method (reference utils/lmdb.py:43-53)."""
+    with open(filepath, 'rb') as f:
+        data = f.read()
+    txn.put(key.encode('ascii'), data)
+
+
 def build_lmdb(filepaths, keys, output_filepath, map_size=None, large=False, page_size=4096):
     """Write one LMDB environment from (file, key) pairs. ``map_size`` / ``large``
     are accepted for interface parity; the native writer sizes the file exactly."""

@@ -86,35 +86,52 @@ def tensor2im(image_tensor, imtype=np.uint8, normalize=True, three_channel_outpu
     return image_numpy.astype(imtype)
 
 
-def _label_colormap(n):
-    cmap = np.zeros((n, 3), dtype=np.uint8)
-    for i in range(n):
-        r = g = b = 0
-        cid = i
-        for j in range(7):
-            r |= ((cid >> 0) & 1) << (7 - j)
-            g |= ((cid >> 1) & 1) << (7 - j)
-            b |= ((cid >> 2) & 1) << (7 - j)
-            cid >>= 3
-        cmap[i] = (r, g, b)
-    return cmap
+# Cityscapes/GTA palettes of the reference (common.py:224-244): 35 train ids, 20 eval ids
+_CITYSCAPES_35 = [(0, 0, 0)] * 5 + [
+    (111, 74, 0), (81, 0, 81), (128, 64, 128), (244, 35, 232), (250, 170, 160),
+    (230, 150, 140), (70, 70, 70), (102, 102, 156), (190, 153, 153), (180, 165, 180),
+    (150, 100, 100), (150, 120, 90), (153, 153, 153), (153, 153, 153), (250, 170, 30),
+    (220, 220, 0), (107, 142, 35), (152, 251, 152), (70, 130, 180), (220, 20, 60),
+    (255, 0, 0), (0, 0, 142), (0, 0, 70), (0, 60, 100), (0, 0, 90), (0, 0, 110),
+    (0, 80, 100), (0, 0, 230), (119, 11, 32), (0, 0, 142)]
+_CITYSCAPES_20 = [
+    (128, 64, 128), (244, 35, 232), (70, 70, 70), (102, 102, 156), (190, 153, 153),
+    (153, 153, 153), (250, 170, 30), (220, 220, 0), (107, 142, 35), (152, 251, 152),
+    (220, 20, 60), (255, 0, 0), (0, 0, 142), (0, 0, 70), (0, 60, 100), (0, 80, 100),
+    (0, 0, 230), (119, 11, 32), (70, 130, 180), (0, 0, 0)]
+
+
+def labelcolormap(N):
+    """[N, 3] uint8 colours for label ids: Cityscapes palettes for N = 35 / 20, otherwise
+    the bit-interleaved PASCAL-style palette (common.py:218-256)."""
+    if N == 35:
+        return np.array(_CITYSCAPES_35, dtype=np.uint8)
+    if N == 20:
+        return np.array(_CITYSCAPES_20, dtype=np.uint8)
+    ids = np.arange(N)
+    cmap = np.zeros((N, 3), dtype=np.int64)
+    for j in range(8):
+        for c in range(3):
+            cmap[:, c] += ((ids >> (3 * j + c)) & 1) << (7 - j)
+    return cmap.astype(np.uint8)
+
+
+_label_colormap = labelcolormap
 
 
 class Colorize(object):
-    """Map integer label maps to RGB colours (common.py:259-290)."""
+    """Map integer label maps [1, H, W] to RGB [3, H, W] uint8 (common.py:259-290);
+    one table gather instead of a per-label mask loop."""
 
     def __init__(self, n=35):
-        self.cmap = torch.from_numpy(_label_colormap(n))
+        self.cmap = torch.from_numpy(labelcolormap(n))
 
     def __call__(self, gray_image):
-        size = gray_image.size()
-        color_image = torch.ByteTensor(3, size[1], size[2]).fill_(0)
-        for label in range(0, len(self.cmap)):
-            mask = (label == gray_image[0]).cpu()
-            color_image[0][mask] = self.cmap[label][0]
-            color_image[1][mask] = self.cmap[label][1]
-            color_image[2][mask] = self.cmap[label][2]
-        return color_image
+        idx = gray_image[0].long().cpu()
+        valid = (idx >= 0) & (idx < len(self.cmap))
+        color = self.cmap[idx.clamp(0, len(self.cmap) - 1)]
+        color[~valid] = 0
+        return color.permute(2, 0, 1).contiguous()
 
 
 def tensor2label(segmap, n_label=None, imtype=np.uint8, colorize=True,
@@ -160,6 +177,32 @@ def tensor2flow(tensor, imtype=np.uint8):
     mmax = mag.max() if mag.max() > 0 else 1.0
     hsv[..., 2] = np.clip(mag / mmax * 255, 0, 255).astype(np.uint8)
     return np.asarray(Image.fromarray(hsv, mode='HSV').convert('RGB'))
+
+
+def plot_keypoints_on_black(resize_h, resize_w, crop_h, crop_w, is_flipped, cfgdata,
+                            keypoints):
+    """Keypoints ([N, 2] or [T, N, 2]) as green discs on black crop_h x crop_w RGB images,
+    one per frame — a dataset ``vis::`` op (common.py:282-311)."""
+    kp = np.asarray(keypoints)
+    if kp.ndim == 2 and kp.shape[1] == 2:
+        kp = kp[np.newaxis]
+    return [plot_keypoints(np.zeros((crop_h, crop_w, 3), np.uint8), kp[t], radius=5)
+            for t in range(kp.shape[0])]
+
+
+def save_tensor_image(filename, image, minus1to1_normalized=False):
+    """Save a [3, H, W] tensor in [0, 1] (or [-1, 1]) as an image file (common.py:14-40)."""
+    if image.dim() != 3:
+        raise ValueError('Image tensor dimension does not equal = 3.')
+    if image.size(0) != 3:
+        raise ValueError('Image has more than 3 channels.')
+    if minus1to1_normalized:
+        image = (image + 1) * 0.5
+    dirname = os.path.dirname(filename)
+    if dirname:
+        os.makedirs(dirname, exist_ok=True)
+    arr = (image.detach().float().clamp(0, 1).cpu().permute(1, 2, 0).numpy() * 255 + 0.5)
+    Image.fromarray(arr.astype(np.uint8)).save(filename)
 
 
 def plot_keypoints(image, keypoints, radius=4, color=(0, 255, 0)):
