@@ -56,8 +56,24 @@ def parse():
     return p.parse_args()
 
 
+def _heartbeat(period=20.0):
+    """Print a line to stderr every ``period`` s: the first warm-up step on a fresh
+    box spends minutes inside MIOpen kernel compilation and prints nothing else."""
+    import threading
+
+    t0 = time.time()
+
+    def run():
+        while True:
+            time.sleep(period)
+            print('[bench] alive %.0f s' % (time.time() - t0), file=sys.__stderr__, flush=True)
+
+    threading.Thread(target=run, daemon=True).start()
+
+
 def main():
     args = parse()
+    _heartbeat()
     if args.eager:
         os.environ['IMAGINAIRE_AMD_EAGER'] = '1'
     import torch

@@ -60,6 +60,13 @@ std::vector<at::Tensor> flow_warp_bwd(const at::Tensor& img, const at::Tensor& f
 at::Tensor resample2d_forward(const at::Tensor& in1, const at::Tensor& flow, int64_t ks);
 std::vector<at::Tensor> resample2d_backward(const at::Tensor& in1, const at::Tensor& flow,
                                             const at::Tensor& dout, int64_t ks);
+// conv_mfma.hip (k10)
+at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                       int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
+                       double slope);
+at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t KH, int64_t KW,
+                             int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh,
+                             int64_t dw);
 void register_lmdb(pybind11::module_& m);
 void profile_marker(int64_t tag);
 std::vector<at::Tensor> mt_sn_scale_cast(const std::vector<at::Tensor>& weights,
@@ -74,6 +81,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mt_sn_power", &iamd::mt_sn_power, "batched spectral-norm power iteration (k5b)");
   m.def("mt_sn_scale_cast", &iamd::mt_sn_scale_cast, "batched W/sigma -> bf16 (k5c)");
   m.def("profile_marker", &iamd::profile_marker, "named no-op kernel for trace phase splits");
+  m.def("conv2d_mfma", &iamd::conv2d_mfma, "MFMA implicit-GEMM NHWC conv + bias + act (k10)");
+  m.def("conv2d_wgrad_mfma", &iamd::conv2d_wgrad_mfma, "MFMA conv weight gradient (k11)");
   m.def("norm_stats", &iamd::norm_stats, "per-(group,channel) statistics (k1)");
   m.def("norm_apply", &iamd::norm_apply, "norm + SPADE modulation + activation (k1 fwd)");
   m.def("norm_bwd_reduce", &iamd::norm_bwd_reduce, "k1 backward reduction");

@@ -1,0 +1,253 @@
+// k10: implicit-GEMM convolution on the gfx950 matrix cores (NHWC, bf16 in, fp32 accumulate).
+//
+// Replaces the MIOpen forward (and, through a flipped/transposed weight, the stride-1 data
+// gradient) of the convolutions that dominate a SPADE/pix2pixHD/vid2vid step: 3x3 / 5x5 /
+// 4x4-stride-2 convs with 64..4096 channels at up to 256x512 (reference layers/conv.py:59-91
+// runs these through cuDNN; the reference has no hand-written conv).
+//
+// GEMM view: rows m = output pixels (b, oh, ow), columns n = output channels,
+// k = (ky, kx, ci) with ci fastest. Both operands are K-contiguous in memory:
+//   A[m][k] = x[b][oh*sh - ph + ky*dh][ow*sw - pw + kx*dw][ci]   (NHWC activation)
+//   B[n][k] = w[n][ky][kx][ci]                                    (OHWI = channels-last weight)
+// so a 64-deep k-step is one filter tap and 64 consecutive input channels (Cin % 64 == 0;
+// the Python wrapper zero-pads odd channel counts such as 185-channel label maps).
+//
+// Block tile 128 (pixels) x BN (channels) x 64 (k), 256 threads = 4 wave64s in a 2x2 grid,
+// each wave owns a 64 x BN/2 sub-tile of v_mfma_f32_16x16x32_bf16 accumulators.
+// Staging: global -> LDS with global_load_lds_dwordx4 (no VGPR round trip), two LDS buffers,
+// one barrier per k-step; the load of step k+1 is in flight while step k runs on the MFMAs.
+// Padding pixels (outside the image) point their DMA at a 16-byte zero page instead of
+// branching. LDS rows are 128 B; the 16-B chunk index is XOR-swizzled with (row & 7) on the
+// global side (the LDS write of a DMA is lane-linear), which makes the ds_read_b128 fragment
+// reads bank-conflict free. Epilogue: + bias, leaky/relu slope, bf16, staged through LDS so
+// every global store is a 16-byte row segment. Block ids are XCD-remapped so the BN-tiles
+// that share one pixel tile run on the same XCD (shared L2 for the activation halo).
+#include "common.h"
+
+namespace iamd {
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+constexpr int kBM = 128;
+constexpr int kBK = 64;
+constexpr int kThreads = 256;
+constexpr int kRowBytes = kBK * 2;  // 128 B per staged row
+constexpr int kEpiStride = 272;     // epilogue LDS row stride in bytes (BN<=128 bf16 + 16 pad)
+
+struct ConvArgs {
+  const __hip_bfloat16* x;
+  const __hip_bfloat16* w;
+  const float* bias;
+  __hip_bfloat16* y;
+  const __hip_bfloat16* zero;
+  int H, W, Cin, Ho, Wo, Cout;
+  int KW, sh, sw, ph, pw, dh, dw;
+  int M, nk, cpt, nNt;
+  float slope;
+};
+
+__device__ __forceinline__ void glds16(const void* src, char* lds) {
+  __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)lds, 16, 0, 0);
+}
+
+template <int BN, bool HAS_BIAS>
+__global__ __launch_bounds__(kThreads, 2) void conv_fwd_mfma(ConvArgs a) {
+  constexpr int NI = BN / 32;                 // 16-wide n-fragments per wave
+  constexpr int kAbytes = kBM * kRowBytes;    // 16 KB
+  constexpr int kBbytes = BN * kRowBytes;     // 8 / 16 KB
+  constexpr int kStage = kAbytes + kBbytes;
+  constexpr int kBLoads = BN / 32;            // glds per thread for the B tile
+  __shared__ __attribute__((aligned(16))) char smem[2 * kStage];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid / a.nNt, nt = bid - mt * a.nNt;
+  const int m0 = mt * kBM, n0 = nt * BN;
+
+  // ---- per-thread DMA sources: rows lrow + 32 i, chunk c_sw (swizzled) -----------------
+  const int lrow = tid >> 3;
+  const int csw = (tid & 7) ^ (lrow & 7);
+  const int HoWo = a.Ho * a.Wo;
+  int a_ih[4], a_iw[4];
+  const __hip_bfloat16* a_base[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int m = m0 + lrow + 32 * i;
+    if (m < a.M) {
+      int b = m / HoWo, r = m - b * HoWo;
+      int oh = r / a.Wo, ow = r - oh * a.Wo;
+      a_ih[i] = oh * a.sh - a.ph;
+      a_iw[i] = ow * a.sw - a.pw;
+      a_base[i] = a.x + (size_t)b * a.H * a.W * a.Cin + csw * 8;
+    } else {
+      a_ih[i] = -(1 << 29);  // never inside the image
+      a_iw[i] = 0;
+      a_base[i] = a.x;
+    }
+  }
+  const size_t wrow = (size_t)a.nk * kBK;  // = KH*KW*Cin
+  const __hip_bfloat16* b_base[kBLoads];
+#pragma unroll
+  for (int i = 0; i < kBLoads; ++i) b_base[i] = a.w + (size_t)(n0 + lrow + 32 * i) * wrow + csw * 8;
+
+  auto issue = [&](int ks, int buf) {
+    const int tap = ks / a.cpt;
+    const int c0 = (ks - tap * a.cpt) * kBK;
+    const int ky = tap / a.KW, kx = tap - ky * a.KW;
+    char* As = smem + buf * kStage;
+    char* Bs = As + kAbytes;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ih = a_ih[i] + ky * a.dh, iw = a_iw[i] + kx * a.dw;
+      const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      const __hip_bfloat16* src = ok ? a_base[i] + ((size_t)ih * a.W + iw) * a.Cin + c0 : a.zero;
+      glds16(src, As + i * 4096 + wid * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < kBLoads; ++i) glds16(b_base[i] + (size_t)ks * kBK, Bs + i * 4096 + wid * 1024);
+  };
+
+  f32x4 acc[4][NI];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read offsets (row & 7 == lane & 7 for every fragment row of this lane)
+  const int frow = lane & 15, fsw = lane & 7, fk = lane >> 4;
+  issue(0, 0);
+  for (int ks = 0; ks < a.nk; ++ks) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (ks + 1 < a.nk) issue(ks + 1, (ks + 1) & 1);
+    const char* As = smem + (ks & 1) * kStage;
+    const char* Bs = As + kAbytes;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int coff = ((kk * 4 + fk) ^ fsw) << 4;
+      bf16x8 af[4], bfr[NI];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + i * 16 + frow) * kRowBytes + coff);
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * (BN / 2) + j * 16 + frow) * kRowBytes + coff);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue: bias + activation -> bf16 tile in LDS -> 16-byte row stores --------------
+  __syncthreads();
+  char* E = smem;
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int cl = wn * (BN / 2) + j * 16 + (lane & 15);
+    const float bv = HAS_BIAS ? a.bias[n0 + cl] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rl = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        float v = acc[i][j][r] + bv;
+        v = v > 0.f ? v : v * a.slope;
+        *reinterpret_cast<__hip_bfloat16*>(E + rl * kEpiStride + cl * 2) = __float2bfloat16(v);
+      }
+    }
+  }
+  __syncthreads();
+  constexpr int kChunks = BN / 8;              // 16-B chunks per output row
+  constexpr int kRowsPerPass = kThreads / kChunks;
+  const int ch = tid % kChunks, rr = tid / kChunks;
+#pragma unroll
+  for (int p = 0; p < kBM / kRowsPerPass; ++p) {
+    const int rl = p * kRowsPerPass + rr;
+    const int m = m0 + rl;
+    if (m < a.M) {
+      const uint4 v = *reinterpret_cast<const uint4*>(E + rl * kEpiStride + ch * 16);
+      *reinterpret_cast<uint4*>(a.y + (size_t)m * a.Cout + n0 + ch * 8) = v;
+    }
+  }
+}
+
+const __hip_bfloat16* zero_page(int dev) {
+  static void* pages[64] = {nullptr};
+  IAMD_CHECK(dev >= 0 && dev < 64, "device index");
+  if (!pages[dev]) {
+    IAMD_HIP_CHECK(hipMalloc(&pages[dev], 256));
+    IAMD_HIP_CHECK(hipMemset(pages[dev], 0, 256));
+  }
+  return reinterpret_cast<const __hip_bfloat16*>(pages[dev]);
+}
+
+}  // namespace
+
+// y[B, Cout, Ho, Wo] (channels-last) = act(conv2d(x, w) + bias), x/w channels-last bf16.
+at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                       int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
+                       double slope) {
+  IAMD_CHECK(x.is_cuda() && w.is_cuda(), "conv2d_mfma: CUDA tensors expected");
+  IAMD_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16,
+             "conv2d_mfma: bf16 operands expected");
+  IAMD_CHECK(x.dim() == 4 && w.dim() == 4, "conv2d_mfma: 4-D tensors expected");
+  IAMD_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                 w.is_contiguous(at::MemoryFormat::ChannelsLast),
+             "conv2d_mfma: packed channels-last operands expected");
+  const int B = (int)x.size(0), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int Cout = (int)w.size(0), KH = (int)w.size(2), KW = (int)w.size(3);
+  IAMD_CHECK(w.size(1) == Cin, "conv2d_mfma: channel mismatch ", w.size(1), " vs ", Cin);
+  IAMD_CHECK(Cin % kBK == 0, "conv2d_mfma: Cin must be a multiple of 64, got ", Cin);
+  IAMD_CHECK(Cout % 64 == 0, "conv2d_mfma: Cout must be a multiple of 64, got ", Cout);
+  IAMD_CHECK(sh >= 1 && sw >= 1 && dh >= 1 && dw >= 1 && ph >= 0 && pw >= 0, "conv2d_mfma: bad geometry");
+  const int Ho = (int)((H + 2 * ph - dh * (KH - 1) - 1) / sh + 1);
+  const int Wo = (int)((W + 2 * pw - dw * (KW - 1) - 1) / sw + 1);
+  IAMD_CHECK(Ho > 0 && Wo > 0, "conv2d_mfma: empty output");
+  IAMD_CHECK((int64_t)B * H * W * Cin < (1ll << 31) && (int64_t)B * Ho * Wo * Cout < (1ll << 31),
+             "conv2d_mfma: tensor too large for 32-bit pixel indexing");
+  auto y = at::empty({B, Cout, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor bf;
+  if (bias.has_value() && bias->defined()) {
+    IAMD_CHECK(bias->numel() == Cout, "conv2d_mfma: bias size");
+    bf = bias->to(at::kFloat).contiguous();
+  }
+  ConvArgs a;
+  a.x = reinterpret_cast<const __hip_bfloat16*>(x.data_ptr());
+  a.w = reinterpret_cast<const __hip_bfloat16*>(w.data_ptr());
+  a.bias = bf.defined() ? bf.data_ptr<float>() : nullptr;
+  a.y = reinterpret_cast<__hip_bfloat16*>(y.data_ptr());
+  a.zero = zero_page(x.get_device());
+  a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
+  a.KW = KW; a.sh = (int)sh; a.sw = (int)sw; a.ph = (int)ph; a.pw = (int)pw; a.dh = (int)dh; a.dw = (int)dw;
+  a.M = B * Ho * Wo;
+  a.cpt = Cin / kBK;
+  a.nk = KH * KW * a.cpt;
+  a.slope = (float)slope;
+  const int nMt = ceil_div(a.M, kBM);
+  const bool bn128 = Cout % 128 == 0;
+  a.nNt = Cout / (bn128 ? 128 : 64);
+  const int64_t grid = (int64_t)nMt * a.nNt;
+  IAMD_CHECK(grid < (1ll << 31), "conv2d_mfma: grid too large");
+  auto launch = [&](auto bnv, auto hbv) {
+    constexpr int BN = decltype(bnv)::value;
+    constexpr bool HB = decltype(hbv)::value;
+    hipLaunchKernelGGL((conv_fwd_mfma<BN, HB>), dim3((unsigned)grid), dim3(kThreads), 0, stream(), a);
+  };
+  if (bn128) {
+    if (a.bias) launch(std::integral_constant<int, 128>(), std::true_type());
+    else launch(std::integral_constant<int, 128>(), std::false_type());
+  } else {
+    if (a.bias) launch(std::integral_constant<int, 64>(), std::true_type());
+    else launch(std::integral_constant<int, 64>(), std::false_type());
+  }
+  IAMD_LAUNCH_CHECK();
+  return y;
+}
+
+}  // namespace iamd

@@ -1,0 +1,302 @@
+// k11: weight gradient of the k10 convolution on the gfx950 matrix cores.
+//
+//   dW[n][ky][kx][ci] = sum_m dy[m][n] * x[b][oh*sh - ph + ky*dh][ow*sw - pw + kx*dw][ci]
+//
+// over all output pixels m = (b, oh, ow). As a GEMM the reduction dimension (pixels) is the
+// OUTER, strided dimension of both NHWC operands, so both MFMA fragments are read with the
+// gfx950 transposing LDS read ds_read_b64_tr_b16: each 16-lane group fetches a 4-pixel x
+// 16-channel block and every lane receives one channel's 4 pixels (cdna_hip_programming.md
+// T10). Two such reads make the 8-deep k-fragment of v_mfma_f32_16x16x32_bf16.
+//
+// Block: one filter tap x BNO output channels x BC input channels, reducing over a
+// contiguous range of 64-pixel k-steps (split-K over pixels so small-tap-count layers still
+// fill 256 CUs). Both 64-pixel tiles are staged global -> LDS with global_load_lds_dwordx4
+// into two buffers (the stage of step k+1 overlaps the MFMAs of step k). The LDS images are
+// [pixel][channel] rows whose 16-byte chunks are XOR-swizzled per row (on the global side:
+// the DMA write is lane-linear) so that the 8 rows a 32-lane half of a transposed read
+// touches fall into 8 different 32-byte bank windows: conflict-free. Out-of-image input
+// pixels (padding) and the pixel tail DMA from a zero page. Partial sums per split are
+// written as fp32 slabs [S][Cout][taps][Cin] and summed by a second, bandwidth-bound kernel
+// (one slab, S == 1, is written straight into dW).
+//
+// Reference: the reference's weight gradients come from cuDNN through nn.Conv2d autograd
+// (layers/conv.py:59-91); there is no hand-written conv in the reference.
+#include "common.h"
+
+namespace iamd {
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(3))) bf16x4* lds_bf16x4_t;
+
+constexpr int kBP = 64;  // pixels per k-step
+constexpr int kThreads = 256;
+
+struct WgradArgs {
+  const __hip_bfloat16* dy;  // [M][Cout]
+  const __hip_bfloat16* x;   // [B][H][W][Cin]
+  float* out;                // [S][Cout][KK][Cin]
+  const __hip_bfloat16* zero;
+  int Bn, H, W, Cin, Ho, Wo, Cout, KW, KK;
+  int sh, sw, ph, pw, dh, dw;
+  int M, nks, kps, nNt, nCt;
+};
+
+// 16-byte chunk swizzle of a [64 pixel rows][RB bytes] image: the 8 rows read by one 32-lane
+// half of a transposed fragment read land in distinct 32-byte bank windows.
+template <int RB>
+__device__ __forceinline__ int swz(int row) {
+  if constexpr (RB == 256) {
+    return ((row & 3) << 2) | ((row >> 2) & 3);
+  } else {
+    return ((((row >> 1) & 1) | (((row >> 3) & 1) << 1)) << 1);
+  }
+}
+
+__device__ __forceinline__ void glds16(const void* src, char* lds) {
+  __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)lds, 16, 0, 0);
+}
+
+__device__ __forceinline__ bf16x4 tr_read(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t)p);
+}
+
+template <int BNO, int BC>
+__global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma(WgradArgs a) {
+  constexpr int RA = BNO * 2, RX = BC * 2;        // image row bytes
+  constexpr int kAbytes = kBP * RA, kXbytes = kBP * RX;
+  constexpr int kStage = kAbytes + kXbytes;
+  constexpr int MI = BNO / 32, NI = BC / 32;      // 16-wide fragments per wave
+  constexpr int CPA = RA / 16, CPX = RX / 16;     // chunks per image row
+  constexpr int LA = kBP * CPA / kThreads;        // glds per thread (dy tile)
+  constexpr int LX = kBP * CPX / kThreads;        // glds per thread (x tile)
+  constexpr int RSA = kThreads / CPA, RSX = kThreads / CPX;  // rows per glds round
+  __shared__ __attribute__((aligned(16))) char smem[2 * kStage];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tiles = a.KK * a.nNt * a.nCt;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / tiles;
+  const int tile = bid - split * tiles;
+  const int tap = tile / (a.nNt * a.nCt);
+  const int r2 = tile - tap * a.nNt * a.nCt;
+  const int nt = r2 / a.nCt, ct = r2 - nt * a.nCt;
+  const int n0 = nt * BNO, c0 = ct * BC;
+  const int ky = tap / a.KW, kx = tap - ky * a.KW;
+  const int ks0 = split * a.kps;
+  const int ks1 = min(a.nks, ks0 + a.kps);
+
+  // ---- DMA bookkeeping ------------------------------------------------------------------
+  const int arow0 = tid / CPA, apos = tid % CPA;
+  const int xrow0 = tid / CPX, xpos = tid % CPX;
+  // x rows: running (b, oh, ow) of pixel m = ks * 64 + row for the step being issued
+  int xb[LX], xoh[LX], xow[LX];
+  const int HoWo = a.Ho * a.Wo;
+#pragma unroll
+  for (int i = 0; i < LX; ++i) {
+    const int m = ks0 * kBP + xrow0 + i * RSX;
+    const int b = m / HoWo, r = m - b * HoWo;
+    xb[i] = b;
+    xoh[i] = r / a.Wo;
+    xow[i] = r - xoh[i] * a.Wo;
+  }
+  const int dyc = n0 + ((apos ^ swz<RA>(arow0)) << 3);  // rows arow0 + i*RSA share row&15
+  const int xc = c0 + ((xpos ^ swz<RX>(xrow0)) << 3);
+
+  auto issue = [&](int ks, int buf) {
+    char* As = smem + buf * kStage;
+    char* Xs = As + kAbytes;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int m = ks * kBP + arow0 + i * RSA;
+      const __hip_bfloat16* src = m < a.M ? a.dy + (size_t)m * a.Cout + dyc : a.zero;
+      glds16(src, As + i * 4096 + wid * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < LX; ++i) {
+      const int ih = xoh[i] * a.sh - a.ph + ky * a.dh;
+      const int iw = xow[i] * a.sw - a.pw + kx * a.dw;
+      const bool ok = xb[i] < a.Bn && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      const __hip_bfloat16* src =
+          ok ? a.x + (((size_t)xb[i] * a.H + ih) * a.W + iw) * a.Cin + xc : a.zero;
+      glds16(src, Xs + i * 4096 + wid * 1024);
+    }
+  };
+  auto advance = [&]() {
+#pragma unroll
+    for (int i = 0; i < LX; ++i) {
+      xow[i] += kBP;
+      while (xow[i] >= a.Wo) { xow[i] -= a.Wo; ++xoh[i]; }
+      while (xoh[i] >= a.Ho) { xoh[i] -= a.Ho; ++xb[i]; }
+    }
+  };
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // transposed-read lane geometry: group g reads pixel rows 8g + q (and + 4), lane p's
+  // 8-byte quarter of the group's 16-channel (32-byte) column block
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  auto a_addr = [&](int row, int colblk) {  // colblk: first channel / 8 of the 16-ch block
+    return row * RA + ((((colblk + (p >> 1)) ^ swz<RA>(row))) << 4) + ((p & 1) << 3);
+  };
+  auto x_addr = [&](int row, int colblk) {
+    return row * RX + ((((colblk + (p >> 1)) ^ swz<RX>(row))) << 4) + ((p & 1) << 3);
+  };
+
+  issue(ks0, 0);
+  for (int ks = ks0; ks < ks1; ++ks) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (ks + 1 < ks1) {
+      advance();
+      issue(ks + 1, (ks + 1 - ks0) & 1);
+    }
+    const char* As = smem + ((ks - ks0) & 1) * kStage;
+    const char* Xs = As + kAbytes;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int r0 = kk * 32 + g * 8 + q;
+      bf16x8 af[MI], xf[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int cb = (wm * (BNO / 2) + i * 16) >> 3;
+        const bf16x4 lo = tr_read(As + a_addr(r0, cb));
+        const bf16x4 hi = tr_read(As + a_addr(r0 + 4, cb));
+        af[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int cb = (wn * (BC / 2) + j * 16) >> 3;
+        const bf16x4 lo = tr_read(Xs + x_addr(r0, cb));
+        const bf16x4 hi = tr_read(Xs + x_addr(r0 + 4, cb));
+        xf[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], xf[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // ---- fp32 partial slab: row n (4 per lane), column ci (16 lanes contiguous) -------------
+  float* o = a.out + (size_t)split * a.Cout * a.KK * a.Cin;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wm * (BNO / 2) + i * 16 + g * 4 + r;
+        const int ci = c0 + wn * (BC / 2) + j * 16 + (lane & 15);
+        o[((size_t)n * a.KK + tap) * a.Cin + ci] = acc[i][j][r];
+      }
+}
+
+__global__ void sum_splits(const float4* __restrict__ P, float4* __restrict__ out, int S,
+                           int64_t n4) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float4 s = P[i];
+    for (int k = 1; k < S; ++k) {
+      const float4 v = P[k * n4 + i];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    out[i] = s;
+  }
+}
+
+const __hip_bfloat16* zero_page_w(int dev) {
+  static void* pages[64] = {nullptr};
+  IAMD_CHECK(dev >= 0 && dev < 64, "device index");
+  if (!pages[dev]) {
+    IAMD_HIP_CHECK(hipMalloc(&pages[dev], 256));
+    IAMD_HIP_CHECK(hipMemset(pages[dev], 0, 256));
+  }
+  return reinterpret_cast<const __hip_bfloat16*>(pages[dev]);
+}
+
+}  // namespace
+
+// dW [Cout, Cin, KH, KW] fp32 (channels-last memory = [Cout][KH][KW][Cin]).
+at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t KH, int64_t KW,
+                             int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh,
+                             int64_t dw) {
+  IAMD_CHECK(dy.is_cuda() && x.is_cuda(), "conv2d_wgrad_mfma: CUDA tensors expected");
+  IAMD_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16,
+             "conv2d_wgrad_mfma: bf16 operands expected");
+  IAMD_CHECK(dy.dim() == 4 && x.dim() == 4, "conv2d_wgrad_mfma: 4-D tensors expected");
+  IAMD_CHECK(dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                 x.is_contiguous(at::MemoryFormat::ChannelsLast),
+             "conv2d_wgrad_mfma: packed channels-last operands expected");
+  const int B = (int)x.size(0), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int Cout = (int)dy.size(1), Ho = (int)dy.size(2), Wo = (int)dy.size(3);
+  IAMD_CHECK(dy.size(0) == B, "conv2d_wgrad_mfma: batch mismatch");
+  IAMD_CHECK(Cin % 64 == 0 && Cout % 64 == 0, "conv2d_wgrad_mfma: channels must be multiples of 64");
+  IAMD_CHECK(Ho == (H + 2 * ph - dh * (KH - 1) - 1) / sh + 1 &&
+                 Wo == (W + 2 * pw - dw * (KW - 1) - 1) / sw + 1,
+             "conv2d_wgrad_mfma: dy spatial size does not match the conv geometry");
+  IAMD_CHECK((int64_t)B * H * W * Cin < (1ll << 31) && (int64_t)B * Ho * Wo * Cout < (1ll << 31),
+             "conv2d_wgrad_mfma: tensor too large for 32-bit pixel indexing");
+  const int KK = (int)(KH * KW);
+  const bool bno128 = Cout % 128 == 0, bc128 = Cin % 128 == 0;
+  WgradArgs a;
+  a.dy = reinterpret_cast<const __hip_bfloat16*>(dy.data_ptr());
+  a.x = reinterpret_cast<const __hip_bfloat16*>(x.data_ptr());
+  a.zero = zero_page_w(x.get_device());
+  a.Bn = B; a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
+  a.KW = (int)KW; a.KK = KK;
+  a.sh = (int)sh; a.sw = (int)sw; a.ph = (int)ph; a.pw = (int)pw; a.dh = (int)dh; a.dw = (int)dw;
+  a.M = B * Ho * Wo;
+  a.nks = ceil_div(a.M, kBP);
+  a.nNt = Cout / (bno128 ? 128 : 64);
+  a.nCt = Cin / (bc128 ? 128 : 64);
+  const int tiles = KK * a.nNt * a.nCt;
+  int S = 1;
+  if (tiles < 512) S = std::max(1, std::min(ceil_div(1024, tiles), a.nks / 4));
+  a.kps = ceil_div(a.nks, S);
+  S = ceil_div(a.nks, a.kps);  // no empty split
+  auto dW = at::empty({Cout, Cin, KH, KW},
+                      x.options().dtype(at::kFloat).memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor part;
+  if (S > 1) {
+    part = at::empty({(int64_t)S * dW.numel()}, x.options().dtype(at::kFloat));
+    a.out = part.data_ptr<float>();
+  } else {
+    a.out = dW.data_ptr<float>();
+  }
+  const int64_t grid = (int64_t)tiles * S;
+  IAMD_CHECK(grid < (1ll << 31), "conv2d_wgrad_mfma: grid too large");
+  auto launch = [&](auto bv, auto cv) {
+    constexpr int BNO = decltype(bv)::value;
+    constexpr int BC = decltype(cv)::value;
+    hipLaunchKernelGGL((conv_wgrad_mfma<BNO, BC>), dim3((unsigned)grid), dim3(kThreads), 0,
+                       stream(), a);
+  };
+  using I64 = std::integral_constant<int, 64>;
+  using I128 = std::integral_constant<int, 128>;
+  if (bno128 && bc128) launch(I128(), I128());
+  else if (bno128) launch(I128(), I64());
+  else if (bc128) launch(I64(), I128());
+  else launch(I64(), I64());
+  IAMD_LAUNCH_CHECK();
+  if (S > 1) {
+    const int64_t n4 = dW.numel() / 4;
+    const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 4096);
+    hipLaunchKernelGGL(sum_splits, dim3(blocks), dim3(256), 0, stream(),
+                       reinterpret_cast<const float4*>(part.data_ptr<float>()),
+                       reinterpret_cast<float4*>(dW.data_ptr<float>()), S, n4);
+    IAMD_LAUNCH_CHECK();
+  }
+  return dW;
+}
+
+}  // namespace iamd

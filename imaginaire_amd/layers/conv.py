@@ -8,8 +8,10 @@ checkpoints are interchangeable.
 MI355X execution plan (decided per forward from the module types):
   * ``N`` immediately followed by a leaky/relu ``A`` → one fused HIP
     norm(+SPADE/AdaIN modulation)+activation kernel (k1, ops/norm.py);
-  * ``C`` immediately followed by a leaky/relu ``A`` (no norm between) → bias-
-    free MIOpen conv + fused bias+activation HIP epilogue (k2, ops/bias_act.py);
+  * ``C`` immediately followed by a leaky/relu ``A`` (no norm between) → one
+    MFMA implicit-GEMM conv with the bias+activation in its epilogue (k10,
+    ops/conv.py) when eligible, else bias-free MIOpen conv + fused bias+activation
+    HIP epilogue (k2, ops/bias_act.py);
   * everything else runs the module as is.
 """
 from types import SimpleNamespace
@@ -112,7 +114,13 @@ class _BaseConvBlock(nn.Module):
                         i += 2
                         continue
                     if name == 'conv' and _fusible_conv(layer):
-                        x = bias_act(_conv_nobias(layer, x), layer.bias, slope)
+                        if isinstance(layer, nn.Conv2d) and x.is_cuda:
+                            x = nhwc_conv.conv2d_act(x, _plain_conv_weight(layer), layer.bias,
+                                                     layer.stride, layer.padding, layer.dilation,
+                                                     slope) if layer.groups == 1 else \
+                                bias_act(_conv_nobias(layer, x), layer.bias, slope)
+                        else:
+                            x = bias_act(_conv_nobias(layer, x), layer.bias, slope)
                         i += 2
                         continue
             if name == 'conv' and _is_plain_conv2d(layer) and x.is_cuda:

@@ -1,18 +1,41 @@
 """NHWC convolution entry points.
 
-MIOpen's fast NHWC solvers (igemm / CK xdlops) require *packed* NHWC
-activations AND weights. When the two layouts differ (e.g. an NCHW-strided
-weight against a channels-last activation, or the NCHW output of a
-reflection pad), MIOpen falls back to its naive direct kernels — measured
-at >95% of a SPADE step on MI355X before this helper existed
-(profiles/spade_step_naive_conv_mi355x.txt). Every convolution issued by
-the framework's layers goes through here so both operands are packed
-channels-last on the GPU (a no-op when they already are).
+Every 2-D convolution issued by the framework's layers goes through here.
+
+* **MFMA path (k10, ``csrc/conv_mfma.hip``).** bf16 (autocast or bf16 tensors), groups 1,
+  Cout % 64 == 0, Cin a multiple of 64 after zero-padding (pad overhead ≤ 1/3), and enough
+  output pixels to fill the chip: the forward runs the hand-written implicit-GEMM kernel
+  (global_load_lds staging, v_mfma_f32_16x16x32_bf16, fused bias + leaky/relu epilogue);
+  the stride-1 data gradient runs the SAME kernel on the flipped, transposed weight; the
+  weight gradient runs the k11 kernel (``csrc/conv_wgrad_mfma.hip``: transposing LDS reads,
+  split-K over pixels). The activation backward + bias gradient is the k2 epilogue kernel.
+* **MIOpen path.** Everything else. MIOpen's fast NHWC solvers require *packed* NHWC
+  activations AND weights, otherwise they fall back to naive direct kernels (measured
+  at >95% of a SPADE step on MI355X, profiles/spade_step_naive_conv_mi355x.txt), so both
+  operands are made packed channels-last. Odd channel counts above 64 (185-channel label
+  maps, 188-channel D inputs) are zero-padded to a multiple of 32 first: MIOpen's igemm
+  kernels run 2.4-2.6x faster on 192 than on 185 channels
+  (profiles/conv_pad_probe_mi355x.txt).
+
+Reference: the reference's blocks call cuDNN through ``nn.Conv2d`` (layers/conv.py:59-91).
 """
+import os
+
 import torch
 import torch.nn.functional as F
 
+from imaginaire_amd.ops import _ext
+
 _CL = torch.channels_last
+# fewer 128-pixel x BN-channel tiles than this and MIOpen's split-K kernels win
+_MFMA_MIN_BLOCKS = int(os.environ.get('IMAGINAIRE_AMD_MFMA_MIN_BLOCKS', '96'))
+_MFMA_MIN_DGRAD_BLOCKS = int(os.environ.get('IMAGINAIRE_AMD_MFMA_MIN_DGRAD_BLOCKS', '512'))
+# k11 MFMA weight gradient (else MIOpen wrw)
+_MFMA_WGRAD = os.environ.get('IMAGINAIRE_AMD_MFMA_WGRAD', '1') == '1'
+
+
+def _mfma_enabled():
+    return os.environ.get('IMAGINAIRE_AMD_MFMA_CONV', '1') == '1' and not _ext.force_eager()
 
 
 def nhwc(t):
@@ -29,12 +52,148 @@ def _pad_arg(padding):
     return [pw, pw, ph, ph]
 
 
+def _pair(v):
+    return (v, v) if isinstance(v, int) else tuple(v)
+
+
+def _round_up(c, m):
+    return (c + m - 1) // m * m
+
+
+def _pad_channels(t, c):
+    """Zero-pad dim 1 of a 4-D tensor to ``c`` channels (packed channels-last result)."""
+    if t.shape[1] == c:
+        return nhwc(t)
+    out = torch.empty((t.shape[0], c, t.shape[2], t.shape[3]), dtype=t.dtype, device=t.device,
+                      memory_format=_CL)
+    out[:, t.shape[1]:].zero_()
+    out[:, :t.shape[1]] = t
+    return out
+
+
+def _compute_dtype(x, w):
+    if x.is_cuda and torch.is_autocast_enabled('cuda'):
+        return torch.get_autocast_dtype('cuda')
+    return x.dtype if x.dtype == w.dtype else None
+
+
+def _out_hw(H, W, k, stride, padding, dilation):
+    return ((H + 2 * padding[0] - dilation[0] * (k[0] - 1) - 1) // stride[0] + 1,
+            (W + 2 * padding[1] - dilation[1] * (k[1] - 1) - 1) // stride[1] + 1)
+
+
+def mfma_eligible(x, w, stride, padding, dilation, groups):
+    """True if the k10 MFMA kernel runs this conv (see module docstring)."""
+    if not (x.is_cuda and x.dim() == 4 and w.dim() == 4 and groups == 1 and _mfma_enabled()):
+        return False
+    if _compute_dtype(x, w) != torch.bfloat16:
+        return False
+    cout, cin = w.shape[0], w.shape[1]
+    if cout % 64 or cin < 48:
+        return False
+    cp = _round_up(cin, 64)
+    if cp * 3 > cin * 4:  # more than 1/3 zero channels
+        return False
+    ho, wo = _out_hw(x.shape[2], x.shape[3], w.shape[2:], stride, padding, dilation)
+    if ho <= 0 or wo <= 0:
+        return False
+    blocks = -(-x.shape[0] * ho * wo // 128) * (cout // (128 if cout % 128 == 0 else 64))
+    return blocks >= _MFMA_MIN_BLOCKS
+
+
+def _flip_t(w):
+    """[Cout, Cin, KH, KW] -> [Cin, Cout, KH, KW] spatially flipped (dgrad-as-conv weight)."""
+    return w.flip(2, 3).transpose(0, 1).contiguous(memory_format=_CL)
+
+
+class _MfmaConv2d(torch.autograd.Function):
+    """k10 forward / stride-1 dgrad, MIOpen wgrad, k2 activation + bias backward."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias, stride, padding, dilation, slope):
+        cin = w.shape[1]
+        cp = _round_up(cin, 64)
+        xb = _pad_channels(x.to(torch.bfloat16), cp)
+        wb = _pad_channels(w.to(torch.bfloat16), cp)
+        y = _ext.ext().conv2d_mfma(xb, wb, bias, stride[0], stride[1], padding[0], padding[1],
+                                   dilation[0], dilation[1], float(slope))
+        ctx.conf = (stride, padding, dilation, float(slope), cin, x.dtype, w.dtype,
+                    None if bias is None else bias.dtype, x.shape[1])
+        ctx.save_for_backward(xb, wb, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xb, wb, y = ctx.saved_tensors
+        stride, padding, dilation, slope, cin, xdt, wdt, bdt, xc = ctx.conf
+        need_x, need_w, need_b = ctx.needs_input_grad[:3]
+        dy = nhwc(dy.to(torch.bfloat16))
+        db = None
+        if slope != 1.0 or need_b:
+            dy, db = _ext.ext().bias_act_bwd(y, dy, slope)
+        dx = dw = None
+        if need_x:
+            kh, kw = wb.shape[2], wb.shape[3]
+            pt = (dilation[0] * (kh - 1) - padding[0], dilation[1] * (kw - 1) - padding[1])
+            cp = wb.shape[1]
+            dblocks = -(-dy.shape[0] * xb.shape[2] * xb.shape[3] // 128) * \
+                (cp // (128 if cp % 128 == 0 else 64))
+            # the dgrad GEMM has N = Cin: with few tiles (wide-K, narrow-N SPADE γ/β convs at
+            # 16x32) MIOpen's split-K kernels win (profiles/conv_mfma_probe_mi355x.txt)
+            if stride == (1, 1) and pt[0] >= 0 and pt[1] >= 0 and dy.shape[1] % 64 == 0 and \
+                    dblocks >= _MFMA_MIN_DGRAD_BLOCKS:
+                dx = _ext.ext().conv2d_mfma(dy, _flip_t(wb), None, 1, 1, pt[0], pt[1],
+                                            dilation[0], dilation[1], 1.0)
+            else:
+                dx = torch.ops.aten.convolution_backward(
+                    dy, xb, wb, None, stride, padding, dilation, False, [0, 0], 1,
+                    [True, False, False])[0]
+            if dx.shape[1] != xc:
+                dx = dx[:, :xc]
+            dx = dx.to(xdt)
+        if need_w:
+            if _MFMA_WGRAD:
+                dw = _ext.ext().conv2d_wgrad_mfma(dy, xb, wb.shape[2], wb.shape[3], stride[0],
+                                                  stride[1], padding[0], padding[1],
+                                                  dilation[0], dilation[1])
+            else:
+                dw = torch.ops.aten.convolution_backward(
+                    dy, xb, wb, None, stride, padding, dilation, False, [0, 0], 1,
+                    [False, True, False])[1]
+            if dw.shape[1] != cin:
+                dw = dw[:, :cin]
+            dw = dw.to(wdt)
+        if db is not None:
+            db = db.to(bdt) if need_b else None
+        return dx, dw, db, None, None, None, None
+
+
+def conv2d_act(x, weight, bias=None, stride=1, padding=0, dilation=1, slope=1.0):
+    """``act(conv2d(x, weight) + bias)`` with a leaky slope (1 = identity, 0 = relu);
+    one k10 launch when eligible, otherwise MIOpen conv + k2 bias-act epilogue."""
+    stride, padding, dilation = _pair(stride), _pair(padding), _pair(dilation)
+    if mfma_eligible(x, weight, stride, padding, dilation, 1):
+        return _MfmaConv2d.apply(x, weight, bias, stride, padding, dilation, slope)
+    from imaginaire_amd.ops.bias_act import bias_act
+    if slope == 1.0:
+        return conv2d(x, weight, bias, stride, padding, dilation)
+    return bias_act(conv2d(x, weight, None, stride, padding, dilation), bias, slope)
+
+
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1,
            padding_mode='zeros'):
     if padding_mode != 'zeros' and padding_mode is not None:
         x = F.pad(x, _pad_arg(padding), mode=padding_mode)
         padding = 0
-    if x.is_cuda:
+    if x.is_cuda and x.dim() == 4:
+        st, pd, dl = _pair(stride), _pair(padding), _pair(dilation)
+        if mfma_eligible(x, weight, st, pd, dl, groups):
+            return _MfmaConv2d.apply(x, weight, bias, st, pd, dl, 1.0)
+        cin = weight.shape[1]
+        if groups == 1 and cin > 64 and cin % 32:
+            cp = _round_up(cin, 32)
+            x = _pad_channels(x, cp)
+            weight = _pad_channels(weight, cp)
         x = nhwc(x)
         weight = nhwc(weight)
     return F.conv2d(x, weight, bias, stride, padding, dilation, groups)

@@ -9,6 +9,8 @@ import sys
 
 def family(name):
     n = name.lower()
+    if 'conv_fwd_mfma' in n:
+        return 'imaginaire_amd MFMA conv (k10)'
     if 'iamd' in n or 'imaginaire' in n or any(k in n for k in (
             'stats_partial', 'stats_finalize', 'apply_fwd', 'bwd_reduce', 'bwd_apply',
             'sum_partials', 'bias_act', 'adam_kernel', 'sn_sigma', 'ema_kernel',

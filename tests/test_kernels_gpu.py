@@ -303,3 +303,53 @@ def test_sn_scale_cast_under_bf16_autocast():
     y.backward(g)
     for (n, p), (_, pr) in zip(net.named_parameters(), ref.named_parameters()):
         torch.testing.assert_close(p.grad, pr.grad, atol=3e-2, rtol=3e-2, msg=n)
+
+
+# ---- k10 MFMA implicit-GEMM convolution ---------------------------------------------------
+_CONV_CASES = [
+    # B, Cin, Cout, H, W, k, stride, pad, dil
+    (2, 128, 128, 16, 24, 3, 1, 1, 1),
+    (1, 64, 64, 10, 13, 3, 1, 1, 1),        # M tail (130 pixels), BN = 64
+    (2, 185, 128, 12, 20, 5, 1, 2, 1),      # label-map channels -> zero-padded to 192
+    (2, 128, 256, 9, 17, 5, 1, 2, 1),
+    (2, 188, 128, 16, 32, 4, 2, 1, 1),      # PatchGAN first layer (stride 2, 4x4)
+    (1, 128, 192, 12, 12, 3, 1, 2, 2),      # dilation
+    (1, 64, 128, 7, 9, 1, 1, 0, 1),         # 1x1
+]
+
+
+@pytest.mark.parametrize('case', _CONV_CASES)
+@pytest.mark.parametrize('slope,bias', [(1.0, False), (0.2, True), (0.0, True)])
+def test_conv2d_mfma_fwd_bwd(case, slope, bias):
+    import os
+    from imaginaire_amd.ops import conv as C
+    os.environ['IMAGINAIRE_AMD_MFMA_MIN_BLOCKS'] = '0'
+    C._MFMA_MIN_BLOCKS = 0
+    C._MFMA_MIN_DGRAD_BLOCKS = 0
+    B, cin, cout, H, W, k, s, p, d = case
+    torch.manual_seed(1)
+    x = torch.randn(B, cin, H, W, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last).requires_grad_(True)
+    # asymmetric weights: catches row/col swaps in the fragment maps
+    w = (torch.randn(cout, cin, k, k, device='cuda') / (cin * k * k) ** 0.5 +
+         torch.arange(cout, device='cuda').view(-1, 1, 1, 1) * 1e-3).to(torch.bfloat16)
+    w = w.contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    b = (torch.randn(cout, device='cuda') * 0.1).requires_grad_(True) if bias else None
+    assert C.mfma_eligible(x, w, (s, s), (p, p), (d, d), 1)
+    y = C.conv2d_act(x, w, b, s, p, d, slope)
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().float().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True) if bias else None
+    yr = F.conv2d(xr, wr, br, s, p, d)
+    assert y.shape == yr.shape
+    if slope != 1.0:  # activation mask from the kernel's own output (bf16 sign ties near 0)
+        yr = torch.where(y.detach().float() > 0, yr, yr * slope)
+    err = (y.float() - yr).abs().max().item()
+    assert err <= 1e-2 * max(1.0, yr.abs().max().item()), err
+    go = torch.randn_like(yr)
+    y.backward(go.to(y.dtype))
+    yr.backward(go)
+    for got, ref, name in ((x.grad, xr.grad, 'dx'), (w.grad, wr.grad, 'dw')) + \
+            (((b.grad, br.grad, 'db'),) if bias else ()):
+        e = (got.float() - ref).abs().max().item()
+        assert e <= 2e-2 * max(1.0, ref.abs().max().item()), (name, e, ref.abs().max().item())
