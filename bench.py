@@ -53,6 +53,8 @@ def parse():
     p.add_argument('--conv-profile', action='store_true',
                    help='after warm-up, profile one step with device activity and shapes and '
                         'print GPU time per (op, input shapes) to stderr')
+    p.add_argument('--op-profile', action='store_true',
+                   help='like --conv-profile but for every aten op (self device time)')
     return p.parse_args()
 
 
@@ -132,21 +134,31 @@ def main():
         print(prof.key_averages().table(sort_by='self_cpu_time_total', row_limit=45),
               flush=True)
 
-    if args.conv_profile and rank == 0:
+    if (args.conv_profile or args.op_profile) and rank == 0:
         from torch.profiler import ProfilerActivity, profile
         torch.cuda.synchronize()
         with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA],
                      record_shapes=True) as prof:
             step(args.warmup)
             torch.cuda.synchronize()
-        rows = [e for e in prof.key_averages(group_by_input_shape=True)
-                if e.key in ('aten::convolution', 'aten::convolution_backward')]
-        rows.sort(key=lambda e: -e.device_time_total)
-        tot = sum(e.device_time_total for e in rows)
-        print('conv GPU time in one step: %.2f ms' % (tot / 1e3))
-        for e in rows[:60]:
-            print('%9.3f ms %4d  %-22s %s' % (e.device_time_total / 1e3, e.count, e.key[6:],
-                                              str(e.input_shapes)[:150]))
+        if args.op_profile:
+            rows = [e for e in prof.key_averages(group_by_input_shape=True)
+                    if e.self_device_time_total > 0]
+            rows.sort(key=lambda e: -e.self_device_time_total)
+            tot = sum(e.self_device_time_total for e in rows)
+            print('op self GPU time in one step: %.2f ms' % (tot / 1e3))
+            for e in rows[:80]:
+                print('%9.3f ms %4d  %-34s %s' % (e.self_device_time_total / 1e3, e.count,
+                                                  e.key[:34], str(e.input_shapes)[:140]))
+        else:
+            rows = [e for e in prof.key_averages(group_by_input_shape=True)
+                    if e.key in ('aten::convolution', 'aten::convolution_backward')]
+            rows.sort(key=lambda e: -e.device_time_total)
+            tot = sum(e.device_time_total for e in rows)
+            print('conv GPU time in one step: %.2f ms' % (tot / 1e3))
+            for e in rows[:60]:
+                print('%9.3f ms %4d  %-22s %s' % (e.device_time_total / 1e3, e.count, e.key[6:],
+                                                  str(e.input_shapes)[:150]))
         sys.stdout.flush()
 
     def barrier():

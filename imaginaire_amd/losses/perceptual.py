@@ -7,13 +7,15 @@ instance-normalised features and multi-scale evaluation.
 MI355X execution: the backbone is kept in bf16 channels-last when the trainer
 runs mixed precision (the reference runs it in fp16 under apex O1), the
 network is truncated after the deepest requested layer (the reference also
-computes the unused tail), and the target branch runs under ``no_grad``.
+computes the unused tail), every conv+ReLU pair is one k10 MFMA launch with
+the bias and ReLU in its epilogue, and the target branch runs under ``no_grad``.
 """
 import torch
 import torch.nn.functional as F
 from torch import nn
 
 from imaginaire_amd.models import backbones
+from imaginaire_amd.ops import conv as nhwc_conv
 from imaginaire_amd.utils.distributed import master_only_print as print
 from imaginaire_amd.utils.misc import apply_imagenet_normalization
 
@@ -109,13 +111,29 @@ class _PerceptualNetwork(nn.Module):
 
     def forward(self, x):
         output = {}
-        for i, layer in enumerate(self.network):
-            x = layer(x)
+        layers = list(self.network)
+        i = 0
+        while i < len(layers):
+            layer = layers[i]
+            nxt = layers[i + 1] if i + 1 < len(layers) else None
+            if x.is_cuda and type(layer) is nn.Conv2d and type(nxt) is nn.ReLU and \
+                    self.layer_name_mapping.get(i, None) not in self.layers and \
+                    layer.padding_mode == 'zeros' and layer.groups == 1:
+                # conv + ReLU as one k10 MFMA launch (bias + ReLU in the epilogue)
+                x = nhwc_conv.conv2d_act(x, layer.weight, layer.bias, layer.stride,
+                                         layer.padding, layer.dilation, 0.0)
+                i += 1
+            elif x.is_cuda and type(layer) is nn.Conv2d:
+                x = nhwc_conv.conv2d(x, layer.weight, layer.bias, layer.stride, layer.padding,
+                                     layer.dilation, layer.groups, layer.padding_mode)
+            else:
+                x = layer(x)
             layer_name = self.layer_name_mapping.get(i, None)
             if layer_name in self.layers:
                 output[layer_name] = x
             if i >= self.last_index:
                 break
+            i += 1
         return output
 
 

@@ -8,7 +8,8 @@ Every 2-D convolution issued by the framework's layers goes through here.
   (global_load_lds staging, v_mfma_f32_16x16x32_bf16, fused bias + leaky/relu epilogue);
   the stride-1 data gradient runs the SAME kernel on the flipped, transposed weight; the
   weight gradient runs the k11 kernel (``csrc/conv_wgrad_mfma.hip``: transposing LDS reads,
-  split-K over pixels). The activation backward + bias gradient is the k2 epilogue kernel.
+  split-K over pixels) or MIOpen's wrw, whichever was measured faster for the shape (first
+  call). The activation backward + bias gradient is the k2 epilogue kernel.
 * **MIOpen path.** Everything else. MIOpen's fast NHWC solvers require *packed* NHWC
   activations AND weights, otherwise they fall back to naive direct kernels (measured
   at >95% of a SPADE step on MI355X, profiles/spade_step_naive_conv_mi355x.txt), so both
@@ -30,8 +31,8 @@ _CL = torch.channels_last
 # fewer 128-pixel x BN-channel tiles than this and MIOpen's split-K kernels win
 _MFMA_MIN_BLOCKS = int(os.environ.get('IMAGINAIRE_AMD_MFMA_MIN_BLOCKS', '96'))
 _MFMA_MIN_DGRAD_BLOCKS = int(os.environ.get('IMAGINAIRE_AMD_MFMA_MIN_DGRAD_BLOCKS', '512'))
-# k11 MFMA weight gradient (else MIOpen wrw)
-_MFMA_WGRAD = os.environ.get('IMAGINAIRE_AMD_MFMA_WGRAD', '1') == '1'
+# weight gradient: 'auto' = per-shape faster of k11 / MIOpen wrw, '1' = k11, '0' = MIOpen
+_MFMA_WGRAD = os.environ.get('IMAGINAIRE_AMD_MFMA_WGRAD', 'auto')
 
 
 def _mfma_enabled():
@@ -89,15 +90,16 @@ def mfma_eligible(x, w, stride, padding, dilation, groups):
     if _compute_dtype(x, w) != torch.bfloat16:
         return False
     cout, cin = w.shape[0], w.shape[1]
-    if cout % 64 or cin < 48:
-        return False
-    cp = _round_up(cin, 64)
-    if cp * 3 > cin * 4:  # more than 1/3 zero channels
+    cp, op = _round_up(cin, 64), _round_up(cout, 64)
+    # zero-padded channels cost MFMA work: allow ≤ 1/3 waste, except for the thin RGB-facing
+    # convs (3-channel image in / out) where MIOpen's kernels run at ~1 TF/s and a 64-channel
+    # padded MFMA tile is still an order of magnitude faster (profiles/spade_step_k10_k11)
+    if cp * op * 3 > cin * cout * 4 and min(cin, cout) > 16:
         return False
     ho, wo = _out_hw(x.shape[2], x.shape[3], w.shape[2:], stride, padding, dilation)
     if ho <= 0 or wo <= 0:
         return False
-    blocks = -(-x.shape[0] * ho * wo // 128) * (cout // (128 if cout % 128 == 0 else 64))
+    blocks = -(-x.shape[0] * ho * wo // 128) * (op // (128 if op % 128 == 0 else 64))
     return blocks >= _MFMA_MIN_BLOCKS
 
 
@@ -106,28 +108,38 @@ def _flip_t(w):
     return w.flip(2, 3).transpose(0, 1).contiguous(memory_format=_CL)
 
 
+def _pad_rows(t, n):
+    """Zero-pad dim 0 of a weight / bias to ``n`` rows."""
+    if t is None or t.shape[0] == n:
+        return t
+    out = t.new_zeros((n,) + tuple(t.shape[1:]))
+    out[:t.shape[0]] = t
+    return out.contiguous(memory_format=_CL) if out.dim() == 4 else out
+
+
 class _MfmaConv2d(torch.autograd.Function):
-    """k10 forward / stride-1 dgrad, MIOpen wgrad, k2 activation + bias backward."""
+    """k10 forward / stride-1 dgrad, k11 wgrad, k2 activation + bias backward. Channel
+    counts are zero-padded to multiples of 64 (input) / 64 (output) around the kernels."""
 
     @staticmethod
     def forward(ctx, x, w, bias, stride, padding, dilation, slope):
-        cin = w.shape[1]
-        cp = _round_up(cin, 64)
+        cout, cin = w.shape[0], w.shape[1]
+        cp, op = _round_up(cin, 64), _round_up(cout, 64)
         xb = _pad_channels(x.to(torch.bfloat16), cp)
-        wb = _pad_channels(w.to(torch.bfloat16), cp)
-        y = _ext.ext().conv2d_mfma(xb, wb, bias, stride[0], stride[1], padding[0], padding[1],
-                                   dilation[0], dilation[1], float(slope))
-        ctx.conf = (stride, padding, dilation, float(slope), cin, x.dtype, w.dtype,
+        wb = _pad_rows(_pad_channels(w.to(torch.bfloat16), cp), op)
+        y = _ext.ext().conv2d_mfma(xb, wb, _pad_rows(bias, op), stride[0], stride[1],
+                                   padding[0], padding[1], dilation[0], dilation[1], float(slope))
+        ctx.conf = (stride, padding, dilation, float(slope), cin, cout, x.dtype, w.dtype,
                     None if bias is None else bias.dtype, x.shape[1])
         ctx.save_for_backward(xb, wb, y)
-        return y
+        return y if op == cout else y[:, :cout]
 
     @staticmethod
     def backward(ctx, dy):
         xb, wb, y = ctx.saved_tensors
-        stride, padding, dilation, slope, cin, xdt, wdt, bdt, xc = ctx.conf
+        stride, padding, dilation, slope, cin, cout, xdt, wdt, bdt, xc = ctx.conf
         need_x, need_w, need_b = ctx.needs_input_grad[:3]
-        dy = nhwc(dy.to(torch.bfloat16))
+        dy = _pad_channels(dy.to(torch.bfloat16), wb.shape[0])
         db = None
         if slope != 1.0 or need_b:
             dy, db = _ext.ext().bias_act_bwd(y, dy, slope)
@@ -140,7 +152,7 @@ class _MfmaConv2d(torch.autograd.Function):
                 (cp // (128 if cp % 128 == 0 else 64))
             # the dgrad GEMM has N = Cin: with few tiles (wide-K, narrow-N SPADE γ/β convs at
             # 16x32) MIOpen's split-K kernels win (profiles/conv_mfma_probe_mi355x.txt)
-            if stride == (1, 1) and pt[0] >= 0 and pt[1] >= 0 and dy.shape[1] % 64 == 0 and \
+            if stride == (1, 1) and pt[0] >= 0 and pt[1] >= 0 and \
                     dblocks >= _MFMA_MIN_DGRAD_BLOCKS:
                 dx = _ext.ext().conv2d_mfma(dy, _flip_t(wb), None, 1, 1, pt[0], pt[1],
                                             dilation[0], dilation[1], 1.0)
@@ -152,20 +164,54 @@ class _MfmaConv2d(torch.autograd.Function):
                 dx = dx[:, :xc]
             dx = dx.to(xdt)
         if need_w:
-            if _MFMA_WGRAD:
-                dw = _ext.ext().conv2d_wgrad_mfma(dy, xb, wb.shape[2], wb.shape[3], stride[0],
-                                                  stride[1], padding[0], padding[1],
-                                                  dilation[0], dilation[1])
-            else:
-                dw = torch.ops.aten.convolution_backward(
-                    dy, xb, wb, None, stride, padding, dilation, False, [0, 0], 1,
-                    [False, True, False])[1]
-            if dw.shape[1] != cin:
-                dw = dw[:, :cin]
+            dw = _wgrad(dy, xb, wb, stride, padding, dilation)
+            if dw.shape[0] != cout or dw.shape[1] != cin:
+                dw = dw[:cout, :cin]
             dw = dw.to(wdt)
         if db is not None:
-            db = db.to(bdt) if need_b else None
+            db = db[:cout].to(bdt) if need_b else None
         return dx, dw, db, None, None, None, None
+
+
+_WGRAD_CHOICE = {}
+
+
+def _wgrad(dy, xb, wb, stride, padding, dilation):
+    """Weight gradient: k11 or MIOpen wrw, whichever measured faster for this shape (timed
+    once per shape, both paths warm; ``IMAGINAIRE_AMD_MFMA_WGRAD`` = auto | 1 | 0)."""
+    def k11():
+        return _ext.ext().conv2d_wgrad_mfma(dy, xb, wb.shape[2], wb.shape[3], stride[0],
+                                            stride[1], padding[0], padding[1], dilation[0],
+                                            dilation[1])
+
+    def miopen():
+        return torch.ops.aten.convolution_backward(
+            dy, xb, wb, None, stride, padding, dilation, False, [0, 0], 1,
+            [False, True, False])[1]
+
+    mode = _MFMA_WGRAD
+    if mode == '1':
+        return k11()
+    if mode == '0':
+        return miopen()
+    key = (tuple(dy.shape), tuple(xb.shape), tuple(wb.shape), stride, padding, dilation)
+    choice = _WGRAD_CHOICE.get(key)
+    if choice is None:
+        if torch.cuda.is_current_stream_capturing():
+            return k11()
+        times = {}
+        for name, fn in (('k11', k11), ('miopen', miopen)):
+            fn()  # warm (MIOpen find / compile)
+            start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            start.record()
+            for _ in range(3):
+                fn()
+            end.record()
+            end.synchronize()
+            times[name] = start.elapsed_time(end)
+        choice = min(times, key=times.get)
+        _WGRAD_CHOICE[key] = choice
+    return k11() if choice == 'k11' else miopen()
 
 
 def conv2d_act(x, weight, bias=None, stride=1, padding=0, dilation=1, slope=1.0):

@@ -315,6 +315,9 @@ _CONV_CASES = [
     (2, 188, 128, 16, 32, 4, 2, 1, 1),      # PatchGAN first layer (stride 2, 4x4)
     (1, 128, 192, 12, 12, 3, 1, 2, 2),      # dilation
     (1, 64, 128, 7, 9, 1, 1, 0, 1),         # 1x1
+    (2, 3, 64, 16, 24, 3, 1, 1, 1),         # RGB in: Cin padded 3 -> 64
+    (2, 64, 3, 16, 24, 3, 1, 1, 1),         # RGB out: Cout padded 3 -> 64
+    (1, 128, 100, 12, 12, 3, 1, 1, 1),      # Cout padded 100 -> 128
 ]
 
 
@@ -326,6 +329,7 @@ def test_conv2d_mfma_fwd_bwd(case, slope, bias):
     os.environ['IMAGINAIRE_AMD_MFMA_MIN_BLOCKS'] = '0'
     C._MFMA_MIN_BLOCKS = 0
     C._MFMA_MIN_DGRAD_BLOCKS = 0
+    C._MFMA_WGRAD = 'auto' if slope == 0.0 else '1'
     B, cin, cout, H, W, k, s, p, d = case
     torch.manual_seed(1)
     x = torch.randn(B, cin, H, W, device='cuda').to(torch.bfloat16).contiguous(
