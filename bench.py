@@ -143,7 +143,8 @@ def main():
             torch.cuda.synchronize()
         if args.op_profile:
             rows = [e for e in prof.key_averages(group_by_input_shape=True)
-                    if e.self_device_time_total > 0]
+                    if e.self_device_time_total > 0 and e.input_shapes is not None and
+                    not e.key.startswith(('void', 'igemm', 'iamd', '__amd', 'Sub'))]
             rows.sort(key=lambda e: -e.self_device_time_total)
             tot = sum(e.self_device_time_total for e in rows)
             print('op self GPU time in one step: %.2f ms' % (tot / 1e3))

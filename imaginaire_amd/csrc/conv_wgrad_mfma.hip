@@ -260,8 +260,23 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
   a.nNt = Cout / (bno128 ? 128 : 64);
   a.nCt = Cin / (bc128 ? 128 : 64);
   const int tiles = KK * a.nNt * a.nCt;
+  // split-K factor: fill the chip in whole rounds of co-resident blocks (2 / 3 / 5 blocks
+  // per CU for the 64 / 48 / 32 KB LDS variants): a 2.3-round grid leaves the last round a
+  // third full (measured: 1200 blocks ran at 28% MFMA issue vs 44% for k10,
+  // profiles/pmc_conv_mi355x.txt)
+  const int slots = 256 * ((bno128 && bc128) ? 2 : (bno128 || bc128) ? 3 : 5);
   int S = 1;
-  if (tiles < 512) S = std::max(1, std::min(ceil_div(1024, tiles), a.nks / 4));
+  if (tiles < slots) {
+    const int smax = std::max(1, std::min(64, a.nks / 4));
+    double best = -1.0;
+    for (int s = 1; s <= smax; ++s) {
+      const int blocks = tiles * s;
+      if (blocks < slots * 9 / 10 && s != smax) continue;
+      const double eff = (double)blocks / ((double)ceil_div(blocks, slots) * slots);
+      if (eff > best + 1e-3) { best = eff; S = s; }
+      if (blocks >= 2 * slots) break;
+    }
+  }
   a.kps = ceil_div(a.nks, S);
   S = ceil_div(a.nks, a.kps);  // no empty split
   auto dW = at::empty({Cout, Cin, KH, KW},

@@ -44,6 +44,11 @@ class FPSEDiscriminator(nn.Module):
         self.seg = Conv2dBlock(num_filters * 2, num_filters * 2, kernel_size=1)
         self.embedding = Conv2dBlock(num_labels, num_filters * 2, kernel_size=1)
 
+    def _embedding_is_linear(self):
+        layers = self.embedding.layers
+        return list(layers.keys()) == ['conv'] and type(layers['conv']) is nn.Conv2d and \
+            layers['conv'].kernel_size == (1, 1) and layers['conv'].stride == (1, 1)
+
     def forward(self, images, segmaps):
         feat11 = self.enc1(images)
         feat12 = self.enc2(feat11)
@@ -63,8 +68,13 @@ class FPSEDiscriminator(nn.Module):
         seg2 = self.seg(feat32)
         seg3 = self.seg(feat33)
         seg4 = self.seg(feat34)
-        segembs = self.embedding(segmaps)
-        segembs = F.avg_pool2d(segembs, kernel_size=2, stride=2)
+        # avg_pool(conv1x1(s)) == conv1x1(avg_pool(s)) for the linear, bias-only embedding
+        # block: pool the label map first so the 1x1 conv (and its weight gradient) runs at
+        # half resolution and the full-resolution 2F-channel embedding is never materialised
+        if self._embedding_is_linear():
+            segembs = self.embedding(F.avg_pool2d(segmaps, kernel_size=2, stride=2))
+        else:
+            segembs = F.avg_pool2d(self.embedding(segmaps), kernel_size=2, stride=2)
         segembs2 = F.avg_pool2d(segembs, kernel_size=2, stride=2)
         segembs3 = F.avg_pool2d(segembs2, kernel_size=2, stride=2)
         segembs4 = F.avg_pool2d(segembs3, kernel_size=2, stride=2)

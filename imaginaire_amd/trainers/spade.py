@@ -64,7 +64,15 @@ class Trainer(BaseTrainer):
             data['label'] = torch.cat([label_label, label_image], 1)
             data['images'] = images
         data = self.to_device(data)
-        return self._resize_data(data)
+        data = self._resize_data(data)
+        if self.amp_dtype is not None:
+            # every consumer of the one-hot label map and the real image is a bf16 conv
+            # (SPADE MLPs, D, VGG): cast once here instead of at each of the ~40 convs, and
+            # halve the bytes of the D-input concatenations / resizes
+            for key in ('label', 'images'):
+                if key in data and torch.is_tensor(data[key]) and data[key].is_floating_point():
+                    data[key] = data[key].to(self.amp_dtype)
+        return data
 
     def gen_forward(self, data):
         net_G_output = self.net_G(data)

@@ -1,0 +1,20 @@
+#!/bin/bash
+# PMC counter passes over one k10 (fwd) and one k11 (wgrad) shape; one rocprofv3 run per pass.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+ROOT=$(pwd)
+mkdir -p gpurun_out/pmc
+cd /tmp && export TMPDIR=/tmp
+SHAPE="4 128 1024 128 256 5"
+P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES"
+P2="SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_INSTS_SALU SQ_INSTS_VMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA SQ_INST_CYCLES_VMEM SQ_WAIT_INST_ANY"
+for mode in fwd wgrad; do
+  for pass in 1 2; do
+    eval "CTRS=\$P$pass"
+    rm -rf /tmp/pmc_$mode$pass
+    timeout -s KILL 120 rocprofv3 --pmc $CTRS --output-format csv -d /tmp/pmc_$mode$pass -o run -- \
+      python3 "$ROOT/scripts/probe/conv_kernel_driver.py" $mode $SHAPE 10 > "$ROOT/gpurun_out/pmc/${mode}_$pass.log" 2>&1
+    rc=$?; echo "[pmc] $mode pass $pass rc=$rc"
+    [ $rc -eq 0 ] || exit $rc
+    find /tmp/pmc_$mode$pass -name '*counter_collection*.csv' -exec cp {} "$ROOT/gpurun_out/pmc/${mode}_$pass.csv" \;
+  done
+done

@@ -1,0 +1,29 @@
+"""Run one k10 / k11 conv shape N times (target for rocprofv3 --pmc counter passes).
+
+    python scripts/probe/conv_kernel_driver.py {fwd|wgrad} B Cin Cout H W k [iters]
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from imaginaire_amd.ops import _ext  # noqa: E402
+
+mode = sys.argv[1]
+B, cin, cout, H, W, k = (int(v) for v in sys.argv[2:8])
+iters = int(sys.argv[8]) if len(sys.argv) > 8 else 20
+CL = torch.channels_last
+pad = (k - 1) // 2
+x = torch.randn(B, cin, H, W, device='cuda', dtype=torch.bfloat16).contiguous(memory_format=CL)
+w = (torch.randn(cout, cin, k, k, device='cuda', dtype=torch.bfloat16) * 0.02).contiguous(
+    memory_format=CL)
+g = torch.randn(B, cout, H, W, device='cuda', dtype=torch.bfloat16).contiguous(memory_format=CL)
+ext = _ext.ext()
+for _ in range(iters):
+    if mode == 'fwd':
+        ext.conv2d_mfma(x, w, None, 1, 1, pad, pad, 1, 1, 1.0)
+    else:
+        ext.conv2d_wgrad_mfma(g, x, k, k, 1, 1, pad, pad, 1, 1)
+torch.cuda.synchronize()
+print('done', mode)

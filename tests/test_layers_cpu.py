@@ -150,3 +150,20 @@ def test_linear_block_and_weight_demod():
              weight_norm_params=NS(cond_dims=8))
     y = blk(torch.randn(2, 4, 5, 5), torch.randn(2, 8))
     assert y.shape == (2, 6, 5, 5)
+
+
+def test_fpse_pool_first_embedding_matches_reference_order():
+    """conv1x1 -> avg_pool (reference discriminators/fpse.py:118-122) == avg_pool -> conv1x1."""
+    import torch
+    from imaginaire_amd.discriminators.fpse import FPSEDiscriminator
+    torch.manual_seed(0)
+    d = FPSEDiscriminator(3, 7, 8, 3, 'spectral', 'none')
+    img = torch.randn(2, 3, 32, 64)
+    seg = torch.randn(2, 7, 32, 64)
+    d.eval()
+    assert d._embedding_is_linear()
+    fast = d(img, seg)
+    d._embedding_is_linear = lambda: False
+    ref = d(img, seg)
+    for a, b in zip(fast, ref):
+        assert torch.allclose(a, b, atol=1e-5, rtol=1e-4)
