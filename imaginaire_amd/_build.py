@@ -111,6 +111,12 @@ def build(jobs=None, force=False, verbose=True):
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError('link failed: {}\n{}\n{}'.format(' '.join(cmd), r.stdout, r.stderr))
+    # a host pass that silently drops a kernel's launch stub links fine and fails only at
+    # import time (undefined __device_stub__ symbol): check the fresh object before publishing
+    r2 = subprocess.run(['nm', '-u', '-C', TARGET + '.tmp'], capture_output=True, text=True)
+    missing = [ln for ln in r2.stdout.splitlines() if '__device_stub__' in ln]
+    if missing:
+        raise RuntimeError('link produced undefined kernel stubs:\n' + '\n'.join(missing))
     os.replace(TARGET + '.tmp', TARGET)
     if verbose:
         print('[imaginaire_amd._build] built %s from %d sources' % (TARGET, len(objs)))

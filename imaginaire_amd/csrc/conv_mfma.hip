@@ -14,11 +14,12 @@
 //
 // Block tile 128 (pixels) x BN (channels) x 64 (k), 256 threads = 4 wave64s in a 2x2 grid,
 // each wave owns a 64 x BN/2 sub-tile of v_mfma_f32_16x16x32_bf16 accumulators.
-// Staging: global -> LDS with global_load_lds_dwordx4 (no VGPR round trip), two LDS buffers,
+// Staging: global -> LDS with buffer_load_dwordx4 ... lds (no VGPR round trip), two LDS buffers,
 // one barrier per k-step; the load of step k+1 is in flight while step k runs on the MFMAs.
-// Padding pixels (outside the image) point their DMA at a 16-byte zero page instead of
-// branching. LDS rows are 128 B; the 16-B chunk index is XOR-swizzled with (row & 7) on the
-// global side (the LDS write of a DMA is lane-linear), which makes the ds_read_b128 fragment
+// Padding pixels (outside the image) and the pixel tail get an out-of-range buffer offset and
+// the buffer unit returns zeros (no branch, no zero page); per-row tap-validity bit masks and
+// SGPR-resident tap/k-step offsets keep the per-load VALU work to a select and an add.
+// LDS rows are 128 B; the 16-B chunk index is XOR-swizzled with (row & 7) on the global side (the LDS write of a DMA is lane-linear), which makes the ds_read_b128 fragment
 // reads bank-conflict free. Epilogue: + bias, leaky/relu slope, bf16, staged through LDS so
 // every global store is a 16-byte row segment. Block ids are XCD-remapped so the BN-tiles
 // that share one pixel tile run on the same XCD (shared L2 for the activation halo).
@@ -37,24 +38,28 @@ constexpr int kThreads = 256;
 constexpr int kRowBytes = kBK * 2;  // 128 B per staged row
 constexpr int kEpiStride = 272;     // epilogue LDS row stride in bytes (BN<=128 bf16 + 16 pad)
 
+// buffer-resource word 3 for raw (unformatted, stride-0) buffers on gfx9-family parts
+constexpr int kBufCfg = 0x00020000;
+// a byte offset past every tensor this kernel accepts (< 2^31 bytes): the buffer unit
+// returns zeros for it
+constexpr int kOobOffset = 0x7ffffff0;
+
 struct ConvArgs {
   const __hip_bfloat16* x;
   const __hip_bfloat16* w;
   const float* bias;
   __hip_bfloat16* y;
-  const __hip_bfloat16* zero;
+  int xbytes, wbytes;
   int H, W, Cin, Ho, Wo, Cout;
-  int KW, sh, sw, ph, pw, dh, dw;
+  int KH, KW, sh, sw, ph, pw, dh, dw;
   int M, nk, cpt, nNt;
   float slope;
 };
 
-__device__ __forceinline__ void glds16(const void* src, char* lds) {
-  __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)lds, 16, 0, 0);
-}
-
 template <int BN, bool HAS_BIAS>
 __global__ __launch_bounds__(kThreads, 2) void conv_fwd_mfma(ConvArgs a) {
+  // The buffer-resource builtins have no host form; the host pass only needs the launch stub.
+#if defined(__HIP_DEVICE_COMPILE__)
   constexpr int NI = BN / 32;                 // 16-wide n-fragments per wave
   constexpr int kAbytes = kBM * kRowBytes;    // 16 KB
   constexpr int kBbytes = BN * kRowBytes;     // 8 / 16 KB
@@ -68,47 +73,59 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_mfma(ConvArgs a) {
   const int mt = bid / a.nNt, nt = bid - mt * a.nNt;
   const int m0 = mt * kBM, n0 = nt * BN;
 
-  // ---- per-thread DMA sources: rows lrow + 32 i, chunk c_sw (swizzled) -----------------
+  // ---- per-thread DMA sources: rows lrow + 32 i, chunk csw (swizzled) -------------------
+  // Buffer-resource loads straight into LDS: the per-lane 32-bit byte offset selects the
+  // pixel row, the wave-uniform parts (tap, channel block, k-step) ride in SGPRs, and an
+  // out-of-range offset (padding pixels, M tail) returns zeros from the buffer unit itself.
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__hip_bfloat16*>(a.x), 0, a.xbytes, kBufCfg);
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__hip_bfloat16*>(a.w), 0, a.wbytes, kBufCfg);
   const int lrow = tid >> 3;
   const int csw = (tid & 7) ^ (lrow & 7);
   const int HoWo = a.Ho * a.Wo;
-  int a_ih[4], a_iw[4];
-  const __hip_bfloat16* a_base[4];
+  int a_off[4];
+  uint32_t a_rmask[4], a_cmask[4];  // bit ky / kx set when that filter row / column is inside
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    int m = m0 + lrow + 32 * i;
+    const int m = m0 + lrow + 32 * i;
+    a_off[i] = 0;
+    a_rmask[i] = 0;
+    a_cmask[i] = 0;
     if (m < a.M) {
-      int b = m / HoWo, r = m - b * HoWo;
-      int oh = r / a.Wo, ow = r - oh * a.Wo;
-      a_ih[i] = oh * a.sh - a.ph;
-      a_iw[i] = ow * a.sw - a.pw;
-      a_base[i] = a.x + (size_t)b * a.H * a.W * a.Cin + csw * 8;
-    } else {
-      a_ih[i] = -(1 << 29);  // never inside the image
-      a_iw[i] = 0;
-      a_base[i] = a.x;
+      const int b = m / HoWo, r = m - b * HoWo;
+      const int oh = r / a.Wo, ow = r - oh * a.Wo;
+      const int ih0 = oh * a.sh - a.ph, iw0 = ow * a.sw - a.pw;
+      a_off[i] = (((b * a.H + ih0) * a.W + iw0) * a.Cin + csw * 8) * 2;
+      for (int ky = 0; ky < a.KH; ++ky)
+        a_rmask[i] |= (uint32_t)((unsigned)(ih0 + ky * a.dh) < (unsigned)a.H) << ky;
+      for (int kx = 0; kx < a.KW; ++kx)
+        a_cmask[i] |= (uint32_t)((unsigned)(iw0 + kx * a.dw) < (unsigned)a.W) << kx;
     }
   }
-  const size_t wrow = (size_t)a.nk * kBK;  // = KH*KW*Cin
-  const __hip_bfloat16* b_base[kBLoads];
+  const int wrow_bytes = a.nk * kBK * 2;  // = KH*KW*Cin*2
+  int b_off[kBLoads];
 #pragma unroll
-  for (int i = 0; i < kBLoads; ++i) b_base[i] = a.w + (size_t)(n0 + lrow + 32 * i) * wrow + csw * 8;
+  for (int i = 0; i < kBLoads; ++i) b_off[i] = (n0 + lrow + 32 * i) * wrow_bytes + csw * 16;
 
   auto issue = [&](int ks, int buf) {
     const int tap = ks / a.cpt;
     const int c0 = (ks - tap * a.cpt) * kBK;
     const int ky = tap / a.KW, kx = tap - ky * a.KW;
+    const int tapoff = ((ky * a.dh * a.W + kx * a.dw) * a.Cin + c0) * 2;
     char* As = smem + buf * kStage;
     char* Bs = As + kAbytes;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int ih = a_ih[i] + ky * a.dh, iw = a_iw[i] + kx * a.dw;
-      const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-      const __hip_bfloat16* src = ok ? a_base[i] + ((size_t)ih * a.W + iw) * a.Cin + c0 : a.zero;
-      glds16(src, As + i * 4096 + wid * 1024);
+      const bool ok = (a_rmask[i] >> ky) & (a_cmask[i] >> kx) & 1u;
+      const int voff = ok ? a_off[i] + tapoff : kOobOffset;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(As + i * 4096 + wid * 1024), 16,
+                                               voff, 0, 0, 0);
     }
 #pragma unroll
-    for (int i = 0; i < kBLoads; ++i) glds16(b_base[i] + (size_t)ks * kBK, Bs + i * 4096 + wid * 1024);
+    for (int i = 0; i < kBLoads; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)(Bs + i * 4096 + wid * 1024), 16,
+                                               b_off[i], ks * kBK * 2, 0, 0);
   };
 
   f32x4 acc[4][NI];
@@ -175,16 +192,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_mfma(ConvArgs a) {
       *reinterpret_cast<uint4*>(a.y + (size_t)m * a.Cout + n0 + ch * 8) = v;
     }
   }
-}
-
-const __hip_bfloat16* zero_page(int dev) {
-  static void* pages[64] = {nullptr};
-  IAMD_CHECK(dev >= 0 && dev < 64, "device index");
-  if (!pages[dev]) {
-    IAMD_HIP_CHECK(hipMalloc(&pages[dev], 256));
-    IAMD_HIP_CHECK(hipMemset(pages[dev], 0, 256));
-  }
-  return reinterpret_cast<const __hip_bfloat16*>(pages[dev]);
+#endif  // __HIP_DEVICE_COMPILE__
 }
 
 }  // namespace
@@ -209,8 +217,10 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
   const int Ho = (int)((H + 2 * ph - dh * (KH - 1) - 1) / sh + 1);
   const int Wo = (int)((W + 2 * pw - dw * (KW - 1) - 1) / sw + 1);
   IAMD_CHECK(Ho > 0 && Wo > 0, "conv2d_mfma: empty output");
-  IAMD_CHECK((int64_t)B * H * W * Cin < (1ll << 31) && (int64_t)B * Ho * Wo * Cout < (1ll << 31),
-             "conv2d_mfma: tensor too large for 32-bit pixel indexing");
+  IAMD_CHECK((int64_t)B * H * W * Cin * 2 < kOobOffset && w.numel() * 2 < kOobOffset &&
+                 (int64_t)B * Ho * Wo * Cout < (1ll << 31),
+             "conv2d_mfma: tensor too large for 32-bit buffer offsets");
+  IAMD_CHECK(KH <= 32 && KW <= 32, "conv2d_mfma: filter larger than 32x32");
   auto y = at::empty({B, Cout, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   at::Tensor bf;
   if (bias.has_value() && bias->defined()) {
@@ -222,7 +232,9 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
   a.w = reinterpret_cast<const __hip_bfloat16*>(w.data_ptr());
   a.bias = bf.defined() ? bf.data_ptr<float>() : nullptr;
   a.y = reinterpret_cast<__hip_bfloat16*>(y.data_ptr());
-  a.zero = zero_page(x.get_device());
+  a.xbytes = (int)(x.numel() * 2);
+  a.wbytes = (int)(w.numel() * 2);
+  a.KH = KH;
   a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
   a.KW = KW; a.sh = (int)sh; a.sw = (int)sw; a.ph = (int)ph; a.pw = (int)pw; a.dh = (int)dh; a.dw = (int)dw;
   a.M = B * Ho * Wo;

@@ -14,8 +14,10 @@
 // into two buffers (the stage of step k+1 overlaps the MFMAs of step k). The LDS images are
 // [pixel][channel] rows whose 16-byte chunks are XOR-swizzled per row (on the global side:
 // the DMA write is lane-linear) so that the 8 rows a 32-lane half of a transposed read
-// touches fall into 8 different 32-byte bank windows: conflict-free. Out-of-image input
-// pixels (padding) and the pixel tail DMA from a zero page. Partial sums per split are
+// touches fall into 8 different 32-byte bank windows: conflict-free. The DMA is
+// buffer_load ... lds: out-of-image input pixels (padding) and the pixel tail get an
+// out-of-range offset and read as zeros; when Wo % 64 == 0 a k-step is one output-row
+// segment and its pixel coordinates are wave-uniform scalars. Partial sums per split are
 // written as fp32 slabs [S][Cout][taps][Cin] and summed by a second, bandwidth-bound kernel
 // (one slab, S == 1, is written straight into dW).
 //
@@ -35,11 +37,16 @@ typedef __attribute__((address_space(3))) bf16x4* lds_bf16x4_t;
 constexpr int kBP = 64;  // pixels per k-step
 constexpr int kThreads = 256;
 
+// buffer-resource word 3 for raw (unformatted, stride-0) buffers on gfx9-family parts
+constexpr int kBufCfg = 0x00020000;
+// a byte offset past every tensor this kernel accepts: the buffer unit returns zeros for it
+constexpr int kOobOffset = 0x7ffffff0;
+
 struct WgradArgs {
   const __hip_bfloat16* dy;  // [M][Cout]
   const __hip_bfloat16* x;   // [B][H][W][Cin]
   float* out;                // [S][Cout][KK][Cin]
-  const __hip_bfloat16* zero;
+  int dybytes, xbytes;
   int Bn, H, W, Cin, Ho, Wo, Cout, KW, KK;
   int sh, sw, ph, pw, dh, dw;
   int M, nks, kps, nNt, nCt;
@@ -56,16 +63,14 @@ __device__ __forceinline__ int swz(int row) {
   }
 }
 
-__device__ __forceinline__ void glds16(const void* src, char* lds) {
-  __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)lds, 16, 0, 0);
-}
-
 __device__ __forceinline__ bf16x4 tr_read(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t)p);
 }
 
-template <int BNO, int BC>
+template <int BNO, int BC, bool ROWS>
 __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma(WgradArgs a) {
+  // The buffer-resource builtins have no host form; the host pass only needs the launch stub.
+#if defined(__HIP_DEVICE_COMPILE__)
   constexpr int RA = BNO * 2, RX = BC * 2;        // image row bytes
   constexpr int kAbytes = kBP * RA, kXbytes = kBP * RX;
   constexpr int kStage = kAbytes + kXbytes;
@@ -91,47 +96,87 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma(WgradArgs a) {
   const int ks1 = min(a.nks, ks0 + a.kps);
 
   // ---- DMA bookkeeping ------------------------------------------------------------------
+  // buffer_load ... lds: per-lane 32-bit byte offsets, wave-uniform parts in SGPRs, and an
+  // out-of-range offset (padding pixels, pixel tail) reads as zeros.
+  const __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__hip_bfloat16*>(a.dy), 0, a.dybytes, kBufCfg);
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__hip_bfloat16*>(a.x), 0, a.xbytes, kBufCfg);
   const int arow0 = tid / CPA, apos = tid % CPA;
   const int xrow0 = tid / CPX, xpos = tid % CPX;
-  // x rows: running (b, oh, ow) of pixel m = ks * 64 + row for the step being issued
-  int xb[LX], xoh[LX], xow[LX];
-  const int HoWo = a.Ho * a.Wo;
-#pragma unroll
-  for (int i = 0; i < LX; ++i) {
-    const int m = ks0 * kBP + xrow0 + i * RSX;
-    const int b = m / HoWo, r = m - b * HoWo;
-    xb[i] = b;
-    xoh[i] = r / a.Wo;
-    xow[i] = r - xoh[i] * a.Wo;
-  }
   const int dyc = n0 + ((apos ^ swz<RA>(arow0)) << 3);  // rows arow0 + i*RSA share row&15
   const int xc = c0 + ((xpos ^ swz<RX>(xrow0)) << 3);
+  int dy_off[LA];
+#pragma unroll
+  for (int i = 0; i < LA; ++i) dy_off[i] = ((arow0 + i * RSA) * a.Cout + dyc) * 2;
+  const int dy_step = kBP * a.Cout * 2;
+  const int HoWo = a.Ho * a.Wo;
+  // ROWS (Wo % 64 == 0): a k-step is 64 consecutive pixels of ONE output row, so (b, oh, ow0)
+  // are wave-uniform scalars advanced by 64 per step; otherwise each lane tracks its pixels.
+  int sb = 0, soh = 0, sow = 0;
+  int xb[LX], xoh[LX], xow[LX];
+  if constexpr (ROWS) {
+    const int m = ks0 * kBP;
+    sb = m / HoWo;
+    const int r = m - sb * HoWo;
+    soh = r / a.Wo;
+    sow = r - soh * a.Wo;
+  } else {
+#pragma unroll
+    for (int i = 0; i < LX; ++i) {
+      const int m = ks0 * kBP + xrow0 + i * RSX;
+      const int b = m / HoWo, r = m - b * HoWo;
+      xb[i] = b;
+      xoh[i] = r / a.Wo;
+      xow[i] = r - xoh[i] * a.Wo;
+    }
+  }
 
   auto issue = [&](int ks, int buf) {
     char* As = smem + buf * kStage;
     char* Xs = As + kAbytes;
 #pragma unroll
-    for (int i = 0; i < LA; ++i) {
-      const int m = ks * kBP + arow0 + i * RSA;
-      const __hip_bfloat16* src = m < a.M ? a.dy + (size_t)m * a.Cout + dyc : a.zero;
-      glds16(src, As + i * 4096 + wid * 1024);
-    }
+    for (int i = 0; i < LA; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(dyr, (lds_ptr_t)(As + i * 4096 + wid * 1024), 16,
+                                               dy_off[i], ks * dy_step, 0, 0);
+    if constexpr (ROWS) {
+      const int ih = soh * a.sh - a.ph + ky * a.dh;
+      const bool rowok = sb < a.Bn && (unsigned)ih < (unsigned)a.H;
+      const int soff = rowok ? (sb * a.H + ih) * a.W * a.Cin * 2 : 0;
 #pragma unroll
-    for (int i = 0; i < LX; ++i) {
-      const int ih = xoh[i] * a.sh - a.ph + ky * a.dh;
-      const int iw = xow[i] * a.sw - a.pw + kx * a.dw;
-      const bool ok = xb[i] < a.Bn && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-      const __hip_bfloat16* src =
-          ok ? a.x + (((size_t)xb[i] * a.H + ih) * a.W + iw) * a.Cin + xc : a.zero;
-      glds16(src, Xs + i * 4096 + wid * 1024);
+      for (int i = 0; i < LX; ++i) {
+        const int iw = (sow + xrow0 + i * RSX) * a.sw - a.pw + kx * a.dw;
+        const bool ok = rowok && (unsigned)iw < (unsigned)a.W;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(Xs + i * 4096 + wid * 1024), 16,
+                                                 ok ? (iw * a.Cin + xc) * 2 : kOobOffset, soff,
+                                                 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < LX; ++i) {
+        const int ih = xoh[i] * a.sh - a.ph + ky * a.dh;
+        const int iw = xow[i] * a.sw - a.pw + kx * a.dw;
+        const bool ok = xb[i] < a.Bn && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            xrs, (lds_ptr_t)(Xs + i * 4096 + wid * 1024), 16,
+            ok ? (((xb[i] * a.H + ih) * a.W + iw) * a.Cin + xc) * 2 : kOobOffset, 0, 0, 0);
+      }
     }
   };
   auto advance = [&]() {
+    if constexpr (ROWS) {
+      sow += kBP;
+      if (sow >= a.Wo) {
+        sow = 0;
+        if (++soh >= a.Ho) { soh = 0; ++sb; }
+      }
+    } else {
 #pragma unroll
-    for (int i = 0; i < LX; ++i) {
-      xow[i] += kBP;
-      while (xow[i] >= a.Wo) { xow[i] -= a.Wo; ++xoh[i]; }
-      while (xoh[i] >= a.Ho) { xoh[i] -= a.Ho; ++xb[i]; }
+      for (int i = 0; i < LX; ++i) {
+        xow[i] += kBP;
+        while (xow[i] >= a.Wo) { xow[i] -= a.Wo; ++xoh[i]; }
+        while (xoh[i] >= a.Ho) { xoh[i] -= a.Ho; ++xb[i]; }
+      }
     }
   };
 
@@ -199,6 +244,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma(WgradArgs a) {
         const int ci = c0 + wn * (BC / 2) + j * 16 + (lane & 15);
         o[((size_t)n * a.KK + tap) * a.Cin + ci] = acc[i][j][r];
       }
+#endif  // __HIP_DEVICE_COMPILE__
 }
 
 __global__ void sum_splits(const float4* __restrict__ P, float4* __restrict__ out, int S,
@@ -212,16 +258,6 @@ __global__ void sum_splits(const float4* __restrict__ P, float4* __restrict__ ou
     }
     out[i] = s;
   }
-}
-
-const __hip_bfloat16* zero_page_w(int dev) {
-  static void* pages[64] = {nullptr};
-  IAMD_CHECK(dev >= 0 && dev < 64, "device index");
-  if (!pages[dev]) {
-    IAMD_HIP_CHECK(hipMalloc(&pages[dev], 256));
-    IAMD_HIP_CHECK(hipMemset(pages[dev], 0, 256));
-  }
-  return reinterpret_cast<const __hip_bfloat16*>(pages[dev]);
 }
 
 }  // namespace
@@ -244,14 +280,15 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
   IAMD_CHECK(Ho == (H + 2 * ph - dh * (KH - 1) - 1) / sh + 1 &&
                  Wo == (W + 2 * pw - dw * (KW - 1) - 1) / sw + 1,
              "conv2d_wgrad_mfma: dy spatial size does not match the conv geometry");
-  IAMD_CHECK((int64_t)B * H * W * Cin < (1ll << 31) && (int64_t)B * Ho * Wo * Cout < (1ll << 31),
-             "conv2d_wgrad_mfma: tensor too large for 32-bit pixel indexing");
+  IAMD_CHECK(x.numel() * 2 < (1ll << 30) && (dy.numel() + 64ll * Cout) * 2 < (1ll << 30),
+             "conv2d_wgrad_mfma: tensors too large for 32-bit buffer offsets");
   const int KK = (int)(KH * KW);
   const bool bno128 = Cout % 128 == 0, bc128 = Cin % 128 == 0;
   WgradArgs a;
   a.dy = reinterpret_cast<const __hip_bfloat16*>(dy.data_ptr());
   a.x = reinterpret_cast<const __hip_bfloat16*>(x.data_ptr());
-  a.zero = zero_page_w(x.get_device());
+  a.dybytes = (int)(dy.numel() * 2);
+  a.xbytes = (int)(x.numel() * 2);
   a.Bn = B; a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
   a.KW = (int)KW; a.KK = KK;
   a.sh = (int)sh; a.sw = (int)sw; a.ph = (int)ph; a.pw = (int)pw; a.dh = (int)dh; a.dw = (int)dw;
@@ -290,11 +327,16 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
   }
   const int64_t grid = (int64_t)tiles * S;
   IAMD_CHECK(grid < (1ll << 31), "conv2d_wgrad_mfma: grid too large");
+  const bool rows = Wo % kBP == 0;
   auto launch = [&](auto bv, auto cv) {
     constexpr int BNO = decltype(bv)::value;
     constexpr int BC = decltype(cv)::value;
-    hipLaunchKernelGGL((conv_wgrad_mfma<BNO, BC>), dim3((unsigned)grid), dim3(kThreads), 0,
-                       stream(), a);
+    if (rows)
+      hipLaunchKernelGGL((conv_wgrad_mfma<BNO, BC, true>), dim3((unsigned)grid), dim3(kThreads),
+                         0, stream(), a);
+    else
+      hipLaunchKernelGGL((conv_wgrad_mfma<BNO, BC, false>), dim3((unsigned)grid), dim3(kThreads),
+                         0, stream(), a);
   };
   using I64 = std::integral_constant<int, 64>;
   using I128 = std::integral_constant<int, 128>;

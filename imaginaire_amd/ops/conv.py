@@ -99,6 +99,10 @@ def mfma_eligible(x, w, stride, padding, dilation, groups):
     ho, wo = _out_hw(x.shape[2], x.shape[3], w.shape[2:], stride, padding, dilation)
     if ho <= 0 or wo <= 0:
         return False
+    # 32-bit buffer byte offsets (k10 < 2 GiB operands, k11 < 1 GiB)
+    if x.shape[0] * cp * x.shape[2] * x.shape[3] * 2 >= (1 << 30) or \
+            x.shape[0] * op * ho * wo * 2 >= (1 << 30):
+        return False
     blocks = -(-x.shape[0] * ho * wo // 128) * (op // (128 if op % 128 == 0 else 64))
     return blocks >= _MFMA_MIN_BLOCKS
 
