@@ -37,7 +37,9 @@ bias_act_fwd_kernel(const T* __restrict__ x, T* __restrict__ out, const float* _
 }
 
 // dx = dy * act'(out); per-block channel partial sums of dx (CL layout: rows x C).
-template <typename T, int VEC>
+// ACT = false (identity activation): only the bias gradient is needed, dx IS dy, so the
+// kernel reads dy alone and writes no dx (a third of the bytes).
+template <typename T, int VEC, bool ACT>
 __global__ void __launch_bounds__(kThreads)
 bias_act_bwd_cl(const T* __restrict__ out, const T* __restrict__ dy, T* __restrict__ dx,
                 int64_t rows, int C, int64_t rows_per_block, int tpr, float slope,
@@ -57,14 +59,15 @@ bias_act_bwd_cl(const T* __restrict__ out, const T* __restrict__ dy, T* __restri
     for (int64_t row = r0 + r; row < r1; row += rpb) {
       const int64_t e = row * C + c0;
       float o[VEC], g[VEC];
-      load_vec<T, VEC>(out + e, o);
       load_vec<T, VEC>(dy + e, g);
+      if constexpr (ACT) {
+        load_vec<T, VEC>(out + e, o);
 #pragma unroll
-      for (int k = 0; k < VEC; ++k) {
-        g[k] *= act_grad(o[k], slope);
-        acc[k] += g[k];
+        for (int k = 0; k < VEC; ++k) g[k] *= act_grad(o[k], slope);
       }
-      store_vec<T, VEC>(dx + e, g);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) acc[k] += g[k];
+      if constexpr (ACT) store_vec<T, VEC>(dx + e, g);
     }
   }
 #pragma unroll
@@ -112,15 +115,26 @@ bias_act_bwd_nchw(const T* __restrict__ out, const T* __restrict__ dy, T* __rest
 
 // Column sums of a [P, C] fp32 matrix: block = 64 columns x 8 row-groups
 // (coalesced along C), row-groups combined through LDS.
-constexpr int kColRows = 8;
+constexpr int kColRows = 16;
 __global__ void __launch_bounds__(64 * kColRows)
 col_sum(const float* __restrict__ partial, int P, int C, float* __restrict__ out) {
   __shared__ float sh[kColRows][64];
   const int lane = threadIdx.x, row = threadIdx.y;
   const int c = blockIdx.x * 64 + lane;
   float t = 0.f;
-  if (c < C)
-    for (int p = row; p < P; p += kColRows) t += partial[(int64_t)p * C + c];
+  if (c < C) {
+    // four independent loads in flight per thread: the column walk is latency-bound
+    float t1 = 0.f, t2 = 0.f, t3 = 0.f;
+    int p = row;
+    for (; p + 3 * kColRows < P; p += 4 * kColRows) {
+      t += partial[(int64_t)p * C + c];
+      t1 += partial[(int64_t)(p + kColRows) * C + c];
+      t2 += partial[(int64_t)(p + 2 * kColRows) * C + c];
+      t3 += partial[(int64_t)(p + 3 * kColRows) * C + c];
+    }
+    for (; p < P; p += kColRows) t += partial[(int64_t)p * C + c];
+    t += t1 + t2 + t3;
+  }
   sh[row][lane] = t;
   __syncthreads();
   if (row == 0 && c < C) {
@@ -188,7 +202,8 @@ std::vector<at::Tensor> bias_act_bwd(const at::Tensor& out, const at::Tensor& dy
   if (dy.scalar_type() != out.scalar_type()) dy = dy.to(out.scalar_type());
   const int N = (int)out.size(0), C = (int)out.size(1);
   const int64_t HW = out.numel() / std::max<int64_t>(1, (int64_t)N * C);
-  auto dx = at::empty_like(out);
+  // identity activation on the channels-fast path: the kernel writes no dx, dx is dy itself
+  auto dx = ((cl || lin) && slope == 1.0) ? dy : at::empty_like(out);
   auto fopt = out.options().dtype(at::kFloat);
   at::Tensor partial;
   int P;
@@ -203,14 +218,20 @@ std::vector<at::Tensor> bias_act_bwd(const at::Tensor& out, const at::Tensor& dy
       const int nzc = ceil_div(C, (int64_t)tpr * vec);
       const int64_t rows = (int64_t)N * HW;
       const int rpb = kThreads / tpr;
-      int64_t rows_per_block = std::max<int64_t>(rpb * 4, (rows + 1023) / 1024);
+      int64_t rows_per_block = std::max<int64_t>(rpb * 4, (rows + 511) / 512);
       P = (int)((rows + rows_per_block - 1) / rows_per_block);
       partial = at::empty({P, C}, fopt);
+      const bool act = slope != 1.0;
       auto launch = [&](auto vt) {
         constexpr int V = decltype(vt)::value;
-        hipLaunchKernelGGL((bias_act_bwd_cl<scalar_t, V>), dim3(P, nzc), dim3(kThreads), 0, stream(),
-                           op, gp, dp, rows, C, rows_per_block, tpr, (float)slope,
-                           partial.data_ptr<float>());
+        if (act)
+          hipLaunchKernelGGL((bias_act_bwd_cl<scalar_t, V, true>), dim3(P, nzc), dim3(kThreads), 0,
+                             stream(), op, gp, dp, rows, C, rows_per_block, tpr, (float)slope,
+                             partial.data_ptr<float>());
+        else
+          hipLaunchKernelGGL((bias_act_bwd_cl<scalar_t, V, false>), dim3(P, nzc), dim3(kThreads), 0,
+                             stream(), op, gp, dp, rows, C, rows_per_block, tpr, (float)slope,
+                             partial.data_ptr<float>());
       };
       switch (vec) {
         case 8: launch(std::integral_constant<int, 8>()); break;

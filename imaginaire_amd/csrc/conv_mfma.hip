@@ -12,8 +12,9 @@
 // so a 64-deep k-step is one filter tap and 64 consecutive input channels (Cin % 64 == 0;
 // the Python wrapper zero-pads odd channel counts such as 185-channel label maps).
 //
-// Block tile 128 (pixels) x BN (channels) x 64 (k), 256 threads = 4 wave64s in a 2x2 grid,
-// each wave owns a 64 x BN/2 sub-tile of v_mfma_f32_16x16x32_bf16 accumulators.
+// Block tile BM (128 / 256 pixels) x BN (64 / 128 channels) x 64 (k), BM/32 wave64s in a
+// (BM/64) x 2 grid, each wave owning a 64 x BN/2 sub-tile of v_mfma_f32_16x16x32_bf16
+// accumulators.
 // Staging: global -> LDS with buffer_load_dwordx4 ... lds (no VGPR round trip), two LDS buffers,
 // one barrier per k-step; the load of step k+1 is in flight while step k runs on the MFMAs.
 // Padding pixels (outside the image) and the pixel tail get an out-of-range buffer offset and
@@ -25,6 +26,8 @@
 // that share one pixel tile run on the same XCD (shared L2 for the activation halo).
 #include "common.h"
 
+#include <cstdlib>
+
 namespace iamd {
 namespace {
 
@@ -32,9 +35,7 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-constexpr int kBM = 128;
 constexpr int kBK = 64;
-constexpr int kThreads = 256;
 constexpr int kRowBytes = kBK * 2;  // 128 B per staged row
 constexpr int kEpiStride = 272;     // epilogue LDS row stride in bytes (BN<=128 bf16 + 16 pad)
 
@@ -53,27 +54,34 @@ struct ConvArgs {
   int H, W, Cin, Ho, Wo, Cout;
   int KH, KW, sh, sw, ph, pw, dh, dw;
   int M, nk, cpt, nNt;
+  int kps;          // k-steps per split (split-K: blockIdx.y = split)
+  float* part;      // split-K fp32 partial slabs [S][M][Cout] (nullptr: direct epilogue)
   float slope;
 };
 
-template <int BN, bool HAS_BIAS>
-__global__ __launch_bounds__(kThreads, 2) void conv_fwd_mfma(ConvArgs a) {
+// BM = 128 (4 waves, 2 blocks/CU) or 256 (8 waves, 1 block/CU: the B tile is shared by twice
+// the pixels, 25% fewer L2->LDS bytes per MFMA); waves form a (BM/64) x 2 grid.
+template <int BM, int BN, bool HAS_BIAS>
+__global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_fwd_mfma(ConvArgs a) {
   // The buffer-resource builtins have no host form; the host pass only needs the launch stub.
 #if defined(__HIP_DEVICE_COMPILE__)
+  constexpr int kThreads = BM * 2;
   constexpr int NI = BN / 32;                 // 16-wide n-fragments per wave
-  constexpr int kAbytes = kBM * kRowBytes;    // 16 KB
+  constexpr int kAbytes = BM * kRowBytes;     // 16 / 32 KB
   constexpr int kBbytes = BN * kRowBytes;     // 8 / 16 KB
   constexpr int kStage = kAbytes + kBbytes;
-  constexpr int kBLoads = BN / 32;            // glds per thread for the B tile
+  constexpr int RS = kThreads / 8;            // staged rows per DMA round
+  constexpr int kLoadBytes = kThreads * 16;   // LDS bytes per DMA round
+  constexpr int kBLoads = BN / RS;            // DMA rounds for the B tile
   __shared__ __attribute__((aligned(16))) char smem[2 * kStage];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int mt = bid / a.nNt, nt = bid - mt * a.nNt;
-  const int m0 = mt * kBM, n0 = nt * BN;
+  const int m0 = mt * BM, n0 = nt * BN;
 
-  // ---- per-thread DMA sources: rows lrow + 32 i, chunk csw (swizzled) -------------------
+  // ---- per-thread DMA sources: rows lrow + RS i, chunk csw (swizzled) -------------------
   // Buffer-resource loads straight into LDS: the per-lane 32-bit byte offset selects the
   // pixel row, the wave-uniform parts (tap, channel block, k-step) ride in SGPRs, and an
   // out-of-range offset (padding pixels, M tail) returns zeros from the buffer unit itself.
@@ -88,7 +96,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_mfma(ConvArgs a) {
   uint32_t a_rmask[4], a_cmask[4];  // bit ky / kx set when that filter row / column is inside
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int m = m0 + lrow + 32 * i;
+    const int m = m0 + lrow + RS * i;
     a_off[i] = 0;
     a_rmask[i] = 0;
     a_cmask[i] = 0;
@@ -106,7 +114,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_mfma(ConvArgs a) {
   const int wrow_bytes = a.nk * kBK * 2;  // = KH*KW*Cin*2
   int b_off[kBLoads];
 #pragma unroll
-  for (int i = 0; i < kBLoads; ++i) b_off[i] = (n0 + lrow + 32 * i) * wrow_bytes + csw * 16;
+  for (int i = 0; i < kBLoads; ++i) b_off[i] = (n0 + lrow + RS * i) * wrow_bytes + csw * 16;
 
   auto issue = [&](int ks, int buf) {
     const int tap = ks / a.cpt;
@@ -119,13 +127,13 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_mfma(ConvArgs a) {
     for (int i = 0; i < 4; ++i) {
       const bool ok = (a_rmask[i] >> ky) & (a_cmask[i] >> kx) & 1u;
       const int voff = ok ? a_off[i] + tapoff : kOobOffset;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(As + i * 4096 + wid * 1024), 16,
-                                               voff, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(As + i * kLoadBytes + wid * 1024),
+                                               16, voff, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < kBLoads; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)(Bs + i * 4096 + wid * 1024), 16,
-                                               b_off[i], ks * kBK * 2, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)(Bs + i * kLoadBytes + wid * 1024),
+                                               16, b_off[i], ks * kBK * 2, 0, 0);
   };
 
   f32x4 acc[4][NI];
@@ -136,12 +144,14 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_mfma(ConvArgs a) {
 
   // fragment read offsets (row & 7 == lane & 7 for every fragment row of this lane)
   const int frow = lane & 15, fsw = lane & 7, fk = lane >> 4;
-  issue(0, 0);
-  for (int ks = 0; ks < a.nk; ++ks) {
+  const int ks0 = blockIdx.y * a.kps;
+  const int ks1 = min(a.nk, ks0 + a.kps);
+  issue(ks0, 0);
+  for (int ks = ks0; ks < ks1; ++ks) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (ks + 1 < a.nk) issue(ks + 1, (ks + 1) & 1);
-    const char* As = smem + (ks & 1) * kStage;
+    if (ks + 1 < ks1) issue(ks + 1, (ks + 1 - ks0) & 1);
+    const char* As = smem + ((ks - ks0) & 1) * kStage;
     const char* Bs = As + kAbytes;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -159,6 +169,20 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_mfma(ConvArgs a) {
         for (int j = 0; j < NI; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
+  }
+
+  if (a.part) {  // split-K: raw fp32 partials, bias/act/bf16 in conv_splitk_reduce
+    float* o = a.part + (size_t)blockIdx.y * a.M * a.Cout;
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+          if (m < a.M) o[(size_t)m * a.Cout + n0 + wn * (BN / 2) + j * 16 + (lane & 15)] = acc[i][j][r];
+        }
+    return;
   }
 
   // ---- epilogue: bias + activation -> bf16 tile in LDS -> 16-byte row stores --------------
@@ -184,7 +208,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_mfma(ConvArgs a) {
   constexpr int kRowsPerPass = kThreads / kChunks;
   const int ch = tid % kChunks, rr = tid / kChunks;
 #pragma unroll
-  for (int p = 0; p < kBM / kRowsPerPass; ++p) {
+  for (int p = 0; p < BM / kRowsPerPass; ++p) {
     const int rl = p * kRowsPerPass + rr;
     const int m = m0 + rl;
     if (m < a.M) {
@@ -193,6 +217,34 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_mfma(ConvArgs a) {
     }
   }
 #endif  // __HIP_DEVICE_COMPILE__
+}
+
+// y = act(sum_s part[s] + bias) in bf16, 8 channels per thread.
+__global__ void __launch_bounds__(256)
+conv_splitk_reduce(const float* __restrict__ part, const float* __restrict__ bias,
+                   __hip_bfloat16* __restrict__ y, int S, int64_t MC, int C, float slope) {
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < MC / 8;
+       v += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = v * 8;
+    float acc[8];
+    const float4* p = reinterpret_cast<const float4*>(part + e);
+    float4 lo = p[0], hi = p[1];
+    acc[0] = lo.x; acc[1] = lo.y; acc[2] = lo.z; acc[3] = lo.w;
+    acc[4] = hi.x; acc[5] = hi.y; acc[6] = hi.z; acc[7] = hi.w;
+    for (int s = 1; s < S; ++s) {
+      const float4* q = reinterpret_cast<const float4*>(part + (int64_t)s * MC + e);
+      lo = q[0]; hi = q[1];
+      acc[0] += lo.x; acc[1] += lo.y; acc[2] += lo.z; acc[3] += lo.w;
+      acc[4] += hi.x; acc[5] += hi.y; acc[6] += hi.z; acc[7] += hi.w;
+    }
+    const int c = (int)(e % C);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float t = acc[k] + (bias ? bias[c + k] : 0.f);
+      acc[k] = t > 0.f ? t : t * slope;
+    }
+    store_vec<__hip_bfloat16, 8>(y + e, acc);
+  }
 }
 
 }  // namespace
@@ -241,22 +293,54 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
   a.cpt = Cin / kBK;
   a.nk = KH * KW * a.cpt;
   a.slope = (float)slope;
-  const int nMt = ceil_div(a.M, kBM);
   const bool bn128 = Cout % 128 == 0;
   a.nNt = Cout / (bn128 ? 128 : 64);
-  const int64_t grid = (int64_t)nMt * a.nNt;
-  IAMD_CHECK(grid < (1ll << 31), "conv2d_mfma: grid too large");
-  auto launch = [&](auto bnv, auto hbv) {
+  // BM = 128 by default (4 waves, 2 blocks/CU); BM = 256 (8 waves) measured no faster on the
+  // SPADE shapes (profiles/conv_mfma_probe_mi355x.txt) and stays selectable for probing
+  int bm = 128;
+  if (const char* e = std::getenv("IMAGINAIRE_AMD_CONV_BM")) {
+    const int v = std::atoi(e);
+    if (v == 128 || v == 256) bm = v;
+  }
+  const int64_t tiles = (int64_t)ceil_div(a.M, bm) * a.nNt;
+  IAMD_CHECK(tiles < (1ll << 31), "conv2d_mfma: grid too large");
+  // split-K over (tap, channel-block) k-steps when the tile grid cannot fill 256 CUs twice
+  // (wide-K / narrow-N data gradients of the SPADE gamma/beta convs at 16x32 .. 64x128)
+  int S = 1;
+  if (tiles < 512 && a.nk >= 16) S = (int)std::min<int64_t>((512 + tiles - 1) / tiles, a.nk / 8);
+  if (const char* e = std::getenv("IMAGINAIRE_AMD_CONV_SPLITK")) S = std::max(1, std::atoi(e));
+  S = std::max(1, std::min(S, a.nk));
+  a.kps = ceil_div(a.nk, S);
+  S = ceil_div(a.nk, a.kps);
+  at::Tensor part;
+  a.part = nullptr;
+  if (S > 1) {
+    part = at::empty({(int64_t)S * a.M * Cout}, x.options().dtype(at::kFloat));
+    a.part = part.data_ptr<float>();
+  }
+  const dim3 grid((unsigned)tiles, (unsigned)S);
+  auto launch = [&](auto bmv, auto bnv, auto hbv) {
+    constexpr int BM = decltype(bmv)::value;
     constexpr int BN = decltype(bnv)::value;
     constexpr bool HB = decltype(hbv)::value;
-    hipLaunchKernelGGL((conv_fwd_mfma<BN, HB>), dim3((unsigned)grid), dim3(kThreads), 0, stream(), a);
+    hipLaunchKernelGGL((conv_fwd_mfma<BM, BN, HB>), grid, dim3(BM * 2), 0, stream(), a);
   };
-  if (bn128) {
-    if (a.bias) launch(std::integral_constant<int, 128>(), std::true_type());
-    else launch(std::integral_constant<int, 128>(), std::false_type());
-  } else {
-    if (a.bias) launch(std::integral_constant<int, 64>(), std::true_type());
-    else launch(std::integral_constant<int, 64>(), std::false_type());
+  auto by_bn = [&](auto bmv, auto hbv) {
+    if (bn128) launch(bmv, std::integral_constant<int, 128>(), hbv);
+    else launch(bmv, std::integral_constant<int, 64>(), hbv);
+  };
+  auto by_bias = [&](auto bmv) {
+    if (a.bias) by_bn(bmv, std::true_type());
+    else by_bn(bmv, std::false_type());
+  };
+  if (bm == 256) by_bias(std::integral_constant<int, 256>());
+  else by_bias(std::integral_constant<int, 128>());
+  if (S > 1) {
+    IAMD_LAUNCH_CHECK();
+    const int64_t MC = (int64_t)a.M * Cout;
+    const int blocks = (int)std::min<int64_t>((MC / 8 + 255) / 256, 8192);
+    hipLaunchKernelGGL(conv_splitk_reduce, dim3(blocks), dim3(256), 0, stream(), a.part, a.bias,
+                       a.y, S, MC, Cout, a.slope);
   }
   IAMD_LAUNCH_CHECK();
   return y;

@@ -7,6 +7,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from imaginaire_amd.layers import Conv2dBlock
+from imaginaire_amd.ops.resize import Upsample
 
 
 class FPSEDiscriminator(nn.Module):
@@ -36,7 +37,7 @@ class FPSEDiscriminator(nn.Module):
         self.lat3 = latent(4 * num_filters, 4 * num_filters)
         self.lat4 = latent(8 * num_filters, 4 * num_filters)
         self.lat5 = latent(8 * num_filters, 4 * num_filters)
-        self.upsample2x = nn.Upsample(scale_factor=2, mode='bilinear', align_corners=False)
+        self.upsample2x = Upsample(scale_factor=2, mode='bilinear', align_corners=False)
         self.final2 = stride1(4 * num_filters, 2 * num_filters)
         self.final3 = stride1(4 * num_filters, 2 * num_filters)
         self.final4 = stride1(4 * num_filters, 2 * num_filters)

@@ -15,6 +15,7 @@ from imaginaire_amd.layers import Conv2dBlock
 from imaginaire_amd.utils.data import (get_paired_input_image_channel_number,
                                        get_paired_input_label_channel_number)
 from imaginaire_amd.utils.distributed import master_only_print as print
+from imaginaire_amd.ops.resize import interpolate
 
 
 class Discriminator(nn.Module):
@@ -54,8 +55,8 @@ class Discriminator(nn.Module):
 
 
 def _down2(x):
-    return F.interpolate(x, scale_factor=0.5, mode='bilinear', align_corners=True,
-                         recompute_scale_factor=True)
+    return interpolate(x, scale_factor=0.5, mode='bilinear', align_corners=True,
+                       recompute_scale_factor=True)
 
 
 class MultiResPatchDiscriminator(nn.Module):
@@ -105,8 +106,8 @@ class WeightSharedMultiResPatchDiscriminator(nn.Module):
             output, features = self.discriminator(input_downsampled)
             output_list.append(output)
             features_list.append(features)
-            input_downsampled = F.interpolate(input_downsampled, scale_factor=0.5,
-                                              mode='bilinear', align_corners=True)
+            input_downsampled = interpolate(input_downsampled, scale_factor=0.5,
+                                            mode='bilinear', align_corners=True)
         return output_list, features_list, input_list
 
 

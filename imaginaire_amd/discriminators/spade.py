@@ -9,6 +9,7 @@ import torch
 import torch.nn as nn
 
 from imaginaire_amd.discriminators.fpse import FPSEDiscriminator
+from imaginaire_amd.ops.resize import interpolate
 from imaginaire_amd.discriminators.multires_patch import NLayerPatchDiscriminator
 from imaginaire_amd.registry import canonical_module_name
 from imaginaire_amd.utils.data import (get_paired_input_image_channel_number,
@@ -54,7 +55,7 @@ class Discriminator(nn.Module):
             output, features = net_discriminator(input_downsampled)
             output_list.append(output)
             features_list.append(features)
-            input_downsampled = nn.functional.interpolate(
+            input_downsampled = interpolate(
                 input_downsampled, scale_factor=0.5, mode='bilinear', align_corners=True)
         return output_list, features_list
 

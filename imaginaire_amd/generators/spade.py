@@ -24,7 +24,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
-from torch.nn import Upsample as NearestUpsample
+from imaginaire_amd.ops.resize import Upsample as NearestUpsample
 
 from imaginaire_amd.layers import Conv2dBlock, LinearBlock, Res2dBlock
 from imaginaire_amd.layers.activation_norm import LabelMapCache

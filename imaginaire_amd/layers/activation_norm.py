@@ -24,6 +24,7 @@ from torch import nn
 from torch.nn import functional as F
 
 from imaginaire_amd.ops.norm import fused_norm_act
+from imaginaire_amd.ops.resize import interpolate
 from .conv import LinearBlock, Conv2dBlock, HyperConv2d, PartialConv2dBlock
 from .misc import PartialSequential
 
@@ -51,11 +52,11 @@ class LabelMapCache(object):
         if tuple(t.shape[2:]) == tuple(size) and mode == 'nearest':
             return t
         if cache is None:
-            return F.interpolate(t, size=size, mode=mode)
+            return interpolate(t, size=size, mode=mode)
         key = (id(t), t.data_ptr(), tuple(size), mode)
         out = cache.store.get(key)
         if out is None:
-            out = F.interpolate(t, size=size, mode=mode)
+            out = interpolate(t, size=size, mode=mode)
             cache.store[key] = out
         return out
 

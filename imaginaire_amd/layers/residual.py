@@ -8,7 +8,7 @@ The blocks' norm/activation pairs run as fused HIP kernels via the conv blocks.
 import functools
 
 from torch import nn
-from torch.nn import Upsample as NearestUpsample
+from imaginaire_amd.ops.resize import Upsample as NearestUpsample
 from torch.utils.checkpoint import checkpoint
 
 from .conv import (Conv1dBlock, Conv2dBlock, Conv3dBlock, HyperConv2dBlock, LinearBlock,

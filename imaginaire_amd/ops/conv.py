@@ -28,9 +28,10 @@ import torch.nn.functional as F
 from imaginaire_amd.ops import _ext
 
 _CL = torch.channels_last
-# fewer 128-pixel x BN-channel tiles than this and MIOpen's split-K kernels win
-_MFMA_MIN_BLOCKS = int(os.environ.get('IMAGINAIRE_AMD_MFMA_MIN_BLOCKS', '96'))
-_MFMA_MIN_DGRAD_BLOCKS = int(os.environ.get('IMAGINAIRE_AMD_MFMA_MIN_DGRAD_BLOCKS', '512'))
+# tiny grids (fewer 128-pixel x BN-channel tiles than this) stay on MIOpen; k10 splits K
+# itself when its tile grid cannot fill the chip
+_MFMA_MIN_BLOCKS = int(os.environ.get('IMAGINAIRE_AMD_MFMA_MIN_BLOCKS', '16'))
+_MFMA_MIN_DGRAD_BLOCKS = int(os.environ.get('IMAGINAIRE_AMD_MFMA_MIN_DGRAD_BLOCKS', '16'))
 # weight gradient: 'auto' = per-shape faster of k11 / MIOpen wrw, '1' = k11, '0' = MIOpen
 _MFMA_WGRAD = os.environ.get('IMAGINAIRE_AMD_MFMA_WGRAD', 'auto')
 
@@ -154,8 +155,8 @@ class _MfmaConv2d(torch.autograd.Function):
             cp = wb.shape[1]
             dblocks = -(-dy.shape[0] * xb.shape[2] * xb.shape[3] // 128) * \
                 (cp // (128 if cp % 128 == 0 else 64))
-            # the dgrad GEMM has N = Cin: with few tiles (wide-K, narrow-N SPADE γ/β convs at
-            # 16x32) MIOpen's split-K kernels win (profiles/conv_mfma_probe_mi355x.txt)
+            # the dgrad GEMM has N = Cin (few tiles, K = taps x Cout for the SPADE γ/β convs):
+            # k10 splits K over the grid's y dimension for those
             if stride == (1, 1) and pt[0] >= 0 and pt[1] >= 0 and \
                     dblocks >= _MFMA_MIN_DGRAD_BLOCKS:
                 dx = _ext.ext().conv2d_mfma(dy, _flip_t(wb), None, 1, 1, pt[0], pt[1],

@@ -115,3 +115,25 @@ for name, B, cin, cout, k, H, W, s, xg in shapes:
     tm, tk = bench(miopen), bench(k11)
     print('%-32s wgrad miopen %7.3f ms %6.0f TF/s | k11 %7.3f ms %6.0f TF/s (relerr %.1e)' % (
         name, tm, flops / tm / 1e9, tk, flops / tk / 1e9, err), flush=True)
+
+print('--- k10 forward tile: BM=128 (4 waves, 2 blocks/CU) vs BM=256 (8 waves) ---', flush=True)
+for name, B, cin, cout, k, H, W, s, xg in shapes:
+    pad = (k - 1) // 2 if s == 1 else 1
+    cp = C._round_up(cin, 64)
+    x = torch.randn(B, cp, H, W, device=dev, dtype=torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(cout, cp, k, k, device=dev, dtype=torch.bfloat16) * 0.02).contiguous(
+        memory_format=CL)
+    ho = (H + 2 * pad - k) // s + 1
+    wo = (W + 2 * pad - k) // s + 1
+    flops = 2.0 * B * ho * wo * cout * cp * k * k
+    res = []
+    for bm in ('128', '256'):
+        os.environ['IMAGINAIRE_AMD_CONV_BM'] = bm
+        y = ext.conv2d_mfma(x, w, None, s, s, pad, pad, 1, 1, 1.0)
+        t = bench(lambda: ext.conv2d_mfma(x, w, None, s, s, pad, pad, 1, 1, 1.0))
+        res.append((t, y))
+    os.environ.pop('IMAGINAIRE_AMD_CONV_BM')
+    same = (res[0][1].float() - res[1][1].float()).abs().max().item()
+    print('%-32s BM128 %7.3f ms %6.0f TF/s | BM256 %7.3f ms %6.0f TF/s | max diff %.1e' % (
+        name, res[0][0], flops / res[0][0] / 1e9, res[1][0], flops / res[1][0] / 1e9, same),
+        flush=True)

@@ -357,3 +357,24 @@ def test_conv2d_mfma_fwd_bwd(case, slope, bias):
             (((b.grad, br.grad, 'db'),) if bias else ()):
         e = (got.float() - ref).abs().max().item()
         assert e <= 2e-2 * max(1.0, ref.abs().max().item()), (name, e, ref.abs().max().item())
+
+
+@pytest.mark.parametrize('splitk', ['1', '3'])
+def test_conv2d_mfma_splitk_matches(splitk):
+    """k10 split-K (fp32 partial slabs + bias/act reduce) == single-pass k10 == fp32 conv."""
+    import os
+    from imaginaire_amd.ops import _ext
+    torch.manual_seed(3)
+    x = torch.randn(2, 128, 12, 20, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    w = (torch.randn(192, 128, 5, 5, device='cuda') * 0.02).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    b = torch.randn(192, device='cuda')
+    os.environ['IMAGINAIRE_AMD_CONV_SPLITK'] = splitk
+    try:
+        y = _ext.ext().conv2d_mfma(x, w, b, 1, 1, 2, 2, 1, 1, 0.2)
+    finally:
+        os.environ.pop('IMAGINAIRE_AMD_CONV_SPLITK')
+    ref = F.leaky_relu(F.conv2d(x.float(), w.float(), b, 1, 2), 0.2)
+    err = (y.float() - ref).abs().max().item()
+    assert err <= 1e-2 * max(1.0, ref.abs().max().item()), err
