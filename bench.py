@@ -148,7 +148,7 @@ def main():
             rows.sort(key=lambda e: -e.self_device_time_total)
             tot = sum(e.self_device_time_total for e in rows)
             print('op self GPU time in one step: %.2f ms' % (tot / 1e3))
-            for e in rows[:80]:
+            for e in rows[:250]:
                 print('%9.3f ms %4d  %-34s %s' % (e.self_device_time_total / 1e3, e.count,
                                                   e.key[:34], str(e.input_shapes)[:140]))
         else:

@@ -61,7 +61,10 @@ struct ConvArgs {
 
 // BM = 128 (4 waves, 2 blocks/CU) or 256 (8 waves, 1 block/CU: the B tile is shared by twice
 // the pixels, 25% fewer L2->LDS bytes per MFMA); waves form a (BM/64) x 2 grid.
-template <int BM, int BN, bool HAS_BIAS>
+// VAR (main-loop schedule experiment, IMAGINAIRE_AMD_CONV_VAR): 0 = per-32-k fragment reads
+// then MFMAs; 1 = same with s_setprio(1) around the MFMA cluster; 2 = all 64-k fragments read
+// up front, then 32 back-to-back MFMAs under s_setprio(1).
+template <int BM, int BN, bool HAS_BIAS, int VAR>
 __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_fwd_mfma(ConvArgs a) {
   // The buffer-resource builtins have no host form; the host pass only needs the launch stub.
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -153,21 +156,46 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_fwd_mfma(ConvA
     if (ks + 1 < ks1) issue(ks + 1, (ks + 1 - ks0) & 1);
     const char* As = smem + ((ks - ks0) & 1) * kStage;
     const char* Bs = As + kAbytes;
+    if constexpr (VAR == 2) {
+      bf16x8 af[2][4], bfr[2][NI];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int coff = ((kk * 4 + fk) ^ fsw) << 4;
-      bf16x8 af[4], bfr[NI];
+      for (int kk = 0; kk < 2; ++kk) {
+        const int coff = ((kk * 4 + fk) ^ fsw) << 4;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + i * 16 + frow) * kRowBytes + coff);
-#pragma unroll
-      for (int j = 0; j < NI; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * (BN / 2) + j * 16 + frow) * kRowBytes + coff);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
+          af[kk][i] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + i * 16 + frow) * kRowBytes + coff);
 #pragma unroll
         for (int j = 0; j < NI; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          bfr[kk][j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * (BN / 2) + j * 16 + frow) * kRowBytes + coff);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int coff = ((kk * 4 + fk) ^ fsw) << 4;
+        bf16x8 af[4], bfr[NI];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          af[i] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + i * 16 + frow) * kRowBytes + coff);
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * (BN / 2) + j * 16 + frow) * kRowBytes + coff);
+        if constexpr (VAR == 1) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        if constexpr (VAR == 1) __builtin_amdgcn_s_setprio(0);
+      }
     }
   }
 
@@ -319,11 +347,24 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
     a.part = part.data_ptr<float>();
   }
   const dim3 grid((unsigned)tiles, (unsigned)S);
+  // main-loop schedule: VAR 2 (fragments up front + setprio) measured +1-5% over 0 / 1
+  // (scripts/probe/conv_var_probe.py, profiles/conv_var_probe_mi355x.txt)
+  int var = 2;
+  if (const char* e = std::getenv("IMAGINAIRE_AMD_CONV_VAR")) var = std::atoi(e);
   auto launch = [&](auto bmv, auto bnv, auto hbv) {
     constexpr int BM = decltype(bmv)::value;
     constexpr int BN = decltype(bnv)::value;
     constexpr bool HB = decltype(hbv)::value;
-    hipLaunchKernelGGL((conv_fwd_mfma<BM, BN, HB>), grid, dim3(BM * 2), 0, stream(), a);
+    if constexpr (BM == 128) {
+      if (var == 1)
+        hipLaunchKernelGGL((conv_fwd_mfma<BM, BN, HB, 1>), grid, dim3(BM * 2), 0, stream(), a);
+      else if (var == 2)
+        hipLaunchKernelGGL((conv_fwd_mfma<BM, BN, HB, 2>), grid, dim3(BM * 2), 0, stream(), a);
+      else
+        hipLaunchKernelGGL((conv_fwd_mfma<BM, BN, HB, 0>), grid, dim3(BM * 2), 0, stream(), a);
+    } else {
+      hipLaunchKernelGGL((conv_fwd_mfma<BM, BN, HB, 0>), grid, dim3(BM * 2), 0, stream(), a);
+    }
   };
   auto by_bn = [&](auto bmv, auto hbv) {
     if (bn128) launch(bmv, std::integral_constant<int, 128>(), hbv);

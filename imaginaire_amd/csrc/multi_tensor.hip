@@ -179,16 +179,21 @@ sn_sigma_kernel(const TensorEntry* __restrict__ ents, const int* __restrict__ bl
   const TensorEntry e = ents[t];
   const float* __restrict__ W = reinterpret_cast<const float*>(e.p[0]);
   const float* __restrict__ u = reinterpret_cast<const float*>(e.p[1]);
-  const float* __restrict__ v = reinterpret_cast<const float*>(e.p[2]);
+  // p[3]: v permuted to the weight's MEMORY column order by sn_vperm (coalesced reads; the
+  // logical-order v of a channels-last conv weight would be a stride-KH*KW gather)
+  const float* __restrict__ v = reinterpret_cast<const float*>(e.p[3]);
   const int64_t ncol = e.cols;
   const int64_t start = (int64_t)chunk * kChunk;
   const int64_t end = min(e.numel, start + (int64_t)kChunk);
   float acc = 0.f;
-  for (int64_t i = start + threadIdx.x; i < end; i += kThreads) {
-    const int64_t r = i / ncol;
-    int64_t c = i - r * ncol;
-    if (e.cl_cin) c = (c % e.cl_cin) * e.cl_khw + c / e.cl_cin;
+  // (row, column) walked incrementally: no 64-bit division per element
+  const int64_t i0 = start + threadIdx.x;
+  int64_t r = i0 / ncol;
+  int64_t c = i0 - r * ncol;
+  for (int64_t i = i0; i < end; i += kThreads) {
     acc = fmaf(u[r] * W[i], v[c], acc);
+    c += kThreads;
+    while (c >= ncol) { c -= ncol; ++r; }
   }
   acc = wave_sum(acc);
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
@@ -197,6 +202,23 @@ sn_sigma_kernel(const TensorEntry* __restrict__ ents, const int* __restrict__ bl
     float s = 0.f;
     for (int k = 0; k < kThreads / 64; ++k) s += sh[k];
     atomicAdd(sigma + t, s);
+  }
+}
+
+// one block per tensor: vm[c] = v[logical(c)] for every memory column c
+__global__ void __launch_bounds__(kThreads)
+sn_vperm(const TensorEntry* __restrict__ ents) {
+  const TensorEntry e = ents[blockIdx.x];
+  const float* __restrict__ v = reinterpret_cast<const float*>(e.p[2]);
+  float* __restrict__ vm = reinterpret_cast<float*>(e.p[3]);
+  const uint32_t cin = (uint32_t)e.cl_cin;
+  for (int64_t c = threadIdx.x; c < e.cols; c += kThreads) {
+    int64_t lc = c;
+    if (cin) {
+      const uint32_t q = (uint32_t)c / cin;
+      lc = (int64_t)((uint32_t)c - q * cin) * e.cl_khw + q;
+    }
+    vm[c] = v[lc];
   }
 }
 
@@ -310,8 +332,28 @@ at::Tensor mt_sn_sigma(const std::vector<at::Tensor>& weights, const std::vector
   check_same_dtype(weights, at::kFloat, "mt_sn_sigma W");
   check_same_dtype(us, at::kFloat, "mt_sn_sigma u");
   check_same_dtype(vs, at::kFloat, "mt_sn_sigma v");
-  Table& tb = get_table({weights, us, vs}, weights[0].device());
+  // persistent per-device workspace for the memory-order v copies: stable pointers keep the
+  // cached device table valid across calls
+  static std::mutex ws_mu;
+  static std::unordered_map<int, at::Tensor> ws_map;
+  int64_t total = 0;
+  for (auto& w : weights) total += w.numel() / std::max<int64_t>(1, w.size(0));
+  std::vector<at::Tensor> vms;
+  {
+    std::lock_guard<std::mutex> lk(ws_mu);
+    at::Tensor& ws = ws_map[weights[0].get_device()];
+    if (!ws.defined() || ws.numel() < total) ws = at::empty({total}, weights[0].options());
+    int64_t off = 0;
+    for (auto& w : weights) {
+      const int64_t cols = w.numel() / std::max<int64_t>(1, w.size(0));
+      vms.push_back(ws.narrow(0, off, cols));
+      off += cols;
+    }
+  }
+  Table& tb = get_table({weights, us, vs, vms}, weights[0].device());
   auto sigma = at::zeros({(int64_t)weights.size()}, weights[0].options());
+  hipLaunchKernelGGL(sn_vperm, dim3((unsigned)weights.size()), dim3(kThreads), 0, stream(),
+                     reinterpret_cast<const TensorEntry*>(tb.entries.data_ptr()));
   hipLaunchKernelGGL(sn_sigma_kernel, dim3(tb.nblocks), dim3(kThreads), 0, stream(),
                      reinterpret_cast<const TensorEntry*>(tb.entries.data_ptr()),
                      tb.blocks.data_ptr<int>(), sigma.data_ptr<float>());

@@ -39,8 +39,14 @@ struct SnEntry {
   int64_t cl_cin, cl_khw;  // channels-last mapping (0 = none)
 };
 
+// memory column -> logical column (32-bit: every SN weight row is < 2^31 elements).
+// Only the u/v state vectors are kept in logical (reference checkpoint) order; the per-call
+// workspaces t/s stay in memory order so the hot GEMV loops never divide.
 __device__ __forceinline__ int64_t logical_col(const SnEntry& e, int64_t c) {
-  return e.cl_cin ? (c % e.cl_cin) * e.cl_khw + c / e.cl_cin : c;
+  if (!e.cl_cin) return c;
+  const uint32_t cc = (uint32_t)c, cin = (uint32_t)e.cl_cin;
+  const uint32_t q = cc / cin;
+  return (int64_t)(cc - q * cin) * e.cl_khw + q;
 }
 
 __device__ float block_sum(float v, float* sh) {
@@ -69,7 +75,7 @@ __global__ void __launch_bounds__(kT) sn_colsum(const SnEntry* __restrict__ ents
   const int64_t r1 = min(e.h, r0 + kRowsPerSplit);
   float acc = 0.f;
   for (int64_t r = r0; r < r1; ++r) acc = fmaf(e.W[r * e.w + c], e.u[r], acc);
-  atomicAdd(e.t + logical_col(e, c), acc);
+  atomicAdd(e.t + c, acc);  // memory order
 }
 
 // one block per layer: sums of squares of t -> scal[l*4 + 0]
@@ -93,11 +99,24 @@ __global__ void __launch_bounds__(64 * kRowsPerBlock) sn_rows(const SnEntry* __r
   const int64_t r = (int64_t)bm[1] + (threadIdx.x >> 6);
   if (r >= e.h) return;
   const int lane = threadIdx.x & 63;
-  const float* x = update ? e.t : e.v;
   const float k = update ? 1.f / fmaxf(sqrtf(scal[4 * bm[0]]), eps) : 1.f;
   const float* row = e.W + r * e.w;
   float acc = 0.f;
-  for (int64_t c = lane; c < e.w; c += 64) acc = fmaf(row[c], x[logical_col(e, c)], acc);
+  if (update) {  // t is in memory order: straight (vectorised when rows are 16-B aligned) dot
+    const float* x = e.t;
+    if ((e.w & 3) == 0) {
+      const float4* r4 = reinterpret_cast<const float4*>(row);
+      const float4* x4 = reinterpret_cast<const float4*>(x);
+      for (int64_t c = lane; c < e.w / 4; c += 64) {
+        const float4 a = r4[c], b = x4[c];
+        acc = fmaf(a.x, b.x, fmaf(a.y, b.y, fmaf(a.z, b.z, fmaf(a.w, b.w, acc))));
+      }
+    } else {
+      for (int64_t c = lane; c < e.w; c += 64) acc = fmaf(row[c], x[c], acc);
+    }
+  } else {
+    for (int64_t c = lane; c < e.w; c += 64) acc = fmaf(row[c], e.v[logical_col(e, c)], acc);
+  }
   acc = wave_sum(acc);
   if (lane == 0) e.s[r] = acc * k;
 }
@@ -116,7 +135,7 @@ __global__ void __launch_bounds__(kT) sn_final(const SnEntry* __restrict__ ents,
     const float inv_s = 1.f / fmaxf(sqrtf(ss), eps);
     const float inv_t = 1.f / fmaxf(sqrtf(scal[4 * blockIdx.x]), eps);
     for (int64_t r = threadIdx.x; r < e.h; r += kT) e.u[r] = e.s[r] * inv_s;
-    for (int64_t c = threadIdx.x; c < e.w; c += kT) e.v[c] = e.t[c] * inv_t;
+    for (int64_t c = threadIdx.x; c < e.w; c += kT) e.v[logical_col(e, c)] = e.t[c] * inv_t;
     if (threadIdx.x == 0) {
       scal[4 * blockIdx.x + 1] = ss;
       sigma[blockIdx.x] = ss * inv_s;  // u . s = |s|^2 / max(|s|, eps)
