@@ -55,6 +55,8 @@ def parse():
                         'print GPU time per (op, input shapes) to stderr')
     p.add_argument('--op-profile', action='store_true',
                    help='like --conv-profile but for every aten op (self device time)')
+    p.add_argument('--op-stack', action='store_true',
+                   help='with --op-profile: group the small elementwise ops by Python call site')
     return p.parse_args()
 
 
@@ -138,10 +140,20 @@ def main():
         from torch.profiler import ProfilerActivity, profile
         torch.cuda.synchronize()
         with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA],
-                     record_shapes=True) as prof:
+                     record_shapes=True, with_stack=args.op_stack) as prof:
             step(args.warmup)
             torch.cuda.synchronize()
-        if args.op_profile:
+        if args.op_profile and args.op_stack:
+            rows = [e for e in prof.key_averages(group_by_stack_n=4)
+                    if e.self_device_time_total > 0 and e.key.startswith('aten::') and
+                    e.key not in ('aten::convolution_backward', 'aten::miopen_convolution')]
+            rows.sort(key=lambda e: -e.self_device_time_total)
+            print('op self GPU time by call site (aten ops only): %.2f ms' % (
+                sum(e.self_device_time_total for e in rows) / 1e3))
+            for e in rows[:60]:
+                print('%9.3f ms %5d  %-24s %s' % (e.self_device_time_total / 1e3, e.count,
+                                                  e.key[:24], ' <- '.join(e.stack[:4])[:220]))
+        elif args.op_profile:
             rows = [e for e in prof.key_averages(group_by_input_shape=True)
                     if e.self_device_time_total > 0 and e.input_shapes is not None and
                     not e.key.startswith(('void', 'igemm', 'iamd', '__amd', 'Sub'))]

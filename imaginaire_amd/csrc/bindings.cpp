@@ -67,6 +67,8 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
 at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t KH, int64_t KW,
                              int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh,
                              int64_t dw);
+at::Tensor sn_scale_backward(const at::Tensor& grad_in, const at::Tensor& weight,
+                             const at::Tensor& u, const at::Tensor& v, const at::Tensor& sigma);
 void register_lmdb(pybind11::module_& m);
 void profile_marker(int64_t tag);
 std::vector<at::Tensor> mt_sn_scale_cast(const std::vector<at::Tensor>& weights,
@@ -83,6 +85,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("profile_marker", &iamd::profile_marker, "named no-op kernel for trace phase splits");
   m.def("conv2d_mfma", &iamd::conv2d_mfma, "MFMA implicit-GEMM NHWC conv + bias + act (k10)");
   m.def("conv2d_wgrad_mfma", &iamd::conv2d_wgrad_mfma, "MFMA conv weight gradient (k11)");
+  m.def("sn_scale_backward", &iamd::sn_scale_backward, "spectral-norm W/sigma backward (k5d)");
   m.def("norm_stats", &iamd::norm_stats, "per-(group,channel) statistics (k1)");
   m.def("norm_apply", &iamd::norm_apply, "norm + SPADE modulation + activation (k1 fwd)");
   m.def("norm_bwd_reduce", &iamd::norm_bwd_reduce, "k1 backward reduction");

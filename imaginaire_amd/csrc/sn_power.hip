@@ -363,3 +363,114 @@ std::vector<at::Tensor> mt_sn_scale_cast(const std::vector<at::Tensor>& weights,
 }
 
 }  // namespace iamd
+
+namespace iamd {
+
+// ---- k5d: spectral-norm scale backward -------------------------------------------------
+//   dW = G/σ − (⟨G, W⟩/σ²) u vᵀ      (W/σ with u, v, σ held constant; reference semantics of
+//                                    torch.nn.utils.spectral_norm's weight = W_orig / σ)
+// Two launches per layer instead of ~7 full-weight PyTorch passes (fp32 cast of G, G·W, sum,
+// outer(u, v), scale, divide, subtract): K1 partial ⟨G, W⟩ per block + v permuted into the
+// weight's memory column order; K2 sums the partials (same order in every block:
+// deterministic) and writes dW row by row with coalesced v reads.
+namespace {
+
+constexpr int kSnbT = 256;
+
+template <typename G>
+__global__ void __launch_bounds__(kSnbT)
+snb_reduce(const G* __restrict__ g, const float* __restrict__ W, int64_t n,
+           const float* __restrict__ v, float* __restrict__ vm, int64_t w, int64_t cl_cin,
+           int64_t cl_khw, float* __restrict__ partial) {
+  __shared__ float sh[kSnbT / 64];
+  const int64_t gtid = (int64_t)blockIdx.x * kSnbT + threadIdx.x;
+  const int64_t gsz = (int64_t)gridDim.x * kSnbT;
+  for (int64_t c = gtid; c < w; c += gsz) {
+    int64_t lc = c;
+    if (cl_cin) {
+      const uint32_t q = (uint32_t)c / (uint32_t)cl_cin;
+      lc = (int64_t)((uint32_t)c - q * (uint32_t)cl_cin) * cl_khw + q;
+    }
+    vm[c] = v[lc];
+  }
+  float acc = 0.f;
+  for (int64_t i = gtid; i < n; i += gsz) acc = fmaf(to_f<G>(g[i]), W[i], acc);
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int k = 0; k < kSnbT / 64; ++k) s += sh[k];
+    partial[blockIdx.x] = s;
+  }
+}
+
+template <typename G>
+__global__ void __launch_bounds__(kSnbT)
+snb_apply(const G* __restrict__ g, const float* __restrict__ u, const float* __restrict__ vm,
+          const float* __restrict__ sigma, const float* __restrict__ partial, int P,
+          float* __restrict__ dw, int64_t h, int64_t w) {
+  __shared__ float sh[kSnbT / 64];
+  float d = 0.f;
+  for (int k = threadIdx.x; k < P; k += kSnbT) d += partial[k];
+  d = wave_sum(d);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = d;
+  __syncthreads();
+  float dot = 0.f;
+  for (int k = 0; k < kSnbT / 64; ++k) dot += sh[k];
+  const float s = sigma[0];
+  const float inv = 1.f / s;
+  const float coef = dot / (s * s);
+  for (int64_t r = blockIdx.x; r < h; r += gridDim.x) {
+    const float cu = coef * u[r];
+    const G* gr = g + r * w;
+    float* dr = dw + r * w;
+    for (int64_t c = threadIdx.x; c < w; c += kSnbT)
+      dr[c] = fmaf(to_f<G>(gr[c]), inv, -cu * vm[c]);
+  }
+}
+
+}  // namespace
+
+at::Tensor sn_scale_backward(const at::Tensor& grad_in, const at::Tensor& weight,
+                             const at::Tensor& u, const at::Tensor& v, const at::Tensor& sigma) {
+  IAMD_CHECK(weight.is_cuda() && weight.scalar_type() == at::kFloat, "sn_scale_backward: fp32 W");
+  IAMD_CHECK(u.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat &&
+                 sigma.scalar_type() == at::kFloat && sigma.numel() >= 1,
+             "sn_scale_backward: fp32 u, v, sigma");
+  const bool cl = weight.dim() == 4 && !weight.is_contiguous() &&
+                  weight.is_contiguous(at::MemoryFormat::ChannelsLast);
+  IAMD_CHECK(cl || weight.is_contiguous(), "sn_scale_backward: W contiguous or channels-last");
+  const auto fmt = cl ? at::MemoryFormat::ChannelsLast : at::MemoryFormat::Contiguous;
+  at::Tensor grad = grad_in.contiguous(fmt);
+  const int64_t n = weight.numel(), h = weight.size(0), w = n / std::max<int64_t>(1, h);
+  IAMD_CHECK(u.numel() == h && v.numel() == w, "sn_scale_backward: u/v sizes");
+  IAMD_CHECK(w < (1ll << 31), "sn_scale_backward: row too long");
+  const int64_t cl_cin = cl ? weight.size(1) : 0, cl_khw = cl ? weight.size(2) * weight.size(3) : 0;
+  auto dw = at::empty_like(weight, fmt);
+  const int P = (int)std::max<int64_t>(1, std::min<int64_t>(512, (n + 4095) / 4096));
+  auto ws = at::empty({P + w}, weight.options());
+  float* partial = ws.data_ptr<float>();
+  float* vm = partial + P;
+  const int ablocks = (int)std::max<int64_t>(1, std::min<int64_t>(h, 1024));
+  hipStream_t st = stream();
+  auto run = [&](auto* gp) {
+    using G = std::remove_const_t<std::remove_pointer_t<decltype(gp)>>;
+    hipLaunchKernelGGL((snb_reduce<G>), dim3(P), dim3(kSnbT), 0, st, gp,
+                       weight.data_ptr<float>(), n, v.data_ptr<float>(), vm, w, cl_cin, cl_khw,
+                       partial);
+    hipLaunchKernelGGL((snb_apply<G>), dim3(ablocks), dim3(kSnbT), 0, st, gp,
+                       u.data_ptr<float>(), vm, sigma.data_ptr<float>(), partial, P,
+                       dw.data_ptr<float>(), h, w);
+  };
+  if (grad.scalar_type() == at::kBFloat16)
+    run(reinterpret_cast<const __hip_bfloat16*>(grad.data_ptr()));
+  else if (grad.scalar_type() == at::kFloat)
+    run(grad.data_ptr<float>());
+  else
+    IAMD_CHECK(false, "sn_scale_backward: grad must be bf16 or fp32");
+  IAMD_LAUNCH_CHECK();
+  return dw;
+}
+
+}  // namespace iamd

@@ -40,6 +40,9 @@ class _SNScale(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad):
         weight, u, v, sigma = ctx.saved_tensors
+        if _ext.use_native(weight) and weight.dtype == torch.float32 and \
+                grad.dtype in (torch.float32, torch.bfloat16):
+            return _ext.ext().sn_scale_backward(grad, weight, u, v, sigma), None, None, None
         g = grad.float()
         dot = (g * weight).sum()
         outer = torch.outer(u, v).view(weight.shape)
