@@ -16,11 +16,16 @@
 //     each lane accumulates up to 3 displacements for its pixel in fp32 registers.
 //     Every input element is read from HBM once per displacement row instead of once
 //     per displacement (21x fewer global reads than the per-pixel reference kernel).
+//   * bf16 inputs with C % 32 == 0 (FlowNetC's 256-channel conv3 features) take the MFMA
+//     forward corr_fwd_mfma: a parity-split banded 16x48 v_mfma_f32_16x16x32_bf16 product per
+//     (row, displacement row, 16*stride2 pixels), fragments loaded straight from NHWC rows.
 //   * Backward is gather-form (one lane per (pixel, channel); displacement loop with
 //     broadcast reads of grad_out) so it needs no atomics and is deterministic.
 //   * Output is written channels-last [N, oH, oW, D*D] so the FlowNetC concat +
 //     conv3_1 that consume it stay NHWC.
 #include "common.h"
+
+#include <cstdlib>
 
 namespace iamd {
 namespace {
@@ -99,6 +104,83 @@ __global__ __launch_bounds__(kCorrThreads) void corr_fwd_k1(
     const int tir = grp + k * ngrp;
     if (tir < D) o[tjr * D + tir] = from_f<T>(acc[k] * inv);
   }
+}
+
+// MFMA forward for kernel_size == 1, stride1 == 1, stride2 in {1, 2}, bf16, C % 32 == 0 (the
+// FlowNetC configuration: pad 20, max_disp 20, stride2 2 on 256-channel conv3 features).
+// For one output row, one displacement row tj and TX = 16*S2 output pixels, split the pixels
+// by parity r = x mod S2: pixel x = S2*a + r needs strip pixel S2*(a + t) + r for t in [0, D),
+// so G_r[a][j] = sum_c A[S2*a + r][c] * B[S2*j + r][c] is a 16 x 48 MFMA product
+// (v_mfma_f32_16x16x32_bf16, three 16-column fragments) and out[x][t] = G_r[a][a + t] is its
+// band. Fragments are 16-byte NHWC channel runs loaded straight from global/L2 (each lane
+// holds 8 channels of one pixel, the MFMA operand layout), so the kernel needs no LDS; the
+// strip row of image 2 is shared by the D blocks of neighbouring output rows through L2.
+template <int S2>
+__global__ __launch_bounds__(64) void corr_fwd_mfma(
+    const __hip_bfloat16* __restrict__ in1, const __hip_bfloat16* __restrict__ in2,
+    __hip_bfloat16* __restrict__ out, int H, int W, int C, int oH, int oW, int pad, int md,
+    int R, int D) {
+  typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+  typedef __attribute__((ext_vector_type(4))) float f32x4;
+  constexpr int TX = 16 * S2;
+  const int ox0 = blockIdx.x * TX, oy = blockIdx.y;
+  const int n = blockIdx.z / D, tjr = blockIdx.z - (blockIdx.z / D) * D;
+  const int lane = threadIdx.x;
+  const int fr = lane & 15, fk = (lane >> 4) * 8;
+  const int y1 = oy + md - pad;
+  const int y2 = y1 + (tjr - R) * S2;
+  const bool row1 = (unsigned)y1 < (unsigned)H, row2 = (unsigned)y2 < (unsigned)H;
+  const int xa0 = ox0 + md - pad;   // image column of tile pixel 0
+  const int xb0 = xa0 - R * S2;     // image column of strip pixel 0
+  const __hip_bfloat16* r1 = in1 + ((int64_t)n * H + (row1 ? y1 : 0)) * W * C;
+  const __hip_bfloat16* r2 = in2 + ((int64_t)n * H + (row2 ? y2 : 0)) * W * C;
+  const bf16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
+  int aoff[S2], boff[S2][3];
+  bool aok[S2], bok[S2][3];
+#pragma unroll
+  for (int r = 0; r < S2; ++r) {
+    const int xa = xa0 + S2 * fr + r;
+    aok[r] = row1 && (unsigned)xa < (unsigned)W && ox0 + S2 * fr + r < oW;
+    aoff[r] = aok[r] ? xa * C + fk : 0;
+#pragma unroll
+    for (int cf = 0; cf < 3; ++cf) {
+      const int xb = xb0 + S2 * (cf * 16 + fr) + r;
+      bok[r][cf] = row2 && (unsigned)xb < (unsigned)W;
+      boff[r][cf] = bok[r][cf] ? xb * C + fk : 0;
+    }
+  }
+  f32x4 acc[S2][3];
+#pragma unroll
+  for (int r = 0; r < S2; ++r)
+#pragma unroll
+    for (int cf = 0; cf < 3; ++cf) acc[r][cf] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int c0 = 0; c0 < C; c0 += 32) {
+#pragma unroll
+    for (int r = 0; r < S2; ++r) {
+      const bf16x8 af = aok[r] ? *reinterpret_cast<const bf16x8*>(r1 + aoff[r] + c0) : zero;
+#pragma unroll
+      for (int cf = 0; cf < 3; ++cf) {
+        const bf16x8 bfr =
+            bok[r][cf] ? *reinterpret_cast<const bf16x8*>(r2 + boff[r][cf] + c0) : zero;
+        acc[r][cf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[r][cf], 0, 0, 0);
+      }
+    }
+  }
+  const float inv = 1.f / (float)C;
+  const int DD = D * D;
+#pragma unroll
+  for (int r = 0; r < S2; ++r)
+#pragma unroll
+    for (int cf = 0; cf < 3; ++cf)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int a = (lane >> 4) * 4 + e;
+        const int t = cf * 16 + fr - a;
+        const int ox = ox0 + S2 * a + r;
+        if (t >= 0 && t < D && ox < oW)
+          out[(((int64_t)n * oH + oy) * oW + ox) * DD + tjr * D + t] =
+              __float2bfloat16(acc[r][cf][e] * inv);
+      }
 }
 
 // Generic forward (any kernel_size): one workgroup (one wave) per output pixel.
@@ -240,6 +322,22 @@ at::Tensor correlation_forward(const at::Tensor& input1, const at::Tensor& input
   auto out = at::empty({N, D * D, oH, oW},
                        a.options().memory_format(at::MemoryFormat::ChannelsLast));
   const int ngrp = kCorrThreads / kTX;
+  const char* mf = std::getenv("IMAGINAIRE_AMD_CORR_MFMA");
+  if ((mf == nullptr || mf[0] != '0') && a.scalar_type() == at::kBFloat16 && ks == 1 && s1 == 1 &&
+      (s2 == 1 || s2 == 2) &&
+      C % 32 == 0 && D <= 33 && (int64_t)H * W * C < (1ll << 31)) {
+    auto pa = reinterpret_cast<const __hip_bfloat16*>(a.data_ptr());
+    auto pb = reinterpret_cast<const __hip_bfloat16*>(b.data_ptr());
+    auto po = reinterpret_cast<__hip_bfloat16*>(out.data_ptr());
+    if (s2 == 2)
+      hipLaunchKernelGGL((corr_fwd_mfma<2>), dim3(ceil_div(oW, 32), oH, N * D), dim3(64), 0,
+                         stream(), pa, pb, po, H, W, C, oH, oW, (int)pad, (int)md, R, D);
+    else
+      hipLaunchKernelGGL((corr_fwd_mfma<1>), dim3(ceil_div(oW, 16), oH, N * D), dim3(64), 0,
+                         stream(), pa, pb, po, H, W, C, oH, oW, (int)pad, (int)md, R, D);
+    IAMD_LAUNCH_CHECK();
+    return out;
+  }
   IAMD_DISPATCH_FLOAT_TYPES(a.scalar_type(), "correlation_fwd", [&] {
     auto pa = reinterpret_cast<const scalar_t*>(a.data_ptr());
     auto pb = reinterpret_cast<const scalar_t*>(b.data_ptr());

@@ -190,10 +190,11 @@ def test_multi_tensor_adam_and_ema(layout):
 
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('params', [(20, 1, 20, 1, 2), (4, 1, 4, 1, 1), (3, 3, 2, 2, 1)])
-def test_correlation(dtype, params):
+@pytest.mark.parametrize('C', [40, 64])  # 64: bf16 takes the MFMA forward (C % 32 == 0)
+def test_correlation(dtype, params, C):
     from imaginaire_amd.ops.flownet_ops import _CorrelationFn, correlation_reference
     torch.manual_seed(3)
-    N, C, H, W = 2, 40, 13, 37
+    N, H, W = 2, 13, 37
     a = torch.randn(N, C, H, W, device='cuda').to(dtype).contiguous(
         memory_format=torch.channels_last).requires_grad_(True)
     b = torch.randn(N, C, H, W, device='cuda').to(dtype).requires_grad_(True)
