@@ -137,7 +137,11 @@ class _MfmaConv2d(torch.autograd.Function):
         ctx.conf = (stride, padding, dilation, float(slope), cin, cout, x.dtype, w.dtype,
                     None if bias is None else bias.dtype, x.shape[1])
         ctx.save_for_backward(xb, wb, y)
-        return y if op == cout else y[:, :cout]
+        if op == cout:
+            return y
+        # a fresh tensor, not a view of y: callers apply in-place activations (nn.ReLU(
+        # inplace=True)) to conv outputs, which autograd forbids on a custom Function's view
+        return y[:, :cout].contiguous(memory_format=_CL)
 
     @staticmethod
     def backward(ctx, dy):

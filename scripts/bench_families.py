@@ -1,0 +1,139 @@
+"""Training-step throughput of any model family on synthetic data (one GPU).
+
+    python scripts/bench_families.py --config <reference-or-framework yaml> [--steps K]
+        [--warmup W] [--batch B] [--seq-len T] [--pool P]
+
+Runs the train.py iteration (``start_of_iteration`` -> ``dis_step`` x ``dis_update`` ->
+``gen_step`` x ``gen_update``) of the family the config names, on batches of the config's
+own shape produced by the synthetic dataset (``imaginaire_amd.datasets.synthetic``, random
+init, no checkpoints) and kept resident on the GPU (a pool of P batches cycled), and prints
+ONE JSON line: samples/s (images for image families, sequences x frames for video families)
+and ms per iteration. The reference configs (configs/projects/... of the reference checkout)
+load unchanged; only ``data.type`` is switched to the synthetic dataset.
+
+Used for the BASELINE.json secondary configs (MUNIT 256x256, vid2vid 512x1024 seq 3, ...);
+the flagship SPADE number comes from ``bench.py``.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument('--config', required=True)
+    p.add_argument('--steps', type=int, default=5)
+    p.add_argument('--warmup', type=int, default=2)
+    p.add_argument('--batch', type=int, default=None)
+    p.add_argument('--seq-len', type=int, default=None,
+                   help='video families: frames per training sequence')
+    p.add_argument('--pool', type=int, default=2)
+    p.add_argument('--cpu', action='store_true', help='plumbing check on the CPU')
+    args = p.parse_args()
+
+    import torch
+    from torch.utils.data import default_collate
+    from imaginaire_amd.config import Config
+    from imaginaire_amd.datasets.synthetic import Dataset
+    from imaginaire_amd.utils.trainer import get_model_optimizer_and_scheduler, get_trainer
+
+    real_stdout, sys.stdout = sys.stdout, sys.stderr
+    device = torch.device('cpu' if args.cpu else 'cuda', 0)
+    if device.type == 'cuda':
+        torch.cuda.set_device(0)
+    cfg = Config(args.config)
+    cfg.logdir = '/tmp/imaginaire_amd_bench_families'
+    # the synthetic dataset is constructed directly below; cfg.data.type keeps naming the
+    # reference dataset so the batch contract (few-shot keys, video axis) follows it
+    if args.batch:
+        cfg.data.train.batch_size = args.batch
+    bs = cfg.data.train.batch_size
+    video = hasattr(cfg.data, 'num_frames_G')
+    if video and args.seq_len:
+        cfg.data.train.initial_sequence_length = args.seq_len
+        cfg.data.train.max_sequence_length = args.seq_len
+    ds = Dataset(cfg)
+
+    class _Loader(list):  # the trainers read train_data_loader.dataset (sequence schedule)
+        dataset = ds
+
+    net_G, net_D, opt_G, opt_D, sch_G, sch_D = get_model_optimizer_and_scheduler(cfg, seed=0)
+    trainer = get_trainer(cfg, net_G, net_D, opt_G, opt_D, sch_G, sch_D,
+                          train_data_loader=_Loader(), val_data_loader=None)
+    if video and args.seq_len:
+        # past the single-frame epochs: temporal network (flow, warping, temporal D) active
+        if hasattr(trainer, 'init_temporal_network'):
+            trainer.init_temporal_network()
+        ds.set_sequence_length(args.seq_len)
+        trainer.sequence_length = args.seq_len
+
+    def to_dev(x):
+        if torch.is_tensor(x):
+            return x.to(device, non_blocking=True)
+        if isinstance(x, dict):
+            return {k: to_dev(v) for k, v in x.items()}
+        if isinstance(x, list):
+            return [to_dev(v) for v in x]
+        return x
+
+    pool = [to_dev(default_collate([ds[(i * bs + j) % max(1, len(ds))] for j in range(bs)]))
+            for i in range(args.pool)]
+
+    def fresh(x):  # some pre-processing (DensePose label remap) edits the batch in place
+        if torch.is_tensor(x):
+            return x.clone()
+        if isinstance(x, dict):
+            return {k: fresh(v) for k, v in x.items()}
+        if isinstance(x, list):
+            return [fresh(v) for v in x]
+        return x
+
+    def step(it):
+        data = fresh(pool[it % len(pool)])
+        data = trainer.start_of_iteration(data, it)
+        for _ in range(cfg.trainer.dis_step):
+            trainer.dis_update(data)
+        for _ in range(cfg.trainer.gen_step):
+            trainer.gen_update(data)
+        return data
+
+    def sync():
+        if device.type == 'cuda':
+            torch.cuda.synchronize()
+
+    data = None
+    for it in range(args.warmup):
+        data = step(it)
+        print('[bench_families] warmup %d done' % it, flush=True)
+    sync()
+    t0 = time.perf_counter()
+    for it in range(args.steps):
+        data = step(args.warmup + it)
+    sync()
+    dt = (time.perf_counter() - t0) / args.steps
+    frames = 1
+    if video:
+        img = data.get('images') if isinstance(data, dict) else None
+        frames = img.shape[1] if torch.is_tensor(img) and img.dim() == 5 else \
+            (args.seq_len or 1)
+    h, w = ds.h, ds.w
+    sys.stdout = real_stdout
+    print(json.dumps({
+        'config': os.path.relpath(args.config),
+        'family': cfg.trainer.type.split('.')[-1],
+        'resolution': '%dx%d' % (h, w), 'batch': bs, 'frames_per_sample': frames,
+        'ms_per_iteration': round(dt * 1e3, 2),
+        'samples_per_s': round(bs / dt, 3), 'frames_per_s': round(bs * frames / dt, 3),
+        'device': torch.cuda.get_device_name(0) if device.type == 'cuda' else 'cpu',
+        'data': 'synthetic, random-init weights',
+        'peak_mem_gb': round(torch.cuda.max_memory_allocated() / 2 ** 30, 2)
+        if device.type == 'cuda' else None}), flush=True)
+
+
+if __name__ == '__main__':
+    main()

@@ -379,3 +379,17 @@ def test_conv2d_mfma_splitk_matches(splitk):
     ref = F.leaky_relu(F.conv2d(x.float(), w.float(), b, 1, 2), 0.2)
     err = (y.float() - ref).abs().max().item()
     assert err <= 1e-2 * max(1.0, ref.abs().max().item()), err
+
+
+def test_conv2d_mfma_padded_cout_allows_inplace_activation():
+    """A Cout padded to 64 must not hand out a view (nn.ReLU(inplace=True) follows convs in
+    MUNIT/FUNIT decoders; found by scripts/gpu/families_round.sh)."""
+    from imaginaire_amd.ops import conv as C
+    x = torch.randn(2, 64, 16, 16, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last).requires_grad_(True)
+    w = (torch.randn(100, 64, 3, 3, device='cuda') * 0.05).to(torch.bfloat16).requires_grad_(True)
+    y = C.conv2d(x, w, None, 1, 1)
+    assert y.shape[1] == 100
+    torch.relu_(y)
+    y.float().sum().backward()
+    assert x.grad is not None and w.grad is not None and torch.isfinite(w.grad.float()).all()
