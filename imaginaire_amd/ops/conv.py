@@ -136,7 +136,9 @@ class _MfmaConv2d(torch.autograd.Function):
                                    padding[0], padding[1], dilation[0], dilation[1], float(slope))
         ctx.conf = (stride, padding, dilation, float(slope), cin, cout, x.dtype, w.dtype,
                     None if bias is None else bias.dtype, x.shape[1])
-        ctx.save_for_backward(xb, wb, y)
+        # the output is needed only for a fused activation's mask: with slope 1 it is not
+        # saved, so in-place ops on the conv output stay legal (as after a plain F.conv2d)
+        ctx.save_for_backward(xb, wb, y if slope != 1.0 else None)
         if op == cout:
             return y
         # a fresh tensor, not a view of y: callers apply in-place activations (nn.ReLU(
@@ -151,7 +153,8 @@ class _MfmaConv2d(torch.autograd.Function):
         dy = _pad_channels(dy.to(torch.bfloat16), wb.shape[0])
         db = None
         if slope != 1.0 or need_b:
-            dy, db = _ext.ext().bias_act_bwd(y, dy, slope)
+            # identity activation: the k2 kernel reads only dy (y stands in for the layout)
+            dy, db = _ext.ext().bias_act_bwd(y if y is not None else dy, dy, slope)
         dx = dw = None
         if need_x:
             kh, kw = wb.shape[2], wb.shape[3]

@@ -34,6 +34,10 @@ def main():
                    help='video families: frames per training sequence')
     p.add_argument('--pool', type=int, default=2)
     p.add_argument('--cpu', action='store_true', help='plumbing check on the CPU')
+    p.add_argument('--set', nargs='*', default=[], metavar='KEY=VALUE',
+                   help='dotted config overrides, e.g. gen.num_filters=64 '
+                        'data.train.augmentations.random_crop_h_w=256,256 (scale a unit-test '
+                        'config up to a recipe without another YAML)')
     args = p.parse_args()
 
     import torch
@@ -48,6 +52,20 @@ def main():
         torch.cuda.set_device(0)
     cfg = Config(args.config)
     cfg.logdir = '/tmp/imaginaire_amd_bench_families'
+    for kv in args.set:
+        key, val = kv.split('=', 1)
+        node = cfg
+        parts = key.split('.')
+        for k in parts[:-1]:
+            node = getattr(node, k)
+        try:
+            val = int(val)
+        except ValueError:
+            try:
+                val = float(val)
+            except ValueError:
+                pass
+        setattr(node, parts[-1], val)
     # the synthetic dataset is constructed directly below; cfg.data.type keeps naming the
     # reference dataset so the batch contract (few-shot keys, video axis) follows it
     if args.batch:

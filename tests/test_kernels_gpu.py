@@ -393,3 +393,17 @@ def test_conv2d_mfma_padded_cout_allows_inplace_activation():
     torch.relu_(y)
     y.float().sum().backward()
     assert x.grad is not None and w.grad is not None and torch.isfinite(w.grad.float()).all()
+
+
+def test_conv2d_mfma_output_allows_inplace_op_without_activation():
+    """Without a fused activation the conv output is not saved for backward, so an in-place
+    op on it (MUNIT decoder at recipe scale) is legal, as after F.conv2d."""
+    from imaginaire_amd.ops import conv as C
+    x = torch.randn(2, 64, 16, 16, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last).requires_grad_(True)
+    w = (torch.randn(128, 64, 3, 3, device='cuda') * 0.05).to(torch.bfloat16).requires_grad_(True)
+    b = torch.zeros(128, device='cuda', requires_grad=True)
+    y = C.conv2d(x, w, b, 1, 1)
+    torch.relu_(y)
+    y.float().sum().backward()
+    assert b.grad is not None and torch.isfinite(w.grad.float()).all()
