@@ -1,9 +1,10 @@
 """SPADE discriminator: PatchGAN pyramid + FPSE (reference discriminators/spade.py:15-117).
 
-Real and fake are run as ONE batched forward (concatenated along the batch
-axis) instead of two separate passes: the same math (no batch-coupled layers,
-activation_norm_type is 'none'), half the kernel launches and twice the
-parallelism per MIOpen call.
+In the D update real and fake are run as ONE batched forward (concatenated
+along the batch axis) instead of two separate passes: the same math (no
+batch-coupled layers, activation_norm_type is 'none'), half the kernel launches
+and twice the parallelism per conv. In the G update (gradient flows through the
+fake branch only) the passes stay separate so the backward skips the real half.
 """
 import torch
 import torch.nn as nn
@@ -62,7 +63,12 @@ class Discriminator(nn.Module):
     def forward(self, data, net_G_output):
         output_x = dict()
         real, fake = data['images'], net_G_output['fake_images']
-        if self.batched and real.shape == fake.shape:
+        # Batch real+fake only in the D update (fake detached; D weights need grads from both
+        # halves). In the G update the real branch needs no backward at all: batched, the
+        # conv backward would still compute it for the real half (~half of D's data-gradient
+        # work), so the two passes run separately there, as in the reference.
+        grad_through_fake = torch.is_grad_enabled() and fake.requires_grad
+        if self.batched and real.shape == fake.shape and not grad_through_fake:
             # NOTE: one spectral-norm power iteration per D call (the reference's
             # two sequential passes take two); σ estimates converge identically.
             n = real.shape[0]
