@@ -394,7 +394,18 @@ snb_reduce(const G* __restrict__ g, const float* __restrict__ W, int64_t n,
     vm[c] = v[lc];
   }
   float acc = 0.f;
-  for (int64_t i = gtid; i < n; i += gsz) acc = fmaf(to_f<G>(g[i]), W[i], acc);
+  if ((n & 7) == 0) {  // 8 elements per lane per trip: 16-B (bf16) / 2x16-B (fp32) loads
+    for (int64_t i = gtid * 8; i < n; i += gsz * 8) {
+      float gv[8], wv[8];
+      load_vec<G, 8>(g + i, gv);
+      load_vec<float, 4>(W + i, *reinterpret_cast<float(*)[4]>(wv));
+      load_vec<float, 4>(W + i + 4, *reinterpret_cast<float(*)[4]>(wv + 4));
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc = fmaf(gv[k], wv[k], acc);
+    }
+  } else {
+    for (int64_t i = gtid; i < n; i += gsz) acc = fmaf(to_f<G>(g[i]), W[i], acc);
+  }
   acc = wave_sum(acc);
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
   __syncthreads();
@@ -425,8 +436,19 @@ snb_apply(const G* __restrict__ g, const float* __restrict__ u, const float* __r
     const float cu = coef * u[r];
     const G* gr = g + r * w;
     float* dr = dw + r * w;
-    for (int64_t c = threadIdx.x; c < w; c += kSnbT)
-      dr[c] = fmaf(to_f<G>(gr[c]), inv, -cu * vm[c]);
+    if ((w & 3) == 0) {  // 4 columns per lane: 16-B fp32 stores / vm loads
+      for (int64_t c = threadIdx.x * 4; c < w; c += kSnbT * 4) {
+        float gv[4], vv[4], o[4];
+        load_vec<G, 4>(gr + c, gv);
+        load_vec<float, 4>(vm + c, vv);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = fmaf(gv[k], inv, -cu * vv[k]);
+        store_vec<float, 4>(dr + c, o);
+      }
+    } else {
+      for (int64_t c = threadIdx.x; c < w; c += kSnbT)
+        dr[c] = fmaf(to_f<G>(gr[c]), inv, -cu * vm[c]);
+    }
   }
 }
 
@@ -449,9 +471,10 @@ at::Tensor sn_scale_backward(const at::Tensor& grad_in, const at::Tensor& weight
   const int64_t cl_cin = cl ? weight.size(1) : 0, cl_khw = cl ? weight.size(2) * weight.size(3) : 0;
   auto dw = at::empty_like(weight, fmt);
   const int P = (int)std::max<int64_t>(1, std::min<int64_t>(512, (n + 4095) / 4096));
-  auto ws = at::empty({P + w}, weight.options());
+  const int P4 = (P + 3) & ~3;  // keeps vm 16-byte aligned for the vector loads
+  auto ws = at::empty({P4 + w}, weight.options());
   float* partial = ws.data_ptr<float>();
-  float* vm = partial + P;
+  float* vm = partial + P4;
   const int ablocks = (int)std::max<int64_t>(1, std::min<int64_t>(h, 1024));
   hipStream_t st = stream();
   auto run = [&](auto* gp) {
