@@ -236,6 +236,11 @@ class DeviceBatchSource(object):
 
     def __init__(self, cfg, batch_size, device, pool=16, seed=0):
         ds = Dataset(cfg)
+        # bf16 batches when the trainer runs bf16 autocast on the GPU (its first use casts)
+        amp = getattr(getattr(cfg, 'trainer', None), 'amp', 'O0')
+        self.dtype = torch.bfloat16 if (torch.device(device).type == 'cuda' and
+                                        amp in ('O1', 'O2', 'O3', 'bf16', True)) \
+            else torch.float32
         self.batch_size = batch_size
         self.device = device
         self.types = ds.types
@@ -256,11 +261,11 @@ class DeviceBatchSource(object):
                     extra[name] = fr[name]
             self.index_maps.append(idx)
             self.extra.append(extra)
-        self.images = torch.stack(self.images).to(device).contiguous(
+        self.images = torch.stack(self.images).to(device, self.dtype).contiguous(
             memory_format=torch.channels_last)
         self.idx = {n: torch.stack([m[n] for m in self.index_maps]).to(device)
                     for n in self.index_maps[0]}
-        self.ext = {n: torch.stack([m[n] for m in self.extra]).to(device)
+        self.ext = {n: torch.stack([m[n] for m in self.extra]).to(device, self.dtype)
                     for n in (self.extra[0] if self.extra else {})}
         self.pool = pool
         self.step = 0
@@ -268,18 +273,27 @@ class DeviceBatchSource(object):
     def next(self):
         sel = torch.arange(self.step, self.step + self.batch_size, device=self.device) % self.pool
         self.step += self.batch_size
-        parts = []
+        # the label is assembled in place in ONE NHWC (= channels-last) buffer of the compute
+        # dtype: one-hot channels by a scatter into their slice, dense channels copied in
+        widths = []
         for name in self.input_labels:
             t = self.types[name]
             if name in self.idx:
-                nc = t.num_channels + (1 if getattr(t, 'use_dont_care', False) else 0)
-                ind = self.idx[name].index_select(0, sel).long()
-                oh = torch.zeros(self.batch_size, self.h, self.w, nc, device=self.device)
-                oh.scatter_(3, ind.unsqueeze(-1), 1.0)
-                parts.append(oh.permute(0, 3, 1, 2))
+                widths.append(t.num_channels + (1 if getattr(t, 'use_dont_care', False) else 0))
             else:
-                parts.append(self.ext[name].index_select(0, sel))
-        label = torch.cat(parts, 1).contiguous(memory_format=torch.channels_last)
+                widths.append(self.ext[name].shape[1])
+        label = torch.zeros(self.batch_size, self.h, self.w, sum(widths), device=self.device,
+                            dtype=self.dtype)
+        off = 0
+        for name, nc in zip(self.input_labels, widths):
+            part = label[..., off:off + nc]
+            if name in self.idx:
+                ind = self.idx[name].index_select(0, sel).long()
+                part.scatter_(3, ind.unsqueeze(-1), 1.0)
+            else:
+                part.copy_(self.ext[name].index_select(0, sel).permute(0, 2, 3, 1))
+            off += nc
+        label = label.permute(0, 3, 1, 2)  # [B, C, H, W] view, channels-last strides
         return {'label': label, 'images': self.images.index_select(0, sel),
                 'key': {'images': ['synthetic'] * self.batch_size},
                 'original_h_w': torch.tensor([[self.h, self.w]] * self.batch_size)}
