@@ -32,7 +32,9 @@ BASELINE_IMG_S = 20.0
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--gpus', type=int, default=1,
+                   help='number of ranks (one per GPU). Without a launcher (no WORLD_SIZE) '
+                        'bench.py starts them itself through torch.distributed.run')
     p.add_argument('--steps', type=int, default=20)
     p.add_argument('--warmup', type=int, default=6)
     p.add_argument('--config', default=os.path.join(HERE, 'configs', 'bench',
@@ -45,6 +47,8 @@ def parse():
     p.add_argument('--backend', default='nccl',
                    help='process-group backend for N>1 (nccl = RCCL over xGMI; gloo for '
                         'single-GPU multi-rank rehearsals with --share-gpu)')
+    p.add_argument('--device', default='cuda', choices=('cuda', 'cpu'),
+                   help='cpu: plumbing rehearsal of the launcher / DDP path (gloo), no GPU')
     p.add_argument('--share-gpu', action='store_true',
                    help='testing only: every rank uses cuda:0 (rehearse the DDP path on one GPU)')
     p.add_argument('--torch-profile', action='store_true',
@@ -75,8 +79,43 @@ def _heartbeat(period=20.0):
     threading.Thread(target=run, daemon=True).start()
 
 
+def _free_port():
+    import socket
+    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args, argv):
+    """``--gpus N`` without a launcher: start N ranks (one process per GPU) as a CHILD
+    ``torch.distributed.run`` and exit with its status. Runs before anything touches the
+    GPU (no exec from a process holding a HIP context). Reference launch form:
+    ``python -m torch.distributed.launch --nproc_per_node=N train.py`` (projects/*/README.md)."""
+    import subprocess
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           '--nproc-per-node=%d' % args.gpus, '--master-addr=127.0.0.1',
+           '--master-port=%d' % _free_port(), os.path.abspath(__file__)] + argv
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    env.setdefault('OMP_NUM_THREADS', '4')
+    print('[bench] launching %d ranks: %s' % (args.gpus, ' '.join(cmd)), file=sys.stderr,
+          flush=True)
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    world_env = os.environ.get('WORLD_SIZE')
+    if world_env is None and args.gpus > 1:
+        sys.exit(launch_ranks(args, sys.argv[1:]))
+    if world_env is not None and int(world_env) != args.gpus:
+        sys.exit('bench.py: --gpus %d but WORLD_SIZE=%s: refusing to report a %s-rank number '
+                 'as %d GPUs' % (args.gpus, world_env, world_env, args.gpus))
+    if args.share_gpu and args.gpus > 1 and args.backend == 'nccl':
+        sys.exit('bench.py: --share-gpu needs --backend gloo (RCCL cannot place two ranks '
+                 'on one GPU)')
     _heartbeat()
     if args.eager:
         os.environ['IMAGINAIRE_AMD_EAGER'] = '1'
@@ -95,13 +134,15 @@ def main():
     from imaginaire_amd.utils.trainer import get_model_optimizer_and_scheduler, get_trainer
     from imaginaire_amd.datasets.synthetic import DeviceBatchSource
 
-    if world > 1:
-        init_dist(local_rank, backend=args.backend)
-    else:
+    on_gpu = args.device == 'cuda'
+    if on_gpu:
+        # set the device before the process group so RCCL binds rank r to GPU r
         torch.cuda.set_device(local_rank)
+    if world > 1:
+        init_dist(local_rank, backend=args.backend if on_gpu else 'gloo')
     from imaginaire_amd.utils.cudnn import init_cudnn
     init_cudnn(False, True)
-    device = torch.device('cuda', local_rank)
+    device = torch.device('cuda', local_rank) if on_gpu else torch.device('cpu')
     cfg = Config(args.config)
     cfg.logdir = os.path.join('/tmp', 'imaginaire_amd_bench')
     if args.batch:
@@ -177,7 +218,8 @@ def main():
     def barrier():
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
+        if on_gpu:
+            torch.cuda.synchronize()
 
     barrier()
     if args.profile_phases:
@@ -195,7 +237,8 @@ def main():
             print('[bench] step {} queued'.format(it), flush=True)
     barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    t = torch.tensor([elapsed], device=device if args.backend == 'nccl' and on_gpu else 'cpu',
+                     dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
@@ -207,7 +250,7 @@ def main():
                 k, getattr(trainer, 'accu_%s_iter_time' % k) / n * 1e3), flush=True)
     ms_per_step = elapsed / args.steps * 1e3
     value = world * bs * args.steps / elapsed
-    mem_gb = torch.cuda.max_memory_allocated(device) / 2 ** 30
+    mem_gb = torch.cuda.max_memory_allocated(device) / 2 ** 30 if on_gpu else 0.0
     sys.stdout = real_stdout
     if rank == 0:
         out = {
@@ -221,14 +264,17 @@ def main():
             'higher_is_better': True,
             'scaling': 'weak',
             'vs_baseline': round(value / BASELINE_IMG_S, 3),
-            'dtype': 'bf16',
+            'dtype': 'bf16' if on_gpu else 'fp32',
             'data': 'synthetic (COCO-Stuff-shaped: 183 classes + dont-care + edge), random-init weights',
             'config': {'model': 'SPADE/GauGAN (cocostuff base128_bs4 recipe: F=128, style VAE, '
                                 'sync-BN SPADE 5x5 separate-projection, 2xPatchGAN+FPSE D, '
                                 'VGG19 perceptual, EMA)',
                        'global_batch': bs * world, 'seq_len': None, 'resolution': '256x512',
                        'parallelism': 'dp%d' % world,
-                       'kernels': 'eager-reference' if args.eager else 'hip'},
+                       'kernels': 'eager-reference' if args.eager else 'hip',
+                       'backend': args.backend if (world > 1 and on_gpu) else
+                       ('gloo' if world > 1 else None),
+                       'device': args.device},
             'peak_mem_gb_rank0': round(mem_gb, 2),
         }
         print(json.dumps(out), flush=True)

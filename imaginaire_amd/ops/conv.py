@@ -32,8 +32,10 @@ _CL = torch.channels_last
 # itself when its tile grid cannot fill the chip
 _MFMA_MIN_BLOCKS = int(os.environ.get('IMAGINAIRE_AMD_MFMA_MIN_BLOCKS', '16'))
 _MFMA_MIN_DGRAD_BLOCKS = int(os.environ.get('IMAGINAIRE_AMD_MFMA_MIN_DGRAD_BLOCKS', '16'))
-# weight gradient: 'auto' = per-shape faster of k11 / MIOpen wrw, '1' = k11, '0' = MIOpen
-_MFMA_WGRAD = os.environ.get('IMAGINAIRE_AMD_MFMA_WGRAD', 'auto')
+# weight gradient: '1' = k11 (default: faster than MIOpen wrw on every SPADE/D/VGG shape in
+# profiles/conv_mfma_probe_mi355x.txt, and it compiles nothing at first call), '0' = MIOpen,
+# 'auto' = per-shape faster of the two (timed once; the choice is agreed across ranks)
+_MFMA_WGRAD = os.environ.get('IMAGINAIRE_AMD_MFMA_WGRAD', '1')
 
 
 def _mfma_enabled():
@@ -221,6 +223,13 @@ def _wgrad(dy, xb, wb, stride, padding, dilation):
             end.record()
             end.synchronize()
             times[name] = start.elapsed_time(end)
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            # every rank must run the same algorithm: sum the timings over ranks
+            dev = 'cpu' if dist.get_backend() == 'gloo' else dy.device
+            t = torch.tensor([times['k11'], times['miopen']], dtype=torch.float64, device=dev)
+            dist.all_reduce(t)
+            times = {'k11': float(t[0]), 'miopen': float(t[1])}
         choice = min(times, key=times.get)
         _WGRAD_CHOICE[key] = choice
     return k11() if choice == 'k11' else miopen()

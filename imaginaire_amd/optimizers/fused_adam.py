@@ -5,6 +5,13 @@ launch updates every parameter of a param group (fp32 master weights, fp32 or
 bf16 gradients). Gradients are consumed as they are (no unscale pass: bf16
 autocast needs no loss scaler). On CPU the update runs through
 ``torch._foreach_*`` with identical math.
+
+State layout follows apex ``FusedAdam``: the step count lives in the param GROUP
+(``group['step']``, one bias correction per group, advanced once per ``step()``
+call that updates anything) and each parameter keeps only ``exp_avg`` /
+``exp_avg_sq`` — so reference (apex) optimizer checkpoints load and resume
+unchanged. States written by torch ``Adam`` (per-parameter ``'step'``) are
+accepted too: the group step is taken from them when the group has none.
 """
 import math
 
@@ -37,18 +44,22 @@ class FusedAdam(Optimizer):
                 if p.grad.is_sparse:
                     raise RuntimeError('FusedAdam does not support sparse gradients')
                 state = self.state[p]
-                if len(state) == 0:
-                    state['step'] = 0
+                if 'exp_avg' not in state:
                     state['exp_avg'] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     state['exp_avg_sq'] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                state['step'] += 1
                 params.append(p)
                 grads.append(p.grad)
                 m.append(state['exp_avg'])
                 v.append(state['exp_avg_sq'])
             if not params:
                 continue
-            step = self.state[params[0]]['step']
+            if 'step' not in group:
+                # torch-Adam-style state (per-parameter step): adopt the largest
+                prev = [self.state[p].get('step', 0) for p in group['params']
+                        if p in self.state]
+                group['step'] = int(max([float(s) for s in prev], default=0))
+            group['step'] += 1
+            step = group['step']
             beta1, beta2 = group['betas']
             lr, eps, wd = group['lr'], group['eps'], group['weight_decay']
             adamw = group['adam_w_mode']

@@ -20,7 +20,15 @@ designed around how the GAN trainers actually use their networks:
   that free) with a small first bucket to start communication early;
 * optional **bf16 wire format** (``comm_dtype=torch.bfloat16``) halves bytes;
 * **buffers** (SN u/v, BN running stats) are broadcast once at construction
-  and on demand (``sync_buffers()``), not before every forward.
+  and on demand (``sync_buffers()``, called by the trainer at checkpoint /
+  evaluation boundaries), not before every forward;
+* **unused parameters** keep ``grad = None`` (as torch DDP with
+  ``find_unused_parameters=True`` leaves them, so Adam skips them instead of
+  decaying their moments on a zero gradient). ``find_unused='local'`` (default)
+  uses this rank's hook arrivals — exact whenever the trainers' control flow
+  is rank-uniform, which it is (it depends on the frame index / phase, never on
+  data). ``find_unused='global'`` all-reduces a used-parameter mask instead
+  (one tiny collective + one host sync per backward, like torch DDP).
 
 On world size 1 (or no process group) it is a transparent wrapper.
 """
@@ -71,8 +79,12 @@ def _comm_device(group, tensors):
 
 class DistributedDataParallel(nn.Module):
     def __init__(self, module, process_group=None, bucket_cap_mb=256, first_bucket_mb=16,
-                 broadcast_buffers=False, comm_dtype=None, overlap=True, **unused):
+                 broadcast_buffers=False, comm_dtype=None, overlap=True, find_unused='local',
+                 **unused):
         super().__init__()
+        assert find_unused in ('local', 'global'), find_unused
+        self.find_unused = find_unused
+        self._used = set()
         self.module = module
         self.process_group = process_group
         self.world = _world(process_group)
@@ -139,12 +151,12 @@ class DistributedDataParallel(nn.Module):
             b = _Bucket(g, device, torch.float32)
             self.buckets.append(b)
         self._param_bucket = {}
+        self._param_list = [p for b in self.buckets for p in b.params]
         for bi, b in enumerate(self.buckets):
             for p, off in zip(b.params, b.offsets):
                 self._param_bucket[p] = (bi, off)
                 p.grad = _grad_view(b.flat, off, p)
-                if self.overlap:
-                    self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
 
     # -- per-phase protocol -----------------------------------------------
     def begin(self):
@@ -152,6 +164,7 @@ class DistributedDataParallel(nn.Module):
         if self.world <= 1:
             return
         self._active = True
+        self._used = set()
         for b in self.buckets:
             b.arrived = 0
             b.expected = sum(1 for p in b.params if p.requires_grad)
@@ -164,6 +177,9 @@ class DistributedDataParallel(nn.Module):
 
     def _on_grad(self, p):
         if not self._active:
+            return
+        self._used.add(p)
+        if not self.overlap:
             return
         bi, _ = self._param_bucket[p]
         b = self.buckets[bi]
@@ -199,6 +215,27 @@ class DistributedDataParallel(nn.Module):
                 b.flat.mul_(inv)
                 b.work = None
         self._active = False
+        self._drop_unused_grads()
+
+    def _drop_unused_grads(self):
+        """grad = None for parameters that received no gradient in this backward."""
+        params = [p for p in self._param_list if p.requires_grad]
+        if self.find_unused == 'global':
+            flags = torch.tensor([1 if p in self._used else 0 for p in params],
+                                 dtype=torch.int32)
+            if dist.get_backend(self.process_group) != 'gloo':
+                flags = flags.to(self.buckets[0].flat.device)
+            dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=self.process_group)
+            used = flags.cpu().tolist()
+            for p, u in zip(params, used):
+                if not u:
+                    p.grad = None
+            return
+        if len(self._used) == len(params):
+            return
+        for p in params:
+            if p not in self._used:
+                p.grad = None
 
     def zero_grad(self):
         """Zero every bucket in place (keeps .grad as bucket views)."""

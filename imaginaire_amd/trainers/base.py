@@ -146,7 +146,17 @@ class BaseTrainer(object):
     def _pre_save_checkpoint(self):
         pass
 
+    def sync_buffers(self):
+        """Broadcast rank 0's buffers (BN running stats, SN u/v, EMA copy) to every rank:
+        the DDP wrapper does not broadcast them before each forward (the reference's torch
+        DDP does), so they are made identical wherever they are observed — checkpoints and
+        evaluation."""
+        _ddp_call(self.net_G, 'sync_buffers')
+        if self.net_D is not None:
+            _ddp_call(self.net_D, 'sync_buffers')
+
     def save_checkpoint(self, current_epoch, current_iteration):
+        self.sync_buffers()
         self._pre_save_checkpoint()
         return _save_checkpoint(self.cfg, self.net_G, self.net_D, self.opt_G, self.opt_D,
                                 self.sch_G, self.sch_D, current_epoch, current_iteration)
@@ -297,6 +307,7 @@ class BaseTrainer(object):
         self.net_G.train()
 
     def write_metrics(self):
+        self.sync_buffers()
         cur_fid = self._compute_fid()
         if cur_fid is not None:
             self.best_fid = cur_fid if self.best_fid is None else min(self.best_fid, cur_fid)

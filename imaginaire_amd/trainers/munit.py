@@ -156,6 +156,7 @@ class Trainer(BaseTrainer):
                     out['images_aba'], out['images_bab']]
 
     def write_metrics(self):
+        self.sync_buffers()
         res = self._compute_fid()
         if res is None:
             return

@@ -150,6 +150,7 @@ class Trainer(BaseTrainer):
                 avg(cal_data)
 
     def write_metrics(self):
+        self.sync_buffers()
         fids = self._compute_fid()
         if fids is None:
             return

@@ -397,6 +397,7 @@ class Trainer(BaseTrainer):
             self.average_fid_meter = Meter('FID/average')
 
     def write_metrics(self):
+        self.sync_buffers()
         if self.cfg.trainer.model_average:
             res = self._compute_fid()
             if res is None or res[0] is None or res[1] is None:

@@ -122,7 +122,11 @@ def _wrap_model(cfg, model):
                 model, device_ids=[torch.cuda.current_device()] if torch.cuda.is_available()
                 else None, find_unused_parameters=True, broadcast_buffers=False)
         return DistributedDataParallel(model, bucket_cap_mb=bucket_mb, comm_dtype=comm,
-                                       overlap=(ddp != 'apex'))
+                                       overlap=(ddp != 'apex'),
+                                       broadcast_buffers=getattr(cfg.trainer,
+                                                                 'ddp_broadcast_buffers', False),
+                                       find_unused=getattr(cfg.trainer, 'ddp_find_unused',
+                                                           'local'))
     return WrappedModel(model)
 
 

@@ -119,3 +119,54 @@ def test_train_py_two_ranks_gloo(tmp_path):
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     assert 'Done with training' in r.stdout
+
+
+def _unused_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from imaginaire_amd.optimizers import FusedAdam
+    from imaginaire_amd.parallel import DistributedDataParallel
+    torch.manual_seed(0)
+    used = torch.nn.Linear(4, 4)
+    unused = torch.nn.Linear(4, 4)
+    net = torch.nn.ModuleDict({'used': used, 'unused': unused})
+    res = {}
+    for mode in ('local', 'global'):
+        ddp = DistributedDataParallel(net, find_unused=mode)
+        opt = FusedAdam(net.parameters(), lr=0.1)
+        x = torch.randn(3, 4)
+        # step 1: both branches used -> both get Adam moments
+        ddp.begin()
+        (used(x).sum() + unused(x).sum()).backward()
+        ddp.finish()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        before = unused.weight.detach().clone()
+        # step 2: the 'unused' branch gets no gradient -> grad None -> untouched by Adam
+        ddp.begin()
+        used(x).sum().backward()
+        ddp.finish()
+        res[mode] = (unused.weight.grad is None, used.weight.grad is not None)
+        opt.step()
+        res[mode] += (bool(torch.equal(before, unused.weight.detach())),)
+        for h in ddp._hooks:
+            h.remove()
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_ddp_unused_parameters_keep_grad_none():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_unused_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for _, r in res:
+        for mode in ('local', 'global'):
+            assert r[mode] == (True, True, True), (mode, r[mode])

@@ -84,3 +84,34 @@ def test_inference_writes_images(tmp_path):
     for r, _, fs in os.walk(str(tmp_path / 'out')):
         files += fs
     assert any(f.endswith('.jpg') for f in files)
+
+
+def test_fused_adam_resumes_apex_style_state():
+    """apex FusedAdam keeps the step in the param group and only exp_avg/exp_avg_sq per
+    parameter (reference utils/trainer.py:271-281): such a state_dict must load and step."""
+    import torch
+    from imaginaire_amd.optimizers import FusedAdam
+    torch.manual_seed(0)
+    p = torch.nn.Parameter(torch.randn(5))
+    q = torch.nn.Parameter(torch.randn(3))
+    opt = FusedAdam([p, q], lr=0.01, betas=(0.0, 0.999))
+    sd = {'state': {0: {'exp_avg': torch.ones(5) * 0.1, 'exp_avg_sq': torch.ones(5) * 0.01},
+                    1: {'exp_avg': torch.ones(3) * 0.2, 'exp_avg_sq': torch.ones(3) * 0.04}},
+          'param_groups': [{'lr': 0.01, 'betas': (0.0, 0.999), 'eps': 1e-8,
+                            'weight_decay': 0.0, 'adam_w_mode': False, 'step': 7,
+                            'params': [0, 1]}]}
+    opt.load_state_dict(sd)
+    p.grad = torch.ones(5)
+    q.grad = None  # params[0]-independent group step
+    p0 = p.detach().clone()
+    opt.step()
+    assert opt.param_groups[0]['step'] == 8
+    # reference Adam math at step 8
+    ref = torch.optim.Adam([torch.nn.Parameter(p0.clone())], lr=0.01, betas=(0.0, 0.999))
+    rp = ref.param_groups[0]['params'][0]
+    ref.state[rp] = {'step': torch.tensor(7.), 'exp_avg': torch.ones(5) * 0.1,
+                     'exp_avg_sq': torch.ones(5) * 0.01}
+    rp.grad = torch.ones(5)
+    ref.step()
+    assert torch.allclose(p.detach(), rp.detach(), atol=1e-6)
+    assert 'step' not in opt.state[p]
