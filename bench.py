@@ -41,7 +41,11 @@ def parse():
                                                      'spade_256x512_synthetic.yaml'))
     p.add_argument('--batch', type=int, default=None, help='per-GPU batch (default: config)')
     p.add_argument('--eager', action='store_true',
-                   help='self-baseline: PyTorch reference ops instead of the HIP kernels')
+                   help='self-baseline: PyTorch reference ops instead of the HIP kernels '
+                        '(implies --no-graph)')
+    p.add_argument('--no-graph', action='store_true',
+                   help='issue every kernel from Python each step instead of replaying the '
+                        'hipGraph-captured step (A/B)')
     p.add_argument('--profile-phases', action='store_true')
     p.add_argument('--verbose', action='store_true')
     p.add_argument('--backend', default='nccl',
@@ -154,14 +158,18 @@ def main():
     trainer = get_trainer(cfg, net_G, net_D, opt_G, opt_D, sch_G, sch_D,
                           train_data_loader=[], val_data_loader=None)
     src = DeviceBatchSource(cfg, bs, device, pool=8, seed=rank)
+    # steady-state iteration: hipGraph-captured (world size 1) after max(1, W-2) eager
+    # warm-up steps, so with W >= 2 the timed steps are all replays
+    from imaginaire_amd.utils.cuda_graph import make_trainer_step
+    use_graph = on_gpu and not (args.no_graph or args.eager or args.profile_phases) and \
+        args.warmup >= 2
+    run_step, graphed = make_trainer_step(trainer, warmup=min(3, max(1, args.warmup - 2)),
+                                          enabled=use_graph)
 
     def step(it):
         data = src.next()
         data = trainer.start_of_iteration(data, it)
-        for _ in range(cfg.trainer.dis_step):
-            trainer.dis_update(data)
-        for _ in range(cfg.trainer.gen_step):
-            trainer.gen_update(data)
+        run_step(data)
 
     for it in range(args.warmup):
         step(it)
@@ -272,6 +280,7 @@ def main():
                        'global_batch': bs * world, 'seq_len': None, 'resolution': '256x512',
                        'parallelism': 'dp%d' % world,
                        'kernels': 'eager-reference' if args.eager else 'hip',
+                       'hipgraph': bool(graphed is not None and graphed.graph is not None),
                        'backend': args.backend if (world > 1 and on_gpu) else
                        ('gloo' if world > 1 else None),
                        'device': args.device},

@@ -37,11 +37,15 @@ std::vector<at::Tensor> partial_conv_renorm(const at::Tensor& raw, const at::Ten
 void mt_adam(const std::vector<at::Tensor>& params, const std::vector<at::Tensor>& grads,
              const std::vector<at::Tensor>& exp_avgs, const std::vector<at::Tensor>& exp_avg_sqs,
              const std::vector<at::Tensor>& shadows, double lr, double beta1, double beta2,
-             double eps, int64_t step, double weight_decay, bool adamw, double grad_scale);
+             double eps, int64_t step, double weight_decay, bool adamw, double grad_scale,
+             const c10::optional<at::Tensor>& hyper);
 at::Tensor mt_sn_sigma(const std::vector<at::Tensor>& weights, const std::vector<at::Tensor>& us,
                        const std::vector<at::Tensor>& vs);
 void mt_ema(const std::vector<at::Tensor>& targets, const std::vector<at::Tensor>& sources,
-            double beta, const c10::optional<at::Tensor>& sigma);
+            double beta, const c10::optional<at::Tensor>& sigma,
+            const c10::optional<at::Tensor>& count, int64_t start);
+int64_t flush_deferred_uploads();
+bool stream_capturing();
 void mt_scale(const std::vector<at::Tensor>& xs, const at::Tensor& s);
 at::Tensor mt_sqnorm(const std::vector<at::Tensor>& xs);
 // correlation.hip (k6 correlation, k8 channelnorm)
@@ -93,9 +97,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_act_fwd", &iamd::bias_act_fwd, "bias + activation epilogue (k2)");
   m.def("bias_act_bwd", &iamd::bias_act_bwd, "k2 backward: dx and dbias");
   m.def("partial_conv_renorm", &iamd::partial_conv_renorm, "partial conv mask/renorm (k3)");
-  m.def("mt_adam", &iamd::mt_adam, "multi-tensor Adam/AdamW (k4)");
+  m.def("mt_adam", &iamd::mt_adam, "multi-tensor Adam/AdamW (k4)", py::arg("params"),
+        py::arg("grads"), py::arg("exp_avgs"), py::arg("exp_avg_sqs"), py::arg("shadows"),
+        py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"), py::arg("step"),
+        py::arg("weight_decay"), py::arg("adamw"), py::arg("grad_scale"),
+        py::arg("hyper") = py::none());
+  m.def("stream_capturing", &iamd::stream_capturing,
+        "true while the current HIP stream is being captured into a graph");
+  m.def("flush_deferred_uploads", &iamd::flush_deferred_uploads,
+        "copy the device tables created during a hipGraph capture (call after capture)");
   m.def("mt_sn_sigma", &iamd::mt_sn_sigma, "multi-tensor spectral-norm sigma (k5)");
-  m.def("mt_ema", &iamd::mt_ema, "multi-tensor EMA with SN absorption (k5)");
+  m.def("mt_ema", &iamd::mt_ema, "multi-tensor EMA with SN absorption (k5)",
+        py::arg("targets"), py::arg("sources"), py::arg("beta"), py::arg("sigma") = py::none(),
+        py::arg("count") = py::none(), py::arg("start") = 0);
   m.def("mt_scale", &iamd::mt_scale, "multi-tensor scale");
   m.def("mt_sqnorm", &iamd::mt_sqnorm, "multi-tensor squared L2 norm");
   m.def("flow_warp_fwd", &iamd::flow_warp_fwd, "bilinear flow warp, border (k9)");

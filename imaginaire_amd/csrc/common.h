@@ -22,6 +22,13 @@ constexpr int kWave = 64;
 
 inline hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
+// True while the current stream is being captured into a hipGraph.
+bool stream_capturing();
+// Host bytes -> new device byte tensor: async pinned copy normally; under hipGraph capture
+// the copy is deferred to flush_deferred_uploads() (multi_tensor.hip).
+at::Tensor stage_to_device(const void* src, size_t bytes, const at::Device& dev);
+int64_t flush_deferred_uploads();
+
 #define IAMD_CHECK(cond, ...) TORCH_CHECK(cond, "imaginaire_amd: ", __VA_ARGS__)
 #define IAMD_HIP_CHECK(expr)                                                     \
   do {                                                                           \

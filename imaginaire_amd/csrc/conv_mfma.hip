@@ -247,6 +247,202 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_fwd_mfma(ConvA
 #endif  // __HIP_DEVICE_COMPILE__
 }
 
+// ---- k10 v2: 256 x 128 tile, 8 waves, 3-stage LDS ring with one stage in flight across
+// the barrier ------------------------------------------------------------------------------
+//
+// The v1 loop above drains every DMA (vmcnt(0) + __syncthreads) once per 64-deep k-step, so
+// each step waits a full L2/HBM round trip that one k-step of MFMAs (512 cycles per wave)
+// cannot cover; v1 hides it only with a second co-resident block. v2 keeps the NEXT stage's
+// DMA in flight across the barrier instead (cdna_hip_programming.md "Pipelining across
+// barriers"): three 48 KB stages (144 KB LDS, 1 block / CU), a counted `s_waitcnt vmcnt(6)`
+// (6 = buffer_load...lds per thread per stage) and a raw s_barrier, so the loads of stage
+// k+2 are issued while stage k computes and stage k+1 is still landing. 8 waves as 4 (M) x 2
+// (N), each owning a 64 x 64 accumulator tile (16 x v_mfma_f32_16x16x32_bf16 per 32-k).
+// The (tap, channel block) cursor of the k loop is advanced in scalar registers (no
+// division per step), and each A row's validity for every filter tap is a precomputed
+// 32-bit tap mask (KH * KW <= 32), so staging a row costs a bit test, a select and an add.
+// Epilogue identical to v1 (bias + leaky, bf16 through LDS, 16-byte row stores) or fp32
+// split-K partials.
+template <bool HAS_BIAS>
+__global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v2(ConvArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  constexpr int BM = 256, BN = 128, kThreads = 512, NST = 3;
+  constexpr int NI = 4;                       // 16-wide n-fragments per wave (64 columns)
+  constexpr int kAbytes = BM * kRowBytes;     // 32 KB
+  constexpr int kBbytes = BN * kRowBytes;     // 16 KB
+  constexpr int kStage = kAbytes + kBbytes;   // 48 KB
+  constexpr int kRound = kThreads * 16;       // LDS bytes per DMA round (64 rows)
+  constexpr int kLoads = (BM + BN) / 64;      // DMA rounds (= glds per thread) per stage: 6
+  __shared__ __attribute__((aligned(16))) char smem[NST * kStage];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid / a.nNt, nt = bid - mt * a.nNt;
+  const int m0 = mt * BM, n0 = nt * BN;
+
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__hip_bfloat16*>(a.x), 0, a.xbytes, kBufCfg);
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__hip_bfloat16*>(a.w), 0, a.wbytes, kBufCfg);
+  const int lrow = tid >> 3;                 // 0..63
+  const int csw = (tid & 7) ^ (lrow & 7);    // swizzled source chunk (row & 7 == lrow & 7)
+  const int HoWo = a.Ho * a.Wo;
+  int a_off[4];
+  uint32_t a_tmask[4];  // bit (ky * KW + kx) set when that filter tap reads inside the image
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + lrow + 64 * i;
+    a_off[i] = 0;
+    a_tmask[i] = 0;
+    if (m < a.M) {
+      const int b = m / HoWo, r = m - b * HoWo;
+      const int oh = r / a.Wo, ow = r - oh * a.Wo;
+      const int ih0 = oh * a.sh - a.ph, iw0 = ow * a.sw - a.pw;
+      a_off[i] = (((b * a.H + ih0) * a.W + iw0) * a.Cin + csw * 8) * 2;
+      for (int ky = 0; ky < a.KH; ++ky) {
+        if ((unsigned)(ih0 + ky * a.dh) >= (unsigned)a.H) continue;
+        for (int kx = 0; kx < a.KW; ++kx)
+          if ((unsigned)(iw0 + kx * a.dw) < (unsigned)a.W) a_tmask[i] |= 1u << (ky * a.KW + kx);
+      }
+    }
+  }
+  const int wrow_bytes = a.nk * kBK * 2;  // = KH*KW*Cin*2
+  int b_off[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) b_off[i] = (n0 + lrow + 64 * i) * wrow_bytes + csw * 16;
+
+  // scalar k cursor of the NEXT stage to issue
+  const int ks0 = blockIdx.y * a.kps;
+  const int ks1 = min(a.nk, ks0 + a.kps);
+  int ctap = ks0 / a.cpt;
+  int cc = (ks0 - ctap * a.cpt) * kBK;         // channel offset within the tap
+  int cky = ctap / a.KW, ckx = ctap - cky * a.KW;
+  const int row_step = a.dh * a.W * a.Cin * 2;  // byte step of one filter row
+  const int col_step = a.dw * a.Cin * 2;        // byte step of one filter column
+  int ctoff = cky * row_step + ckx * col_step + cc * 2;
+  int cks = ks0;
+
+  auto issue = [&](int buf) {
+    char* As = smem + buf * kStage;
+    char* Bs = As + kAbytes;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool ok = (a_tmask[i] >> ctap) & 1u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          xrs, (lds_ptr_t)(As + i * kRound + wid * 1024), 16, ok ? a_off[i] + ctoff : kOobOffset,
+          0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)(Bs + i * kRound + wid * 1024),
+                                               16, b_off[i], cks * (kBK * 2), 0, 0);
+    // advance the cursor: next channel block, else next tap
+    ++cks;
+    cc += kBK;
+    ctoff += kBK * 2;
+    if (cc == a.Cin) {
+      cc = 0;
+      ++ctap;
+      if (++ckx == a.KW) {
+        ckx = 0;
+        ++cky;
+      }
+      ctoff = cky * row_step + ckx * col_step;
+    }
+  };
+
+  f32x4 acc[4][NI];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int frow = lane & 15, fsw = lane & 7, fk = lane >> 4;
+  const int nks = ks1 - ks0;
+  issue(0);
+  if (nks > 1) issue(1);
+  int rb = 0;  // ring slot of the stage being computed
+  for (int it = 0; it < nks; ++it) {
+    // this wave's DMA of stage `it` has landed; 6 newer glds (stage it+1) may still fly
+    if (it + 1 < nks)
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's stage-it DMA landed; slot (it-1)%3 is free
+    if (it + 2 < nks) issue(rb == 0 ? 2 : rb - 1);
+    const char* As = smem + rb * kStage;
+    const char* Bs = As + kAbytes;
+    bf16x8 af[2][4], bfr[2][NI];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int coff = ((kk * 4 + fk) ^ fsw) << 4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[kk][i] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + i * 16 + frow) * kRowBytes + coff);
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        bfr[kk][j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * 64 + j * 16 + frow) * kRowBytes + coff);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    rb = rb == 2 ? 0 : rb + 1;
+  }
+
+  if (a.part) {  // split-K: raw fp32 partials, bias/act/bf16 in conv_splitk_reduce
+    float* o = a.part + (size_t)blockIdx.y * a.M * a.Cout;
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+          if (m < a.M) o[(size_t)m * a.Cout + n0 + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+        }
+    return;
+  }
+
+  __syncthreads();  // every wave is done reading the ring: reuse it for the epilogue tile
+  char* E = smem;
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int cl = wn * 64 + j * 16 + (lane & 15);
+    const float bv = HAS_BIAS ? a.bias[n0 + cl] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rl = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        float v = acc[i][j][r] + bv;
+        v = v > 0.f ? v : v * a.slope;
+        *reinterpret_cast<__hip_bfloat16*>(E + rl * kEpiStride + cl * 2) = __float2bfloat16(v);
+      }
+    }
+  }
+  __syncthreads();
+  constexpr int kChunks = BN / 8;                 // 16
+  constexpr int kRowsPerPass = kThreads / kChunks;  // 32
+  const int ch = tid % kChunks, rr = tid / kChunks;
+#pragma unroll
+  for (int p = 0; p < BM / kRowsPerPass; ++p) {
+    const int rl = p * kRowsPerPass + rr;
+    const int m = m0 + rl;
+    if (m < a.M) {
+      const uint4 v = *reinterpret_cast<const uint4*>(E + rl * kEpiStride + ch * 16);
+      *reinterpret_cast<uint4*>(a.y + (size_t)m * a.Cout + n0 + ch * 8) = v;
+    }
+  }
+#endif  // __HIP_DEVICE_COMPILE__
+}
+
 // y = act(sum_s part[s] + bias) in bf16, 8 channels per thread.
 __global__ void __launch_bounds__(256)
 conv_splitk_reduce(const float* __restrict__ part, const float* __restrict__ bias,
@@ -322,20 +518,29 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
   a.nk = KH * KW * a.cpt;
   a.slope = (float)slope;
   const bool bn128 = Cout % 128 == 0;
+  // v1 by default: the v2 kernel (256 x 128 tile, 3-stage ring, 1 block / CU) measured
+  // 0.83-0.95x of v1 on every SPADE-step shape (profiles/conv_v2_probe_mi355x.txt) — two
+  // co-resident v1 blocks hide each other's barrier + LDS-read phases better than one deeper
+  // pipeline. IMAGINAIRE_AMD_CONV_V=2 selects v2 (Cout % 128 == 0, <= 32 taps) for probing.
+  int ver = 1;
+  if (const char* e = std::getenv("IMAGINAIRE_AMD_CONV_V")) ver = std::atoi(e);
+  const bool v2 = ver == 2 && bn128 && KH * KW <= 32;
   a.nNt = Cout / (bn128 ? 128 : 64);
   // BM = 128 by default (4 waves, 2 blocks/CU); BM = 256 (8 waves) measured no faster on the
   // SPADE shapes (profiles/conv_mfma_probe_mi355x.txt) and stays selectable for probing
-  int bm = 128;
+  int bm = v2 ? 256 : 128;
   if (const char* e = std::getenv("IMAGINAIRE_AMD_CONV_BM")) {
     const int v = std::atoi(e);
-    if (v == 128 || v == 256) bm = v;
+    if (!v2 && (v == 128 || v == 256)) bm = v;
   }
   const int64_t tiles = (int64_t)ceil_div(a.M, bm) * a.nNt;
   IAMD_CHECK(tiles < (1ll << 31), "conv2d_mfma: grid too large");
-  // split-K over (tap, channel-block) k-steps when the tile grid cannot fill 256 CUs twice
-  // (wide-K / narrow-N data gradients of the SPADE gamma/beta convs at 16x32 .. 64x128)
+  // split-K over (tap, channel-block) k-steps when the tile grid cannot fill the chip (v1: 2
+  // blocks per CU, v2: 1) — the wide-K / narrow-N data gradients of the SPADE gamma/beta
+  // convs at 16x32 .. 64x128 and the 2048-channel head convs
+  const int64_t slots = v2 ? 256 : 512;
   int S = 1;
-  if (tiles < 512 && a.nk >= 16) S = (int)std::min<int64_t>((512 + tiles - 1) / tiles, a.nk / 8);
+  if (tiles < slots && a.nk >= 16) S = (int)std::min<int64_t>((slots + tiles - 1) / tiles, a.nk / 8);
   if (const char* e = std::getenv("IMAGINAIRE_AMD_CONV_SPLITK")) S = std::max(1, std::atoi(e));
   S = std::max(1, std::min(S, a.nk));
   a.kps = ceil_div(a.nk, S);
@@ -374,8 +579,14 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
     if (a.bias) by_bn(bmv, std::true_type());
     else by_bn(bmv, std::false_type());
   };
-  if (bm == 256) by_bias(std::integral_constant<int, 256>());
-  else by_bias(std::integral_constant<int, 128>());
+  if (v2) {
+    if (a.bias) hipLaunchKernelGGL((conv_fwd_mfma_v2<true>), grid, dim3(512), 0, stream(), a);
+    else hipLaunchKernelGGL((conv_fwd_mfma_v2<false>), grid, dim3(512), 0, stream(), a);
+  } else if (bm == 256) {
+    by_bias(std::integral_constant<int, 256>());
+  } else {
+    by_bias(std::integral_constant<int, 128>());
+  }
   if (S > 1) {
     IAMD_LAUNCH_CHECK();
     const int64_t MC = (int64_t)a.M * Cout;

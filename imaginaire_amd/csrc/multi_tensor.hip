@@ -44,6 +44,86 @@ struct Table {
 std::mutex g_mu;
 std::unordered_map<uint64_t, Table> g_cache;
 
+}  // namespace
+
+// ---- host -> device table staging that is safe under hipGraph capture -----------------------
+// Outside a capture: pinned staging + async copy on the current stream (never blocks the
+// host). During a capture no copy may be enqueued (a pageable/pinned H2D node would re-read a
+// host buffer that is gone by replay time), so the device buffer is allocated (from the
+// graph's private pool) and the upload is DEFERRED: flush_deferred_uploads() copies it
+// synchronously after the capture has ended, before the first replay. Buffers created during
+// a capture are also kept alive for the life of the process, so a later cache eviction can
+// never free memory a graph still reads.
+namespace {
+struct Deferred {
+  at::Tensor dst;
+  std::vector<uint8_t> bytes;
+};
+std::mutex g_def_mu;
+std::vector<Deferred> g_deferred;
+std::vector<at::Tensor> g_graph_keep;
+// Tables made during a capture are carved from a persistent arena allocated OUTSIDE any
+// capture (regular caching-allocator memory): graph-pool memory allocated inside a capture
+// belongs to the graph's own allocation nodes and need not hold host-written bytes at
+// replay time.
+constexpr int64_t kArenaBytes = 64ll << 20;
+std::unordered_map<int, std::pair<at::Tensor, int64_t>> g_arena;
+
+void ensure_arena(const at::Device& dev) {
+  auto& a = g_arena[dev.index()];
+  if (!a.first.defined())
+    a = {at::empty({kArenaBytes}, at::TensorOptions().dtype(at::kByte).device(dev)), 0};
+}
+}  // namespace
+
+bool stream_capturing() {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  IAMD_HIP_CHECK(hipStreamIsCapturing(stream(), &st));
+  return st != hipStreamCaptureStatusNone;
+}
+
+at::Tensor stage_to_device(const void* src, size_t bytes, const at::Device& dev) {
+  const int64_t n = (int64_t)std::max<size_t>(bytes, 1);
+  if (stream_capturing()) {
+    std::lock_guard<std::mutex> lk(g_def_mu);
+    auto it = g_arena.find(dev.index());
+    IAMD_CHECK(it != g_arena.end() && it->second.first.defined(),
+               "no table arena: run the step once eagerly before capturing it");
+    const int64_t off = (it->second.second + 255) / 256 * 256;
+    IAMD_CHECK(off + n <= kArenaBytes, "capture table arena exhausted");
+    auto d = it->second.first.narrow(0, off, n);
+    it->second.second = off + n;
+    Deferred df;
+    df.dst = d;
+    df.bytes.assign(reinterpret_cast<const uint8_t*>(src),
+                    reinterpret_cast<const uint8_t*>(src) + bytes);
+    g_deferred.push_back(std::move(df));
+    g_graph_keep.push_back(d);
+    return d;
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_def_mu);
+    ensure_arena(dev);  // reserved at the first eager use, ready for a later capture
+  }
+  auto pin = at::TensorOptions().dtype(at::kByte).pinned_memory(true);
+  auto h = at::empty({n}, pin);
+  if (bytes) memcpy(h.data_ptr(), src, bytes);
+  return h.to(dev, /*non_blocking=*/true);
+}
+
+int64_t flush_deferred_uploads() {
+  std::lock_guard<std::mutex> lk(g_def_mu);
+  const int64_t n = (int64_t)g_deferred.size();
+  for (auto& d : g_deferred)
+    if (!d.bytes.empty())
+      IAMD_HIP_CHECK(hipMemcpy(d.dst.data_ptr(), d.bytes.data(), d.bytes.size(),
+                               hipMemcpyHostToDevice));
+  g_deferred.clear();
+  return n;
+}
+
+namespace {
+
 uint64_t mix(uint64_t h, uint64_t v) {
   h ^= v + 0x9e3779b97f4a7c15ULL + (h << 6) + (h >> 2);
   return h;
@@ -83,27 +163,35 @@ Table& get_table(const std::vector<std::vector<at::Tensor>>& lists, const at::De
       bm.push_back((int32_t)c);
     }
   }
-  // pinned staging + async copy on the current stream: a cache miss never
-  // blocks the host (the caching host allocator keeps the staging alive).
-  auto pin = at::TensorOptions().dtype(at::kByte).pinned_memory(true);
-  auto cpu_e = at::empty({(int64_t)(T * sizeof(TensorEntry))}, pin);
-  memcpy(cpu_e.data_ptr(), ents.data(), T * sizeof(TensorEntry));
-  auto cpu_b = at::empty({(int64_t)(bm.size() * sizeof(int32_t))}, pin);
-  memcpy(cpu_b.data_ptr(), bm.data(), bm.size() * sizeof(int32_t));
+  // pinned staging + async copy on the current stream (deferred under graph capture)
   Table t;
-  t.entries = cpu_e.to(dev, /*non_blocking=*/true);
-  t.blocks = cpu_b.to(dev, /*non_blocking=*/true).view(at::kInt);
+  t.entries = stage_to_device(ents.data(), T * sizeof(TensorEntry), dev);
+  t.blocks = stage_to_device(bm.data(), bm.size() * sizeof(int32_t), dev).view(at::kInt);
   t.nblocks = (int)(bm.size() / 2);
   if (g_cache.size() > 256) g_cache.clear();
   auto res = g_cache.emplace(h, std::move(t));
   return res.first->second;
 }
 
+// Device-resident Adam hyper-parameters [lr, step, step_size, rsqrt(bc2)] (capturable
+// optimizer step: the step count and the bias corrections live on the device, so a replayed
+// hipGraph advances them instead of baking the capture-time values).
+__global__ void adam_hyper_step(float* __restrict__ hyper, float beta1, float beta2) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const float step = hyper[1] + 1.f;
+    hyper[1] = step;
+    const float bc1 = 1.f - powf(beta1, step);
+    const float bc2 = 1.f - powf(beta2, step);
+    hyper[2] = hyper[0] / bc1;
+    hyper[3] = rsqrtf(bc2);
+  }
+}
+
 template <typename G>
 __global__ void __launch_bounds__(kThreads)
 adam_kernel(const TensorEntry* __restrict__ ents, const int* __restrict__ blocks, float lr,
             float beta1, float beta2, float eps, float bc1, float bc2, float wd, int adamw,
-            float grad_scale) {
+            float grad_scale, const float* __restrict__ hyper) {
   const int b = blockIdx.x;
   const int t = blocks[2 * b], chunk = blocks[2 * b + 1];
   const TensorEntry e = ents[t];
@@ -114,8 +202,15 @@ adam_kernel(const TensorEntry* __restrict__ ents, const int* __restrict__ blocks
   __hip_bfloat16* __restrict__ shadow = reinterpret_cast<__hip_bfloat16*>(e.p[4]);
   const int64_t start = (int64_t)chunk * kChunk;
   const int64_t end = min(e.numel, start + (int64_t)kChunk);
-  const float step_size = lr / bc1;
-  const float rbc2 = rsqrtf(bc2);
+  float step_size, rbc2;
+  if (hyper) {
+    lr = hyper[0];
+    step_size = hyper[2];
+    rbc2 = hyper[3];
+  } else {
+    step_size = lr / bc1;
+    rbc2 = rsqrtf(bc2);
+  }
   const bool vec_ok = (((uintptr_t)p | (uintptr_t)m | (uintptr_t)v) % 16 == 0) &&
                       ((uintptr_t)g % (4 * sizeof(G)) == 0) && (start % 4 == 0);
   if (vec_ok) {
@@ -226,10 +321,14 @@ sn_vperm(const TensorEntry* __restrict__ ents) {
 template <typename T>
 __global__ void __launch_bounds__(kThreads)
 ema_kernel(const TensorEntry* __restrict__ ents, const int* __restrict__ blocks, float beta,
-           const float* __restrict__ inv_scale) {
+           const float* __restrict__ inv_scale, const int64_t* __restrict__ count,
+           int64_t warm_until) {
   const int b = blockIdx.x;
   const int t = blocks[2 * b], chunk = blocks[2 * b + 1];
   const TensorEntry e = ents[t];
+  // device-side warm-up switch (model_average.py: beta = 0 until start_iteration), so a
+  // replayed hipGraph turns the average on at the right iteration
+  if (count && *count <= warm_until) beta = 0.f;
   T* __restrict__ dst = reinterpret_cast<T*>(e.p[0]);
   const T* __restrict__ src = reinterpret_cast<const T*>(e.p[1]);
   const float sc = inv_scale ? 1.f / inv_scale[t] : 1.f;
@@ -292,8 +391,16 @@ void check_same_dtype(const std::vector<at::Tensor>& l, at::ScalarType st, const
 void mt_adam(const std::vector<at::Tensor>& params, const std::vector<at::Tensor>& grads,
              const std::vector<at::Tensor>& exp_avgs, const std::vector<at::Tensor>& exp_avg_sqs,
              const std::vector<at::Tensor>& shadows, double lr, double beta1, double beta2,
-             double eps, int64_t step, double weight_decay, bool adamw, double grad_scale) {
+             double eps, int64_t step, double weight_decay, bool adamw, double grad_scale,
+             const c10::optional<at::Tensor>& hyper) {
   if (params.empty()) return;
+  float* hp = nullptr;
+  if (hyper.has_value() && hyper->defined()) {
+    IAMD_CHECK(hyper->is_cuda() && hyper->scalar_type() == at::kFloat && hyper->numel() == 4 &&
+                   hyper->is_contiguous(),
+               "mt_adam: hyper must be a contiguous fp32 device tensor [lr, step, ., .]");
+    hp = hyper->data_ptr<float>();
+  }
   IAMD_CHECK(params.size() == grads.size() && params.size() == exp_avgs.size() &&
                  params.size() == exp_avg_sqs.size(),
              "mt_adam: list sizes differ");
@@ -313,14 +420,17 @@ void mt_adam(const std::vector<at::Tensor>& params, const std::vector<at::Tensor
   const float bc2 = 1.f - (float)std::pow(beta2, (double)step);
   auto ents = reinterpret_cast<const TensorEntry*>(tb.entries.data_ptr());
   auto blks = tb.blocks.data_ptr<int>();
+  if (hp)
+    hipLaunchKernelGGL(adam_hyper_step, dim3(1), dim3(64), 0, stream(), hp, (float)beta1,
+                       (float)beta2);
   if (gdt == at::kFloat)
     hipLaunchKernelGGL((adam_kernel<float>), dim3(tb.nblocks), dim3(kThreads), 0, stream(), ents,
                        blks, (float)lr, (float)beta1, (float)beta2, (float)eps, bc1, bc2,
-                       (float)weight_decay, adamw ? 1 : 0, (float)grad_scale);
+                       (float)weight_decay, adamw ? 1 : 0, (float)grad_scale, hp);
   else if (gdt == at::kBFloat16)
     hipLaunchKernelGGL((adam_kernel<__hip_bfloat16>), dim3(tb.nblocks), dim3(kThreads), 0,
                        stream(), ents, blks, (float)lr, (float)beta1, (float)beta2, (float)eps,
-                       bc1, bc2, (float)weight_decay, adamw ? 1 : 0, (float)grad_scale);
+                       bc1, bc2, (float)weight_decay, adamw ? 1 : 0, (float)grad_scale, hp);
   else
     IAMD_CHECK(false, "mt_adam: grads must be fp32 or bf16");
   IAMD_LAUNCH_CHECK();
@@ -362,8 +472,15 @@ at::Tensor mt_sn_sigma(const std::vector<at::Tensor>& weights, const std::vector
 }
 
 void mt_ema(const std::vector<at::Tensor>& targets, const std::vector<at::Tensor>& sources,
-            double beta, const c10::optional<at::Tensor>& sigma) {
+            double beta, const c10::optional<at::Tensor>& sigma,
+            const c10::optional<at::Tensor>& count, int64_t start) {
   if (targets.empty()) return;
+  const int64_t* cp = nullptr;
+  if (count.has_value() && count->defined()) {
+    IAMD_CHECK(count->is_cuda() && count->scalar_type() == at::kLong && count->numel() == 1,
+               "mt_ema: count must be a 1-element int64 device tensor");
+    cp = count->data_ptr<int64_t>();
+  }
   const auto dt = targets[0].scalar_type();
   check_same_dtype(targets, dt, "mt_ema targets");
   check_same_dtype(sources, dt, "mt_ema sources");
@@ -377,7 +494,7 @@ void mt_ema(const std::vector<at::Tensor>& targets, const std::vector<at::Tensor
   IAMD_DISPATCH_FLOAT_TYPES(dt, "mt_ema", [&] {
     hipLaunchKernelGGL((ema_kernel<scalar_t>), dim3(tb.nblocks), dim3(kThreads), 0, stream(),
                        reinterpret_cast<const TensorEntry*>(tb.entries.data_ptr()),
-                       tb.blocks.data_ptr<int>(), (float)beta, sp);
+                       tb.blocks.data_ptr<int>(), (float)beta, sp, cp, start);
   });
   IAMD_LAUNCH_CHECK();
 }

@@ -217,13 +217,8 @@ SnPlan& get_plan(const std::vector<at::Tensor>& W, const std::vector<at::Tensor>
       rb.push_back((int32_t)r);
     }
   }
-  auto pin = at::TensorOptions().dtype(at::kByte).pinned_memory(true);
   auto dev = W[0].device();
-  auto stage = [&](const void* src, size_t bytes) {
-    auto h = at::empty({(int64_t)bytes}, pin);
-    memcpy(h.data_ptr(), src, bytes);
-    return h.to(dev, /*non_blocking=*/true);
-  };
+  auto stage = [&](const void* src, size_t bytes) { return stage_to_device(src, bytes, dev); };
   p.ents = stage(ents.data(), ents.size() * sizeof(SnEntry));
   p.col_blocks = stage(cb.data(), cb.size() * sizeof(int32_t)).view(at::kInt);
   p.row_blocks = stage(rb.data(), rb.size() * sizeof(int32_t)).view(at::kInt);
@@ -328,14 +323,9 @@ ScPlan& get_sc_plan(const std::vector<at::Tensor>& W) {
     off += (W[i].numel() + 7) / 8 * 8;  // 16-byte aligned views
   }
   p.total = off;
-  auto pin = at::TensorOptions().dtype(at::kByte).pinned_memory(true);
   auto dev = W[0].device();
-  auto he = at::empty({(int64_t)(ents.size() * sizeof(ScEntry))}, pin);
-  memcpy(he.data_ptr(), ents.data(), ents.size() * sizeof(ScEntry));
-  auto hb = at::empty({(int64_t)(bm.size() * sizeof(int32_t))}, pin);
-  memcpy(hb.data_ptr(), bm.data(), bm.size() * sizeof(int32_t));
-  p.ents = he.to(dev, true);
-  p.blocks = hb.to(dev, true).view(at::kInt);
+  p.ents = stage_to_device(ents.data(), ents.size() * sizeof(ScEntry), dev);
+  p.blocks = stage_to_device(bm.data(), bm.size() * sizeof(int32_t), dev).view(at::kInt);
   p.nblocks = (int)(bm.size() / 2);
   if (g_sc_cache.size() > 64) g_sc_cache.clear();
   return g_sc_cache.emplace(h, std::move(p)).first->second;

@@ -33,6 +33,56 @@ class FusedAdam(Optimizer):
     def zero_grad(self, set_to_none=True):
         super().zero_grad(set_to_none=set_to_none)
 
+    # -- capturable (hipGraph) support ------------------------------------------------
+    # On the native path every group carries a device tensor [lr, step, lr/bc1, 1/sqrt(bc2)]
+    # that the k4 launch advances itself (one 1-thread kernel ahead of the update), so the
+    # same step can be captured into a hipGraph and replayed: the bias corrections move on
+    # with every replay. group['step'] stays the host mirror (checkpoint format).
+    def _hyper(self, group, device, step_before):
+        h = group.get('_hyper')
+        if h is None or h.device != device:
+            h = torch.tensor([float(group['lr']), float(step_before), 0.0, 0.0],
+                             dtype=torch.float32, device=device)
+            group['_hyper'] = h
+            group['_hyper_lr'] = float(group['lr'])
+        return h
+
+    def sync_hyper(self):
+        """Push a changed learning rate (LR scheduler) into the device hyper-parameters.
+        Call outside any capture — e.g. before replaying a captured step."""
+        for group in self.param_groups:
+            h = group.get('_hyper')
+            lr = float(group['lr'])
+            if h is not None and group.get('_hyper_lr') != lr:
+                h[0:1].fill_(lr)
+                group['_hyper_lr'] = lr
+
+    def advance_host_step(self, n=1):
+        """Host mirror of ``n`` replayed steps (the device counter advanced in the graph)."""
+        for group in self.param_groups:
+            if '_hyper' in group:
+                group['step'] += n
+
+    def state_dict(self):
+        sd = super().state_dict()
+        for g in sd['param_groups']:
+            g.pop('_hyper', None)
+            g.pop('_hyper_lr', None)
+        return sd
+
+    def load_state_dict(self, state_dict):
+        hypers = [g.get('_hyper') for g in self.param_groups]
+        super().load_state_dict(state_dict)
+        for g, h in zip(self.param_groups, hypers):
+            # refresh the device counters IN PLACE: a captured step keeps its pointer
+            if h is not None:
+                h.copy_(torch.tensor([float(g['lr']), float(g.get('step', 0)), 0.0, 0.0]))
+                g['_hyper'] = h
+                g['_hyper_lr'] = float(g['lr'])
+            else:
+                g.pop('_hyper', None)
+                g.pop('_hyper_lr', None)
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
@@ -68,6 +118,12 @@ class FusedAdam(Optimizer):
             native = _ext.use_native(params[0]) and all(
                 p.dtype == torch.float32 and _ext.is_dense(p) for p in params)
             if native:
+                # device counter created at the pre-increment step: the launch advances it
+                hyper = self._hyper(group, params[0].device, step - 1)
+                if not torch.cuda.is_current_stream_capturing() and \
+                        group.get('_hyper_lr') != float(lr):
+                    hyper[0:1].fill_(float(lr))
+                    group['_hyper_lr'] = float(lr)
                 gdt = grads[0].dtype
                 if gdt not in (torch.float32, torch.bfloat16):
                     gdt = torch.float32
@@ -77,7 +133,7 @@ class FusedAdam(Optimizer):
                       else torch.empty_like(p, dtype=gdt).copy_(g)
                       for g, p in zip(grads, params)]
                 _ext.ext().mt_adam(params, gl, m, v, [], lr, beta1, beta2, eps, int(step), wd,
-                                   bool(adamw), 1.0)
+                                   bool(adamw), 1.0, hyper)
             else:
                 _reference_adam(params, grads, m, v, lr, beta1, beta2, eps, step, wd, adamw)
         return loss

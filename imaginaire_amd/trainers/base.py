@@ -94,7 +94,10 @@ class BaseTrainer(object):
     def autocast(self):
         if self.amp_dtype is None:
             return contextlib.nullcontext()
-        return torch.autocast(device_type='cuda', dtype=self.amp_dtype)
+        # no autocast weight-cast cache inside a hipGraph capture (cached casts would be
+        # graph-pool tensors outliving the region that produced them)
+        return torch.autocast(device_type='cuda', dtype=self.amp_dtype,
+                              cache_enabled=not torch.cuda.is_current_stream_capturing())
 
     def _reset_speed_accumulators(self):
         for k in ('gen_forw', 'gen_loss', 'gen_back', 'gen_step', 'gen_avg', 'dis_forw',

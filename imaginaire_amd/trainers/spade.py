@@ -23,6 +23,10 @@ from imaginaire_amd.utils.visualization import tensor2label
 
 
 class Trainer(BaseTrainer):
+    # the D -> G -> EMA iteration is device-only with fixed shapes: hipGraph-capturable
+    # (utils/cuda_graph.py)
+    graph_capturable = True
+
     def __init__(self, cfg, net_G, net_D, opt_G, opt_D, sch_G, sch_D, train_data_loader,
                  val_data_loader):
         super().__init__(cfg, net_G, net_D, opt_G, opt_D, sch_G, sch_D, train_data_loader,

@@ -1,0 +1,231 @@
+"""hipGraph capture of a trainer's steady-state iteration (D update -> G update -> EMA).
+
+The reference runs every iteration eagerly (trainers/base.py:594-666, apex AMP): ~1,450
+kernel launches per SPADE step issued one by one from Python. On MI355X the whole
+iteration is captured ONCE into a hipGraph (``torch.cuda.graph``) and replayed:
+
+* inputs are copied into static device buffers before each replay;
+* everything the step changes between iterations lives on the device: the Adam step
+  counter / bias corrections / learning rate (FusedAdam's device hyper-parameters), the
+  EMA warm-up switch (``num_updates_tracked``), BatchNorm running statistics, spectral-norm
+  u/v vectors, the philox RNG offsets of the style-encoder noise;
+* host-side mirrors (optimizer ``group['step']``, ``ModelAverage._host_updates``) are
+  advanced after each replay, and a changed learning rate is pushed to the device
+  (``FusedAdam.sync_hyper``) before it;
+* device tables that the multi-tensor kernels build on first use are uploaded after the
+  capture (``flush_deferred_uploads``), never as copy nodes inside the graph.
+
+Single-process only by default: with ``world_size > 1`` the step contains RCCL
+collectives (DDP buckets, SyncBN) and host-side bucket bookkeeping, so the trainer keeps
+the eager path there (``IMAGINAIRE_AMD_GRAPH=force`` overrides).
+"""
+import os
+import time
+
+import torch
+
+from imaginaire_amd.utils.distributed import get_world_size
+from imaginaire_amd.utils.distributed import master_only_print as print
+
+
+def graph_mode_default():
+    """'1' (default: on for world size 1), '0' (off) or 'force' (also with world > 1)."""
+    return os.environ.get('IMAGINAIRE_AMD_GRAPH', '1')
+
+
+def graph_supported(trainer):
+    mode = graph_mode_default()
+    if mode == '0' or trainer.device.type != 'cuda':
+        return False
+    if getattr(trainer.cfg, 'speed_benchmark', False):
+        return False  # per-phase host timers synchronise inside the step
+    if getattr(trainer.cfg.trainer, 'skip_nonfinite_steps', False):
+        return False  # host-side decision per step
+    if get_world_size() > 1 and mode != 'force':
+        return False
+    return True
+
+
+def _static_copy(dst, src):
+    if torch.is_tensor(dst):
+        dst.copy_(src, non_blocking=True)
+    elif isinstance(dst, dict):
+        for k in dst:
+            _static_copy(dst[k], src[k])
+    elif isinstance(dst, (list, tuple)):
+        for d, s in zip(dst, src):
+            _static_copy(d, s)
+
+
+def _clone(x):
+    if torch.is_tensor(x):
+        return x.clone()
+    if isinstance(x, dict):
+        return {k: _clone(v) for k, v in x.items()}
+    if isinstance(x, list):
+        return [_clone(v) for v in x]
+    if isinstance(x, tuple):
+        return tuple(_clone(v) for v in x)
+    return x
+
+
+def _same_structure(a, b):
+    if torch.is_tensor(a):
+        return torch.is_tensor(b) and a.shape == b.shape and a.dtype == b.dtype and \
+            a.stride() == b.stride()
+    if isinstance(a, dict):
+        return isinstance(b, dict) and a.keys() == b.keys() and \
+            all(_same_structure(a[k], b[k]) for k in a)
+    if isinstance(a, (list, tuple)):
+        return isinstance(b, (list, tuple)) and len(a) == len(b) and \
+            all(_same_structure(x, y) for x, y in zip(a, b))
+    return a == b
+
+
+class GraphedStep(object):
+    """Runs ``step_fn(data)`` eagerly for ``warmup`` iterations (on a side stream, as
+    stream capture requires), then captures it and replays the graph from then on.
+
+    ``step_fn`` must be the steady-state iteration: no host synchronisation, fixed shapes.
+    ``pre_replay`` / ``post_replay`` are host hooks run around every replay.
+    """
+
+    def __init__(self, step_fn, warmup=3, pre_replay=None, post_replay=None, name='step',
+                 save_host=None, restore_host=None):
+        self.step_fn = step_fn
+        self.warmup = warmup
+        self.pre_replay = pre_replay
+        self.post_replay = post_replay
+        # host-side counters the captured (not executed) iteration advanced: rolled back
+        self.save_host = save_host
+        self.restore_host = restore_host
+        self.name = name
+        self.graph = None
+        self.static = None
+        self.n_eager = 0
+        self.failed = False
+        self.capture_s = None
+        self.stream = None
+
+    def __call__(self, data):
+        if self.failed:
+            return self.step_fn(data)
+        if self.graph is not None:
+            if not _same_structure(self.static, data):
+                # e.g. a ragged last batch: run it eagerly, keep the graph
+                return self.step_fn(data)
+            _static_copy(self.static, data)
+            if self.pre_replay:
+                self.pre_replay()
+            self.graph.replay()
+            if self.post_replay:
+                self.post_replay()
+            return None
+        if self.n_eager < self.warmup:
+            # warm up on the stream the capture will use: autograd's AccumulateGrad nodes
+            # remember the stream they were created on
+            if self.stream is None:
+                self.stream = torch.cuda.Stream()
+            self.stream.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self.stream):
+                self.step_fn(data)
+            torch.cuda.current_stream().wait_stream(self.stream)
+            self.n_eager += 1
+            return None
+        return self._capture_and_run(data)
+
+    def _capture_and_run(self, data):
+        from imaginaire_amd.ops import _ext
+        torch.cuda.synchronize()
+        t0 = time.time()
+        # private copies: the batch source may hand out views of its own pool
+        self.static = _clone(data)
+        saved = self.save_host() if self.save_host else None
+        g = torch.cuda.CUDAGraph()
+        try:
+            if self.stream is None:
+                self.stream = torch.cuda.Stream()
+            with torch.cuda.graph(g, stream=self.stream):
+                self.step_fn(self.static)
+        except Exception as e:  # noqa: BLE001 - any capture failure: stay eager
+            if os.environ.get('IMAGINAIRE_AMD_GRAPH_DEBUG'):
+                raise
+            print('[graph] capture of {} failed ({}: {}); running eagerly'.format(
+                self.name, type(e).__name__, str(e).splitlines()[0][:200]))
+            self.failed = True
+            self.static = None
+            if self.restore_host:
+                self.restore_host(saved)
+            torch.cuda.synchronize()
+            return self.step_fn(data)
+        if self.restore_host:
+            self.restore_host(saved)
+        if _ext.available():
+            _ext.ext().flush_deferred_uploads()
+        torch.cuda.synchronize()
+        self.graph = g
+        self.capture_s = time.time() - t0
+        print('[graph] captured {} in {:.1f} s'.format(self.name, self.capture_s))
+        # the capture itself executed nothing: run this iteration as the first replay
+        if self.pre_replay:
+            self.pre_replay()
+        g.replay()
+        if self.post_replay:
+            self.post_replay()
+        return None
+
+
+def make_trainer_step(trainer, warmup=None, enabled=True):
+    """The steady-state iteration of an image trainer: ``dis_step`` D updates then
+    ``gen_step`` G updates (reference train.py:72-84), as a GraphedStep when supported
+    (``trainer.graph_capturable`` and :func:`graph_supported`). Returns (callable, graph or
+    None)."""
+    cfg = trainer.cfg
+    if warmup is None:
+        warmup = int(os.environ.get('IMAGINAIRE_AMD_GRAPH_WARMUP', '3'))
+
+    def step(data):
+        for _ in range(cfg.trainer.dis_step):
+            trainer.dis_update(data)
+        for _ in range(cfg.trainer.gen_step):
+            trainer.gen_update(data)
+
+    if not (enabled and getattr(trainer, 'graph_capturable', False) and
+            graph_supported(trainer)):
+        return step, None
+
+    opts = [o for o in (trainer.opt_G, trainer.opt_D) if o is not None]
+    n_updates = {id(trainer.opt_D): cfg.trainer.dis_step, id(trainer.opt_G): cfg.trainer.gen_step}
+
+    def pre():
+        for o in opts:
+            if hasattr(o, 'sync_hyper'):
+                o.sync_hyper()
+
+    def post():
+        for o in opts:
+            if hasattr(o, 'advance_host_step'):
+                o.advance_host_step(n_updates.get(id(o), 1))
+        if cfg.trainer.model_average:
+            ma = trainer.net_G.module
+            if hasattr(ma, '_host_updates'):
+                ma._host_updates += cfg.trainer.gen_step
+
+    def save_host():
+        ma = trainer.net_G.module if cfg.trainer.model_average else None
+        return ([[g.get('step') for g in o.param_groups] for o in opts],
+                getattr(ma, '_host_updates', None))
+
+    def restore_host(saved):
+        steps, host_updates = saved
+        for o, st in zip(opts, steps):
+            for g, v in zip(o.param_groups, st):
+                if v is not None:
+                    g['step'] = v
+        if host_updates is not None:
+            trainer.net_G.module._host_updates = host_updates
+
+    gs = GraphedStep(step, warmup=warmup, pre_replay=pre, post_replay=post,
+                     name=type(trainer).__module__, save_host=save_host,
+                     restore_host=restore_host)
+    return gs, gs

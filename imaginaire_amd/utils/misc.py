@@ -121,6 +121,7 @@ def truncated_gaussian(threshold, size, seed=None, device=None):
 
 _IMNET_MEAN = (0.485, 0.456, 0.406, 0.5)
 _IMNET_STD = (0.229, 0.224, 0.225, 0.225)
+_IMNET_CACHE = {}
 
 
 def apply_imagenet_normalization(input):
@@ -130,7 +131,15 @@ def apply_imagenet_normalization(input):
     uses 3. Here the statistics are sliced to the input's channel count.
     """
     c = input.shape[1]
-    normalized_input = (input + 1) / 2
-    mean = normalized_input.new_tensor(_IMNET_MEAN[:c]).view(1, c, 1, 1)
-    std = normalized_input.new_tensor(_IMNET_STD[:c]).view(1, c, 1, 1)
-    return (normalized_input - mean) / std
+    # ((x + 1) / 2 - mean) / std == x * (0.5 / std) + (0.5 - mean) / std: one fused
+    # multiply-add with per-channel constants cached per (device, dtype) — created on
+    # first use, so the op is also legal inside a hipGraph capture (no H2D copy there)
+    key = (input.device, input.dtype, c)
+    sc = _IMNET_CACHE.get(key)
+    if sc is None:
+        mean = torch.tensor(_IMNET_MEAN[:c], dtype=torch.float64)
+        std = torch.tensor(_IMNET_STD[:c], dtype=torch.float64)
+        scale = (0.5 / std).view(1, c, 1, 1).to(input.device, input.dtype)
+        shift = ((0.5 - mean) / std).view(1, c, 1, 1).to(input.device, input.dtype)
+        sc = _IMNET_CACHE[key] = (scale, shift)
+    return torch.addcmul(sc[1], input, sc[0])

@@ -131,11 +131,14 @@ class ModelAverage(nn.Module):
             (len(sn_t) == 0 and plain and _ext.use_native(next(iter(plain.values()))[0][0]))
         if native:
             ext = _ext.ext()
+            # the warm-up switch (beta = 0 until start_iteration) is evaluated on the device
+            # from num_updates_tracked, so a captured step replays it correctly
+            cnt, start = self.num_updates_tracked, int(self.start_iteration)
             if sn_t:
                 sigma = ext.mt_sn_sigma(sn_w, sn_u, sn_v)
-                ext.mt_ema(sn_t, sn_w, beta, sigma)
+                ext.mt_ema(sn_t, sn_w, self.beta, sigma, cnt, start)
             for dt, (ts, ss) in plain.items():
-                ext.mt_ema(ts, ss, beta, None)
+                ext.mt_ema(ts, ss, self.beta, None, cnt, start)
         else:
             for t, w, u, v in zip(sn_t, sn_w, sn_u, sn_v):
                 t.copy_(t * beta + self.sn_compute_weight(w, u, v) * (1 - beta))

@@ -36,6 +36,8 @@ def parse_args(argv=None):
     parser.add_argument('--single_gpu', action='store_true')
     parser.add_argument('--num_workers', type=int)
     parser.add_argument('--backend', default=None, help='nccl (RCCL) / gloo; default auto')
+    parser.add_argument('--no_graph', '--no-graph', action='store_true',
+                        help='run every iteration eagerly (no hipGraph replay)')
     return parser.parse_args(argv)
 
 
@@ -59,6 +61,10 @@ def main(argv=None):
     trainer = get_trainer(cfg, net_G, net_D, opt_G, opt_D, sch_G, sch_D, train_data_loader,
                           val_data_loader)
     current_epoch, current_iteration = trainer.load_checkpoint(cfg, args.checkpoint)
+    # the D -> G iteration; replayed from a hipGraph after a few eager iterations when the
+    # trainer supports it (single process, see imaginaire_amd/utils/cuda_graph.py)
+    from imaginaire_amd.utils.cuda_graph import make_trainer_step
+    train_step, _ = make_trainer_step(trainer, enabled=not args.no_graph)
     for epoch in range(current_epoch, cfg.max_epoch):
         print('Epoch {} ...'.format(epoch))
         if hasattr(train_data_loader.sampler, 'set_epoch'):
@@ -66,10 +72,7 @@ def main(argv=None):
         trainer.start_of_epoch(current_epoch)
         for it, data in enumerate(train_data_loader):
             data = trainer.start_of_iteration(data, current_iteration)
-            for _ in range(cfg.trainer.dis_step):
-                trainer.dis_update(data)
-            for _ in range(cfg.trainer.gen_step):
-                trainer.gen_update(data)
+            train_step(data)
             current_iteration += 1
             trainer.end_of_iteration(data, current_epoch, current_iteration)
             if current_iteration >= cfg.max_iter:
