@@ -443,6 +443,261 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v2(ConvArgs a) {
 #endif  // __HIP_DEVICE_COMPILE__
 }
 
+// ---- k10 v3: 256 x 256 (or 512 x 128) tile, 8 waves of 128 x 64, 8-phase half-tile schedule -
+//
+// Structure after the 256x256 "8-phase" GEMM of cdna_hip_programming.md §5 (T1-T5), adapted to
+// the implicit-GEMM A operand. Each wave (2 (M) x 4 (N) grid) owns a 128 x 64 accumulator
+// tile = 4 quadrants of 64 x 32; one K-tile (64 deep) is computed in 4 phases, one quadrant
+// (16 v_mfma_f32_16x16x32_bf16) per phase, in the order (0,0) (0,1) (1,1) (1,0) so that each
+// phase changes only the A or only the B half of the operands. Per phase, behind ONE barrier:
+//   * one HALF-tile of the next K-tile (128 rows x 64 k = 2 buffer_load ... lds per thread) is
+//     issued into the other LDS buffer — four half-tiles per K-tile, each issued 2-3 phases
+//     before its first read, retired by a counted `s_waitcnt vmcnt(2|4)` (never 0 in the loop);
+//   * the fragments the NEXT phase needs are read from LDS into a second register set while
+//     this phase's 16 MFMAs run on the set read one phase earlier (so the MFMAs never wait on
+//     a ds_read issued in their own phase);
+//   * the fragment register sets rotate with a period of two K-tiles, so the loop body holds
+//     8 phases (2 K-tiles) with every register index static.
+// K-steps past the end of the (split-K) range are issued as out-of-range (zero) loads, so the
+// schedule never branches; an odd K-step count costs one zero tile.
+template <int BM, int BN, bool HAS_BIAS>
+__global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v3(ConvArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  static_assert((BM / 128) * (BN / 64) == 8, "8 waves of 128 x 64");
+  constexpr int WN = BN / 64;                        // waves along N
+  constexpr int LA = BM / 128, LB = BN / 128;        // glds per thread per A / B half-tile
+  constexpr int kAbytes = BM * kRowBytes;
+  constexpr int kBuf = (BM + BN) * kRowBytes;        // 64 / 80 KB per K-tile buffer
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform (SGPR)
+  const int wm = wid / WN, wn = wid % WN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid / a.nNt, nt = bid - mt * a.nNt;
+  const int m0 = mt * BM, n0 = nt * BN;
+
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__hip_bfloat16*>(a.x), 0, a.xbytes, kBufCfg);
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__hip_bfloat16*>(a.w), 0, a.wbytes, kBufCfg);
+
+  // ---- staging geometry: glds (half h, round i) of wave w moves 8 tile rows -----------------
+  //   A rows  i*128 + h*64 + w*8 + lr          (A half h = rows with (row >> 6) & 1 == h)
+  //   B rows  (2i + (w >> 2))*64 + h*32 + (w & 3)*8 + lr   (B half h = (row >> 5) & 1 == h)
+  // (Cout % BN == 0: every B row exists; the B rows of one thread differ by wave-uniform
+  // multiples of the weight row, carried in the scalar offset)
+  const int lr = lane >> 3;
+  const int csw = (lane & 7) ^ lr;  // every row group starts at a multiple of 8: row & 7 == lr
+  const int HoWo = a.Ho * a.Wo;
+  int a_off[2][LA];
+  uint32_t a_tm[2][LA];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int m = m0 + i * 128 + h * 64 + wid * 8 + lr;
+      a_off[h][i] = 0;
+      a_tm[h][i] = 0;
+      if (m < a.M) {
+        const int b = m / HoWo, r = m - b * HoWo;
+        const int oh = r / a.Wo, ow = r - oh * a.Wo;
+        const int ih0 = oh * a.sh - a.ph, iw0 = ow * a.sw - a.pw;
+        a_off[h][i] = (((b * a.H + ih0) * a.W + iw0) * a.Cin + csw * 8) * 2;
+        for (int ky = 0; ky < a.KH; ++ky) {
+          if ((unsigned)(ih0 + ky * a.dh) >= (unsigned)a.H) continue;
+          for (int kx = 0; kx < a.KW; ++kx)
+            if ((unsigned)(iw0 + kx * a.dw) < (unsigned)a.W) a_tm[h][i] |= 1u << (ky * a.KW + kx);
+        }
+      }
+    }
+  const int wrow_bytes = a.nk * kBK * 2;
+  const int b_base = (n0 + (wid >> 2) * 64 + (wid & 3) * 8 + lr) * wrow_bytes + csw * 16;
+
+  // ---- scalar cursor of the K-step being staged. Past the end of the split's range the
+  // tap index becomes 31 (no row has that bit: KH*KW <= 31) and the weight offset runs out
+  // of range, so those stages load zeros without a branch.
+  const int ks0 = blockIdx.y * a.kps;
+  const int ks1 = min(a.nk, ks0 + a.kps);
+  int ctap = ks0 / a.cpt;
+  int cc = (ks0 - ctap * a.cpt) * kBK;
+  int cky = ctap / a.KW, ckx = ctap - cky * a.KW;
+  const int row_step = a.dh * a.W * a.Cin * 2;
+  const int col_step = a.dw * a.Cin * 2;
+  int ctoff = cky * row_step + ckx * col_step + cc * 2;
+  int cks = ks0;
+  int mtap = ctap, csoff = cks * (kBK * 2);
+
+  auto issueA = [&](int buf, int h) {
+    const uint32_t bit = 1u << mtap;
+#pragma unroll
+    for (int i = 0; i < LA; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          xrs, (lds_ptr_t)(smem + buf * kBuf + (i * 128 + h * 64 + wid * 8) * kRowBytes), 16,
+          (a_tm[h][i] & bit) ? a_off[h][i] + ctoff : kOobOffset, 0, 0, 0);
+  };
+  auto issueB = [&](int buf, int h) {
+#pragma unroll
+    for (int i = 0; i < LB; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          wrs,
+          (lds_ptr_t)(smem + buf * kBuf + kAbytes +
+                      ((2 * i + (wid >> 2)) * 64 + h * 32 + (wid & 3) * 8) * kRowBytes),
+          16, b_base, csoff + (i * 128 + h * 32) * wrow_bytes, 0, 0);
+  };
+  auto advance = [&]() {
+    ++cks;
+    cc += kBK;
+    ctoff += kBK * 2;
+    if (cc == a.Cin) {
+      cc = 0;
+      ++ctap;
+      if (++ckx == a.KW) {
+        ckx = 0;
+        ++cky;
+      }
+      ctoff = cky * row_step + ckx * col_step;
+    }
+    const bool kv = cks < ks1;
+    mtap = kv ? ctap : 31;
+    csoff = kv ? cks * (kBK * 2) : kOobOffset;
+  };
+
+  // ---- fragments ------------------------------------------------------------------------
+  const int frow = lane & 15, fsw = lane & 7, fk = lane >> 4;
+  auto readA = [&](int buf, int mq, bf16x8 (&f)[2][4]) {
+    const char* As = smem + buf * kBuf;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int coff = ((kk * 4 + fk) ^ fsw) << 4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        f[kk][i] = *reinterpret_cast<const bf16x8*>(
+            As + (wm * 128 + mq * 64 + i * 16 + frow) * kRowBytes + coff);
+    }
+  };
+  auto readB = [&](int buf, int nq, bf16x8 (&f)[2][2]) {
+    const char* Bs = smem + buf * kBuf + kAbytes;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int coff = ((kk * 4 + fk) ^ fsw) << 4;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        f[kk][j] = *reinterpret_cast<const bf16x8*>(
+            Bs + (wn * 64 + nq * 32 + j * 16 + frow) * kRowBytes + coff);
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#define IAMD_V3_MFMA(AF, BF, MQ, NQ)                                                        \
+  do {                                                                                      \
+    __builtin_amdgcn_s_setprio(1);                                                          \
+    _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                        \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                           \
+    _Pragma("unroll") for (int j = 0; j < 2; ++j)                                           \
+      acc[(MQ) * 4 + i][(NQ) * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(             \
+          AF[kk][i], BF[kk][j], acc[(MQ) * 4 + i][(NQ) * 2 + j], 0, 0, 0);                  \
+    __builtin_amdgcn_s_setprio(0);                                                          \
+  } while (0)
+#define IAMD_V3_SYNC(N)                                          \
+  do {                                                           \
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");     \
+    __builtin_amdgcn_s_barrier();                                \
+  } while (0)
+  // counted waits (glds per thread still allowed in flight) at each phase of a K-tile:
+  // ph1 needs B0, B1 (A1 may fly), ph2 needs A1 (A0' may fly), ph3 needs nothing new (A0', B0'
+  // may fly), ph4 needs A0' (B0', B1' may fly); prologue needs A0 (B0, B1, A1 may fly)
+  constexpr int W1 = LA, W2 = LA, W3 = LA + LB, W4 = 2 * LB, W0 = 2 * LB + LA;
+
+  // Register budget (2 waves / SIMD -> 256 VGPRs): 128 accumulators + at most 80 operand
+  // registers live. At a K-tile boundary only the A half is read one phase ahead; the first
+  // phase of a K-tile reads its B halves itself (4 + 4 ds_read_b128 it waits on, covered by
+  // the partner wave's MFMAs).
+  bf16x8 a0[2][4], a1[2][4], bX[2][2], bY[2][2];
+  const int nks = ks1 - ks0;
+  const int nt2 = (nks + 1) & ~1;  // K-tiles rounded up to the 2-tile loop body
+  // prologue: stage K-tile 0 into buffer 0 in first-use order, read its A0 half
+  issueA(0, 0);
+  issueB(0, 0);
+  issueB(0, 1);
+  issueA(0, 1);
+  advance();
+  IAMD_V3_SYNC(W0);
+  readA(0, 0, a0);
+  for (int t = 0; t < nt2; t += 2) {
+    // K-tile t in buffer 0, staging K-tile t+1 into buffer 1
+    IAMD_V3_SYNC(W1); issueA(1, 0); readB(0, 0, bX); readB(0, 1, bY); IAMD_V3_MFMA(a0, bX, 0, 0);
+    IAMD_V3_SYNC(W2); issueB(1, 0); readA(0, 1, a1); IAMD_V3_MFMA(a0, bY, 0, 1);
+    IAMD_V3_SYNC(W3); issueB(1, 1); readB(0, 0, bX); IAMD_V3_MFMA(a1, bY, 1, 1);
+    IAMD_V3_SYNC(W4); issueA(1, 1); advance(); readA(1, 0, a0); IAMD_V3_MFMA(a1, bX, 1, 0);
+    // K-tile t+1 in buffer 1, staging K-tile t+2 into buffer 0
+    IAMD_V3_SYNC(W1); issueA(0, 0); readB(1, 0, bX); readB(1, 1, bY); IAMD_V3_MFMA(a0, bX, 0, 0);
+    IAMD_V3_SYNC(W2); issueB(0, 0); readA(1, 1, a1); IAMD_V3_MFMA(a0, bY, 0, 1);
+    IAMD_V3_SYNC(W3); issueB(0, 1); readB(1, 0, bX); IAMD_V3_MFMA(a1, bY, 1, 1);
+    IAMD_V3_SYNC(W4); issueA(0, 1); advance(); readA(0, 0, a0); IAMD_V3_MFMA(a1, bX, 1, 0);
+  }
+#undef IAMD_V3_MFMA
+#undef IAMD_V3_SYNC
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // the trailing (zero) prefetches and reads are done: smem is free
+
+  if (a.part) {  // split-K: raw fp32 partials
+    float* o = a.part + (size_t)blockIdx.y * a.M * a.Cout;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * 128 + i * 16 + (lane >> 4) * 4 + r;
+          const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+          if (m < a.M) o[(size_t)m * a.Cout + n] = acc[i][j][r];
+        }
+    return;
+  }
+
+  // ---- epilogue: 128-column slices through LDS, 16-byte row stores ------------------------
+  char* E = smem;
+#pragma unroll
+  for (int half = 0; half < BN / 128; ++half) {
+    if ((wn >> 1) == half) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int cl = (wn & 1) * 64 + j * 16 + (lane & 15);
+        const int n = n0 + half * 128 + cl;
+        const float bv = HAS_BIAS ? a.bias[n] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int rl = wm * 128 + i * 16 + (lane >> 4) * 4 + r;
+            float v = acc[i][j][r] + bv;
+            v = v > 0.f ? v : v * a.slope;
+            *reinterpret_cast<__hip_bfloat16*>(E + rl * kEpiStride + cl * 2) = __float2bfloat16(v);
+          }
+      }
+    }
+    __syncthreads();
+    const int ch = tid & 15, rr = tid >> 4;  // 16 chunks per row, 32 rows per pass
+#pragma unroll
+    for (int p = 0; p < BM / 32; ++p) {
+      const int rl = p * 32 + rr;
+      const int m = m0 + rl;
+      if (m < a.M) {
+        const uint4 v = *reinterpret_cast<const uint4*>(E + rl * kEpiStride + ch * 16);
+        *reinterpret_cast<uint4*>(a.y + (size_t)m * a.Cout + n0 + half * 128 + ch * 8) = v;
+      }
+    }
+    __syncthreads();
+  }
+#endif  // __HIP_DEVICE_COMPILE__
+}
+
 // y = act(sum_s part[s] + bias) in bf16, 8 channels per thread.
 __global__ void __launch_bounds__(256)
 conv_splitk_reduce(const float* __restrict__ part, const float* __restrict__ bias,
@@ -518,31 +773,57 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
   a.nk = KH * KW * a.cpt;
   a.slope = (float)slope;
   const bool bn128 = Cout % 128 == 0;
-  // v1 by default: the v2 kernel (256 x 128 tile, 3-stage ring, 1 block / CU) measured
-  // 0.83-0.95x of v1 on every SPADE-step shape (profiles/conv_v2_probe_mi355x.txt) — two
-  // co-resident v1 blocks hide each other's barrier + LDS-read phases better than one deeper
-  // pipeline. IMAGINAIRE_AMD_CONV_V=2 selects v2 (Cout % 128 == 0, <= 32 taps) for probing.
-  int ver = 1;
+  // Kernel choice (IMAGINAIRE_AMD_CONV_V = 0 auto | 1 | 2 | 3 forces one):
+  //  v3 — 8-phase 256 x 256 (Cout % 256 == 0) or 512 x 128 (Cout % 128 == 0) tile, one block
+  //       per CU; 1.12-1.22x v1 when every block runs >= 40 K-steps, slower on short K loops
+  //       (profiles/conv_v3_probe_mi355x.txt);
+  //  v1 — 128 x 128 / 64 tile, two blocks per CU: everything else;
+  //  v2 — 256 x 128 3-stage ring: 0.83-0.95x v1 everywhere (profiles/conv_v2_probe_mi355x.txt),
+  //       kept for probing only.
+  int ver = 0;
   if (const char* e = std::getenv("IMAGINAIRE_AMD_CONV_V")) ver = std::atoi(e);
-  const bool v2 = ver == 2 && bn128 && KH * KW <= 32;
-  a.nNt = Cout / (bn128 ? 128 : 64);
-  // BM = 128 by default (4 waves, 2 blocks/CU); BM = 256 (8 waves) measured no faster on the
-  // SPADE shapes (profiles/conv_mfma_probe_mi355x.txt) and stays selectable for probing
-  int bm = v2 ? 256 : 128;
-  if (const char* e = std::getenv("IMAGINAIRE_AMD_CONV_BM")) {
-    const int v = std::atoi(e);
-    if (!v2 && (v == 128 || v == 256)) bm = v;
+  const bool v3_ok = bn128 && KH * KW <= 31;
+  const int v3_bn = Cout % 256 == 0 ? 256 : 128;
+  const int v3_bm = v3_bn == 256 ? 256 : 512;
+  // split factor for a grid of `tiles` blocks at `slots` resident blocks
+  auto split_for = [&](int64_t tiles, int64_t slots) {
+    int S = 1;
+    if (tiles < slots && a.nk >= 16) S = (int)std::min<int64_t>((slots + tiles - 1) / tiles, a.nk / 8);
+    if (const char* e = std::getenv("IMAGINAIRE_AMD_CONV_SPLITK")) S = std::max(1, std::atoi(e));
+    S = std::max(1, std::min(S, a.nk));
+    return ceil_div(a.nk, ceil_div(a.nk, S));
+  };
+  bool v3 = false, v2 = false;
+  if (ver == 3) {
+    v3 = v3_ok;
+  } else if (ver == 2) {
+    v2 = bn128 && KH * KW <= 32;
+  } else if (ver == 0 && v3_ok && v3_bn == 256) {
+    // (the 512 x 128 variant measured 0.88-0.98x v1 on the 128-channel SPADE / dgrad shapes:
+    // selectable with IMAGINAIRE_AMD_CONV_V=3 only)
+    const int64_t t3 = (int64_t)ceil_div(a.M, v3_bm) * (Cout / v3_bn);
+    v3 = ceil_div(a.nk, split_for(t3, 256)) >= 40;
+  }
+  int bm = 128;
+  if (v3) {
+    bm = v3_bm;
+    a.nNt = Cout / v3_bn;
+  } else if (v2) {
+    bm = 256;
+    a.nNt = Cout / 128;
+  } else {
+    a.nNt = Cout / (bn128 ? 128 : 64);
+    if (const char* e = std::getenv("IMAGINAIRE_AMD_CONV_BM")) {
+      const int v = std::atoi(e);
+      if (v == 128 || v == 256) bm = v;
+    }
   }
   const int64_t tiles = (int64_t)ceil_div(a.M, bm) * a.nNt;
   IAMD_CHECK(tiles < (1ll << 31), "conv2d_mfma: grid too large");
   // split-K over (tap, channel-block) k-steps when the tile grid cannot fill the chip (v1: 2
-  // blocks per CU, v2: 1) — the wide-K / narrow-N data gradients of the SPADE gamma/beta
+  // blocks per CU, v2 / v3: 1) — the wide-K / narrow-N data gradients of the SPADE gamma/beta
   // convs at 16x32 .. 64x128 and the 2048-channel head convs
-  const int64_t slots = v2 ? 256 : 512;
-  int S = 1;
-  if (tiles < slots && a.nk >= 16) S = (int)std::min<int64_t>((slots + tiles - 1) / tiles, a.nk / 8);
-  if (const char* e = std::getenv("IMAGINAIRE_AMD_CONV_SPLITK")) S = std::max(1, std::atoi(e));
-  S = std::max(1, std::min(S, a.nk));
+  int S = split_for(tiles, (v2 || v3) ? 256 : 512);
   a.kps = ceil_div(a.nk, S);
   S = ceil_div(a.nk, a.kps);
   at::Tensor part;
@@ -579,7 +860,15 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
     if (a.bias) by_bn(bmv, std::true_type());
     else by_bn(bmv, std::false_type());
   };
-  if (v2) {
+  if (v3) {
+    if (v3_bn == 256) {
+      if (a.bias) hipLaunchKernelGGL((conv_fwd_mfma_v3<256, 256, true>), grid, dim3(512), 0, stream(), a);
+      else hipLaunchKernelGGL((conv_fwd_mfma_v3<256, 256, false>), grid, dim3(512), 0, stream(), a);
+    } else {
+      if (a.bias) hipLaunchKernelGGL((conv_fwd_mfma_v3<512, 128, true>), grid, dim3(512), 0, stream(), a);
+      else hipLaunchKernelGGL((conv_fwd_mfma_v3<512, 128, false>), grid, dim3(512), 0, stream(), a);
+    }
+  } else if (v2) {
     if (a.bias) hipLaunchKernelGGL((conv_fwd_mfma_v2<true>), grid, dim3(512), 0, stream(), a);
     else hipLaunchKernelGGL((conv_fwd_mfma_v2<false>), grid, dim3(512), 0, stream(), a);
   } else if (bm == 256) {

@@ -1,0 +1,89 @@
+"""Attribute the ATen glue of one SPADE training step to Python call sites (GPU).
+
+    python scripts/probe/op_sites.py [--config ...] [--ops copy_,cat,...]
+
+A TorchDispatchMode records every listed aten op of one steady-state step (forward and
+the autograd engine's backward thread) with its output bytes and the innermost repository
+frames of the Python stack; the table is sorted by bytes moved.
+"""
+import argparse
+import collections
+import os
+import sys
+import threading
+import traceback
+
+HERE = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, HERE)
+
+import torch  # noqa: E402
+from torch.utils._python_dispatch import TorchDispatchMode  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument('--config', default=os.path.join(HERE, 'configs', 'bench',
+                                                    'spade_256x512_synthetic.yaml'))
+    p.add_argument('--ops', default='copy_,_to_copy,cat,fill_,add_,add,mul,div,flip,'
+                                    'upsample_nearest2d,upsample_bilinear2d,avg_pool2d,'
+                                    'clone,sub,mul_,zero_,constant_pad_nd,contiguous')
+    p.add_argument('--top', type=int, default=60)
+    args = p.parse_args()
+    from imaginaire_amd.config import Config
+    from imaginaire_amd.utils.trainer import get_model_optimizer_and_scheduler, get_trainer
+    from imaginaire_amd.datasets.synthetic import DeviceBatchSource
+    torch.cuda.set_device(0)
+    cfg = Config(args.config)
+    cfg.logdir = '/tmp/iamd_opsites'
+    nets = get_model_optimizer_and_scheduler(cfg, seed=0)
+    tr = get_trainer(cfg, *nets, train_data_loader=[], val_data_loader=None)
+    src = DeviceBatchSource(cfg, cfg.data.train.batch_size, torch.device('cuda', 0), pool=4)
+
+    def step(i):
+        d = tr.start_of_iteration(src.next(), i)
+        tr.dis_update(d)
+        tr.gen_update(d)
+
+    for i in range(2):
+        step(i)
+    torch.cuda.synchronize()
+    wanted = set(args.ops.split(','))
+    stats = collections.defaultdict(lambda: [0, 0])
+    lock = threading.Lock()
+
+    def site():
+        fr = [f for f in traceback.extract_stack()[:-3]
+              if HERE in f.filename and 'op_sites' not in f.filename]
+        return ' <- '.join('%s:%d' % (os.path.relpath(f.filename, HERE), f.lineno)
+                           for f in reversed(fr[-3:])) or '<backward/engine>'
+
+    class Mode(TorchDispatchMode):
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            out = func(*args, **(kwargs or {}))
+            name = func.__name__.split('.')[0]
+            if name in wanted:
+                t = out if torch.is_tensor(out) else (args[0] if args and torch.is_tensor(
+                    args[0]) else None)
+                nbytes = t.numel() * t.element_size() if t is not None else 0
+                shape = tuple(t.shape) if t is not None else ()
+                dt = str(t.dtype).replace('torch.', '') if t is not None else ''
+                with lock:
+                    s = stats[(name, shape, dt, site())]
+                    s[0] += 1
+                    s[1] += nbytes
+            return out
+
+    # the backward engine runs on its own thread: enable the mode there too
+    torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch(False)
+    with Mode():
+        step(2)
+    torch.cuda.synchronize()
+    rows = sorted(stats.items(), key=lambda kv: -kv[1][1])
+    tot = sum(v[1] for _, v in rows)
+    print('recorded %d op calls, %.2f GB output' % (sum(v[0] for _, v in rows), tot / 1e9))
+    for (name, shape, dt, st), (n, b) in rows[:args.top]:
+        print('%8.1f MB %4d  %-20s %-9s %-26s %s' % (b / 1e6, n, name, dt, str(shape)[:26], st))
+
+
+if __name__ == '__main__':
+    main()
