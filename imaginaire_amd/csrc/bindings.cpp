@@ -45,6 +45,16 @@ void mt_ema(const std::vector<at::Tensor>& targets, const std::vector<at::Tensor
             double beta, const c10::optional<at::Tensor>& sigma,
             const c10::optional<at::Tensor>& count, int64_t start);
 int64_t flush_deferred_uploads();
+at::Tensor mt_l1_loss(const std::vector<at::Tensor>& a, const std::vector<at::Tensor>& b,
+                      const std::vector<double>& w);
+std::vector<at::Tensor> mt_l1_loss_backward(const std::vector<at::Tensor>& a,
+                                            const std::vector<at::Tensor>& b,
+                                            const std::vector<double>& w, const at::Tensor& gout);
+at::Tensor resize_bilinear_fwd(const at::Tensor& x, int64_t Ho, int64_t Wo, double scale_h,
+                               double scale_w, bool align_corners,
+                               const c10::optional<at::Tensor>& add);
+at::Tensor resize_bilinear_bwd(const at::Tensor& dy, int64_t H, int64_t W, double scale_h,
+                               double scale_w, bool align_corners);
 bool stream_capturing();
 void mt_scale(const std::vector<at::Tensor>& xs, const at::Tensor& s);
 at::Tensor mt_sqnorm(const std::vector<at::Tensor>& xs);
@@ -112,6 +122,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("count") = py::none(), py::arg("start") = 0);
   m.def("mt_scale", &iamd::mt_scale, "multi-tensor scale");
   m.def("mt_sqnorm", &iamd::mt_sqnorm, "multi-tensor squared L2 norm");
+  m.def("mt_l1_loss", &iamd::mt_l1_loss, "multi-tensor weighted L1 loss (k13)");
+  m.def("mt_l1_loss_backward", &iamd::mt_l1_loss_backward, "k13 backward");
+  m.def("resize_bilinear_fwd", &iamd::resize_bilinear_fwd,
+        "NHWC bilinear resize (+ residual) (k12)");
+  m.def("resize_bilinear_bwd", &iamd::resize_bilinear_bwd, "k12 backward (gather)");
   m.def("flow_warp_fwd", &iamd::flow_warp_fwd, "bilinear flow warp, border (k9)");
   m.def("flow_warp_bwd", &iamd::flow_warp_bwd, "k9 backward");
   m.def("resample2d_forward", &iamd::resample2d_forward, "FlowNet2 Resample2d (k7)");

@@ -7,7 +7,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from imaginaire_amd.layers import Conv2dBlock
-from imaginaire_amd.ops.resize import Upsample
+from imaginaire_amd.ops.resize import Upsample, upsample_add
 
 
 class FPSEDiscriminator(nn.Module):
@@ -50,16 +50,20 @@ class FPSEDiscriminator(nn.Module):
         return list(layers.keys()) == ['conv'] and type(layers['conv']) is nn.Conv2d and \
             layers['conv'].kernel_size == (1, 1) and layers['conv'].stride == (1, 1)
 
-    def forward(self, images, segmaps):
+    def forward(self, images, segmaps, seg_repeat=1):
+        """``seg_repeat``: ``images`` holds that many stacked copies of the batch of
+        ``segmaps`` (real and fake halves of a batched D pass): the label embedding is computed
+        once and repeated at the (small) prediction resolutions."""
         feat11 = self.enc1(images)
         feat12 = self.enc2(feat11)
         feat13 = self.enc3(feat12)
         feat14 = self.enc4(feat13)
         feat15 = self.enc5(feat14)
         feat25 = self.lat5(feat15)
-        feat24 = self.upsample2x(feat25) + self.lat4(feat14)
-        feat23 = self.upsample2x(feat24) + self.lat3(feat13)
-        feat22 = self.upsample2x(feat23) + self.lat2(feat12)
+        # bilinear 2x up + lateral in one k12 pass (ops/resize.upsample_add)
+        feat24 = upsample_add(feat25, self.lat4(feat14))
+        feat23 = upsample_add(feat24, self.lat3(feat13))
+        feat22 = upsample_add(feat23, self.lat2(feat12))
         feat32 = self.final2(feat22)
         feat33 = self.final3(feat23)
         feat34 = self.final4(feat24)
@@ -79,6 +83,9 @@ class FPSEDiscriminator(nn.Module):
         segembs2 = F.avg_pool2d(segembs, kernel_size=2, stride=2)
         segembs3 = F.avg_pool2d(segembs2, kernel_size=2, stride=2)
         segembs4 = F.avg_pool2d(segembs3, kernel_size=2, stride=2)
+        if seg_repeat > 1:
+            segembs2, segembs3, segembs4 = (e.repeat(seg_repeat, 1, 1, 1)
+                                            for e in (segembs2, segembs3, segembs4))
         pred2 = pred2 + torch.mul(segembs2, seg2).sum(dim=1, keepdim=True)
         pred3 = pred3 + torch.mul(segembs3, seg3).sum(dim=1, keepdim=True)
         pred4 = pred4 + torch.mul(segembs4, seg4).sum(dim=1, keepdim=True)

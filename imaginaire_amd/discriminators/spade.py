@@ -10,6 +10,7 @@ import torch
 import torch.nn as nn
 
 from imaginaire_amd.discriminators.fpse import FPSEDiscriminator
+from imaginaire_amd.ops.conv import mark_zero_tail
 from imaginaire_amd.ops.resize import interpolate
 from imaginaire_amd.discriminators.multires_patch import NLayerPatchDiscriminator
 from imaginaire_amd.registry import canonical_module_name
@@ -46,10 +47,38 @@ class Discriminator(nn.Module):
                                                     fpse_kernel_size, weight_norm_type,
                                                     fpse_activation_norm_type)
 
-    def _single_forward(self, input_label, input_image):
-        input_x = torch.cat((input_label, input_image), 1)
+    @staticmethod
+    def _patch_input(labels, images):
+        """The PatchGAN input ``cat(label, image)`` (reference discriminators/spade.py:73-77)
+        written ONCE into a channel-padded NHWC buffer (188 -> 192 channels on the COCO-Stuff
+        recipe, zero tail): the convs and the bilinear pyramid consume it without the
+        concat + pad copies; ``labels`` / ``images`` are lists (real and fake halves) stacked
+        along the batch."""
+        lab, img = labels[0], images[0]
+        cl, ci = lab.shape[1], img.shape[1]
+        c = cl + ci
+        if not (lab.is_cuda and lab.dim() == 4):
+            return torch.cat([torch.cat((lb, im), 1) for lb, im in zip(labels, images)], 0)
+        cp = (c + 7) // 8 * 8 if c <= 64 else (c + 31) // 32 * 32
+        n = [lb.shape[0] for lb in labels]
+        dtype = img.dtype if img.is_floating_point() else lab.dtype
+        out = torch.empty((sum(n), cp) + tuple(lab.shape[2:]), dtype=dtype, device=lab.device,
+                          memory_format=torch.channels_last)
+        o = 0
+        for lb, im, k in zip(labels, images, n):
+            out[o:o + k, :cl] = lb
+            out[o:o + k, cl:c] = im
+            o += k
+        if cp > c:
+            out[:, c:].zero_()
+            mark_zero_tail(out, c)
+        return out
+
+    def _single_forward(self, input_label, input_image, input_x=None, seg_repeat=1):
+        if input_x is None:
+            input_x = self._patch_input([input_label], [input_image])
         features_list = []
-        pred2, pred3, pred4 = self.fpse_discriminator(input_image, input_label)
+        pred2, pred3, pred4 = self.fpse_discriminator(input_image, input_label, seg_repeat)
         output_list = [pred2, pred3, pred4]
         input_downsampled = input_x
         for net_discriminator in self.discriminators:
@@ -72,9 +101,13 @@ class Discriminator(nn.Module):
             # NOTE: one spectral-norm power iteration per D call (the reference's
             # two sequential passes take two); σ estimates converge identically.
             n = real.shape[0]
-            images = torch.cat([real, fake.to(real.dtype)], 0)
+            fake = fake.to(real.dtype)
+            images = torch.cat([real, fake], 0)
             label = data['label']
-            outs, feats = self._single_forward(torch.cat([label, label], 0), images)
+            # the label of both halves is the same tensor: FPSE embeds it once (seg_repeat)
+            outs, feats = self._single_forward(
+                label, images, input_x=self._patch_input([label, label], [real, fake]),
+                seg_repeat=2)
             output_x['real_outputs'] = [o[:n] for o in outs]
             output_x['fake_outputs'] = [o[n:] for o in outs]
             output_x['real_features'] = [[f[:n] for f in fl] for fl in feats]

@@ -47,17 +47,28 @@ class LabelMapCache(object):
         self.store = {}
 
     @staticmethod
-    def resize(t, size, mode='nearest'):
+    def resize(t, size, mode='nearest', conv_pad=False):
+        """Resized conditional map, memoised per forward. ``conv_pad``: the consumer is a
+        conv block — a CUDA NHWC map with an odd channel count (185-channel COCO-Stuff
+        labels) is returned zero-padded to the conv kernels' channel granularity and marked
+        (ops.conv.mark_zero_tail), so the padding happens once per resolution per forward
+        instead of inside every SPADE layer's MLP conv."""
         cache = LabelMapCache._active
-        if tuple(t.shape[2:]) == tuple(size) and mode == 'nearest':
+        same = tuple(t.shape[2:]) == tuple(size) and mode == 'nearest'
+        pad = conv_pad and t.is_cuda and t.dim() == 4 and t.shape[1] > 64 and \
+            t.shape[1] % 64 != 0
+        if same and not pad:
             return t
-        if cache is None:
-            return interpolate(t, size=size, mode=mode)
-        key = (id(t), t.data_ptr(), tuple(size), mode)
-        out = cache.store.get(key)
+        key = (id(t), t.data_ptr(), tuple(size), mode, pad)
+        out = cache.store.get(key) if cache is not None else None
         if out is None:
-            out = interpolate(t, size=size, mode=mode)
-            cache.store[key] = out
+            out = t if same else interpolate(t, size=size, mode=mode)
+            if pad:
+                c = out.shape[1]
+                out = nhwc_conv.mark_zero_tail(nhwc_conv._pad_channels(out, (c + 63) // 64 * 64),
+                                               c)
+            if cache is not None:
+                cache.store[key] = out
         return out
 
 
@@ -317,7 +328,8 @@ class SpatiallyAdaptiveNorm(nn.Module):
         size = x.shape[2:]
         gbs = []
         for i in active:
-            label_map = LabelMapCache.resize(cond_inputs[i], size)
+            label_map = LabelMapCache.resize(cond_inputs[i], size,
+                                             conv_pad=not self.partial[i])
             gbs.append(self._gb(i, label_map))
         if len(gbs) == 0:
             return fused_norm_or_none(self.norm, x, act_slope=act_slope)

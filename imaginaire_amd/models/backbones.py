@@ -46,7 +46,30 @@ def load_pretrained(model, name, strict=False):
                 missing, unexpected = model.load_state_dict(sd, strict=strict)
                 return True
     warnings.warn('imaginaire_amd: no local weights for {}; using random init'.format(name))
+    stable_random_init(model, name)
     return False
+
+
+def stable_random_init(model, name):
+    """Offline fallback weights: a deterministic (seeded from the network name, independent
+    of the global RNG and of the rank), variance-preserving init — He-normal convs / linears,
+    identity BatchNorm — so activations stay O(1) through the 48-layer Inception-v3 and
+    FID / KID / PRDC on random weights are finite and reproducible (PyTorch's default init
+    shrinks Inception pool features to ~1e-7 and the Frechet distance degenerates)."""
+    import zlib
+    g = torch.Generator().manual_seed(zlib.crc32(name.encode()) & 0x7fffffff)
+    with torch.no_grad():
+        for m in model.modules():
+            if isinstance(m, (nn.Conv2d, nn.Linear)):
+                fan_in = m.weight[0].numel()
+                m.weight.copy_(torch.randn(m.weight.shape, generator=g) * (2.0 / fan_in) ** 0.5)
+                if m.bias is not None:
+                    m.bias.zero_()
+            elif isinstance(m, nn.BatchNorm2d):
+                m.weight.fill_(1.0)
+                m.bias.zero_()
+                m.running_mean.zero_()
+                m.running_var.fill_(1.0)
 
 
 # ---------------------------------------------------------------------------

@@ -75,6 +75,27 @@ def _pad_channels(t, c):
     return out
 
 
+def mark_zero_tail(t, valid_channels):
+    """Declare channels ``[valid_channels:]`` of the NHWC tensor ``t`` to be zeros (a
+    channel-padded buffer such as the 192-channel label|image discriminator input). A conv
+    whose weight has ``valid_channels`` input channels then consumes ``t`` directly, its weight
+    zero-padded to match (tiny), instead of slicing / re-padding the activation every call."""
+    t._iamd_valid_channels = int(valid_channels)
+    return t
+
+
+def _match_channels(x, weight):
+    cx, cw = x.shape[1], weight.shape[1]
+    if cx == cw:
+        return weight
+    if cx > cw and getattr(x, '_iamd_valid_channels', None) == cw:
+        if weight.dim() == 4 and weight.is_cuda:
+            return _pad_channels(weight, cx)
+        return torch.cat([weight, weight.new_zeros((weight.shape[0], cx - cw) +
+                                                   tuple(weight.shape[2:]))], 1)
+    raise RuntimeError('conv: input has {} channels, weight expects {}'.format(cx, cw))
+
+
 def _compute_dtype(x, w):
     if x.is_cuda and torch.is_autocast_enabled('cuda'):
         return torch.get_autocast_dtype('cuda')
@@ -239,6 +260,7 @@ def conv2d_act(x, weight, bias=None, stride=1, padding=0, dilation=1, slope=1.0)
     """``act(conv2d(x, weight) + bias)`` with a leaky slope (1 = identity, 0 = relu);
     one k10 launch when eligible, otherwise MIOpen conv + k2 bias-act epilogue."""
     stride, padding, dilation = _pair(stride), _pair(padding), _pair(dilation)
+    weight = _match_channels(x, weight)
     if mfma_eligible(x, weight, stride, padding, dilation, 1):
         return _MfmaConv2d.apply(x, weight, bias, stride, padding, dilation, slope)
     from imaginaire_amd.ops.bias_act import bias_act
@@ -249,6 +271,8 @@ def conv2d_act(x, weight, bias=None, stride=1, padding=0, dilation=1, slope=1.0)
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1,
            padding_mode='zeros'):
+    if groups == 1:
+        weight = _match_channels(x, weight)
     if padding_mode != 'zeros' and padding_mode is not None:
         x = F.pad(x, _pad_arg(padding), mode=padding_mode)
         padding = 0

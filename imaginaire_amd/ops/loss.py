@@ -1,0 +1,63 @@
+"""Multi-tensor weighted L1 (k13, ``csrc/loss.hip``).
+
+``weighted_l1(as_, bs, weights) = sum_t weights[t] * mean(|as_[t] - bs[t]|)`` as one forward
+and one backward launch over every pair (fp32 accumulation, bf16 features read in place,
+deterministic fixed-order reduction). Used by the perceptual and feature-matching losses
+(reference losses/perceptual.py:139-180, losses/feature_matching.py:19-38), which PyTorch
+autocast would otherwise run as per-layer fp32 copies + l1_loss. CPU / unsupported inputs
+use ``F.l1_loss`` with identical math.
+"""
+import torch
+import torch.nn.functional as F
+
+from imaginaire_amd.ops import _ext
+
+_MAX_PAIRS = 16
+
+
+class _MultiL1(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, weights, *ts):
+        a, b = list(ts[0::2]), list(ts[1::2])
+        ctx.weights = weights
+        ctx.save_for_backward(*ts)
+        return _ext.ext().mt_l1_loss(a, b, weights)
+
+    @staticmethod
+    def backward(ctx, g):
+        ts = ctx.saved_tensors
+        a, b = list(ts[0::2]), list(ts[1::2])
+        need = ctx.needs_input_grad[1::2]
+        grads = _ext.ext().mt_l1_loss_backward(a, b, ctx.weights, g) if any(need) else \
+            [None] * len(a)
+        out = [None]
+        for ga, na in zip(grads, need):
+            out += [ga if na else None, None]
+        return tuple(out)
+
+
+def _native_ok(a, b):
+    return a.is_cuda and _ext.use_native(a) and a.dtype in (torch.bfloat16, torch.float32) and \
+        a.dtype == b.dtype and a.shape == b.shape and a.stride() == b.stride() and \
+        _ext.is_dense(a) and not b.requires_grad
+
+
+def weighted_l1(as_, bs, weights):
+    """sum_t weights[t] * mean(|as_[t] - bs[t]|) as an fp32 scalar (``bs`` treated as
+    constants, like the detached targets of both callers)."""
+    as_, bs, weights = list(as_), list(bs), [float(w) for w in weights]
+    total = None
+    native = [i for i in range(len(as_)) if _native_ok(as_[i], bs[i])]
+    for s in range(0, len(native), _MAX_PAIRS):
+        idx = native[s:s + _MAX_PAIRS]
+        args = []
+        for i in idx:
+            args += [as_[i], bs[i].detach()]
+        v = _MultiL1.apply([weights[i] for i in idx], *args)
+        total = v if total is None else total + v
+    for i in sorted(set(range(len(as_))) - set(native)):
+        v = weights[i] * F.l1_loss(as_[i], bs[i].detach()).float()
+        total = v if total is None else total + v
+    if total is None:
+        raise ValueError('weighted_l1: empty input')
+    return total

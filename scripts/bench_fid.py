@@ -56,6 +56,14 @@ def main():
     from imaginaire_amd.utils.trainer import get_model_optimizer_and_scheduler, get_trainer
 
     real_stdout, sys.stdout = sys.stdout, sys.stderr
+    import threading
+
+    def heartbeat(t0=time.time()):  # the eager path runs minutes without other output
+        while True:
+            time.sleep(20)
+            print('[bench_fid] alive %.0f s' % (time.time() - t0), file=sys.__stderr__,
+                  flush=True)
+    threading.Thread(target=heartbeat, daemon=True).start()
     torch.cuda.set_device(0)
     init_cudnn(False, True)
     device = torch.device('cuda', 0)
@@ -67,6 +75,15 @@ def main():
     n_batches = max(1, args.samples // args.batch)
     src = DeviceBatchSource(cfg, args.batch, device, pool=32, seed=123)
     preprocess = functools.partial(trainer._start_of_iteration, current_iteration=0)
+    # A freshly initialised G is not evaluable: its spectral-norm u/v are random (sigma =
+    # u^T W v can be ~0 -> inf weights) and its BatchNorm running stats are the defaults.
+    # A few no-grad train-mode forwards (power iterations + running statistics) stand in for
+    # training, as in the reference where FID is computed on a trained checkpoint.
+    calib = 5
+    with torch.no_grad(), trainer.autocast():
+        net_G.train()
+        for _ in range(calib):
+            net_G(preprocess(src.next()), random_style=True)
     net_G.eval()
     gen = functools.partial(net_G, random_style=True)
 
@@ -87,6 +104,8 @@ def main():
     t0 = time.perf_counter()
     fid = calculate_frechet_distance(real_mean, real_cov, fake_mean, fake_cov)
     t_fd = time.perf_counter() - t0
+    # determinism: the same statistics again give the same distance
+    fid2 = calculate_frechet_distance(real_mean, real_cov, fake_mean, fake_cov)
     n = n_batches * args.batch
     sys.stdout = real_stdout
     print(json.dumps({
@@ -94,6 +113,7 @@ def main():
         'value': round(n / t_fake, 2), 'unit': 'images/s', 'n_gpus': 1, 'samples': n,
         'batch': args.batch, 'real_stats_img_s': round(n / t_real, 2),
         'frechet_distance_s': round(t_fd, 3), 'fid_random_init': round(float(fid), 4),
+        'fid_repeat_equal': bool(float(fid) == float(fid2)), 'g_calibration_steps': calib,
         'dtype': 'bf16', 'data': 'synthetic COCO-Stuff-shaped, random-init G and Inception',
         'kernels': 'eager-reference' if args.eager else 'hip'}), flush=True)
 

@@ -407,3 +407,92 @@ def test_conv2d_mfma_output_allows_inplace_op_without_activation():
     torch.relu_(y)
     y.float().sum().backward()
     assert b.grad is not None and torch.isfinite(w.grad.float()).all()
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('case', [
+    # (N, C, H, W, size, scale, align_corners, add)
+    (2, 192, 32, 64, None, 0.5, True, False),    # SPADE D input pyramid
+    (2, 64, 8, 16, None, 2.0, False, True),      # FPSE top-down up(x) + lateral
+    (1, 16, 7, 9, (4, 5), None, False, False),   # odd sizes, size given
+    (1, 8, 5, 6, (11, 13), None, True, False),   # upsample, align_corners
+])
+def test_bilinear_resize_k12(dtype, case):
+    from imaginaire_amd.ops.resize import interpolate, upsample_add
+    N, C, H, W, size, scale, ac, add = case
+    torch.manual_seed(0)
+    x = torch.randn(N, C, H, W, device='cuda').to(dtype).contiguous(
+        memory_format=torch.channels_last).requires_grad_(True)
+    xr = x.detach().float().requires_grad_(True)
+    ref = F.interpolate(xr, size=size, scale_factor=scale, mode='bilinear', align_corners=ac)
+    if add:
+        r = torch.randn_like(ref).to(dtype).contiguous(memory_format=torch.channels_last)
+        r.requires_grad_(True)
+        y = upsample_add(x, r, scale_factor=scale, align_corners=ac)
+        ref = ref + r.detach().float()
+    else:
+        y = interpolate(x, size=size, scale_factor=scale, mode='bilinear', align_corners=ac)
+    assert y.dtype == dtype and y.shape == ref.shape
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert (y.float() - ref).abs().max().item() <= tol * max(1.0, ref.abs().max().item())
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    y.backward(g.to(dtype).contiguous(memory_format=torch.channels_last))
+    err = (x.grad.float() - xr.grad).abs().max().item()
+    assert err <= (1e-4 if dtype == torch.float32 else 5e-2) * max(1.0, xr.grad.abs().max().item())
+    if add:
+        assert torch.allclose(r.grad.float(), g.to(dtype).float(), atol=1e-6)
+
+
+def test_spade_discriminator_padded_input_matches_concat():
+    """The channel-padded 192-channel D input (+ conv weight padding) equals the reference
+    concat(label, image) input (reference discriminators/spade.py:73-117)."""
+    import os
+    from imaginaire_amd.config import Config
+    from imaginaire_amd.discriminators.spade import Discriminator
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cfg = Config(os.path.join(root, 'configs', 'unit_test', 'spade.yaml'))
+    torch.manual_seed(0)
+    d = Discriminator(cfg.dis, cfg.data).cuda().to(memory_format=torch.channels_last)
+    from imaginaire_amd.utils.data import get_paired_input_label_channel_number
+    nl = get_paired_input_label_channel_number(cfg.data)
+    label = torch.zeros(2, nl, 64, 128, device='cuda')
+    label.scatter_(1, torch.randint(0, nl, (2, 1, 64, 128), device='cuda'), 1.0)
+    label = label.contiguous(memory_format=torch.channels_last)
+    img = torch.randn(2, 3, 64, 128, device='cuda').contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        x_pad = d._patch_input([label], [img])
+        c = nl + 3
+        assert x_pad.shape[1] % 8 == 0 and x_pad.shape[1] >= c
+        assert x_pad.shape[1] == c or x_pad[:, c:].abs().max() == 0
+        x_cat = torch.cat((label, img), 1).contiguous(memory_format=torch.channels_last)
+        for net in d.discriminators:
+            net.eval()
+            a, _ = net(x_pad)
+            b, _ = net(x_cat)
+            assert torch.allclose(a, b, atol=1e-4, rtol=1e-3)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_multi_tensor_l1_k13(dtype):
+    from imaginaire_amd.ops.loss import weighted_l1
+    torch.manual_seed(0)
+    shapes = [(2, 64, 32, 64), (2, 128, 16, 32), (3, 7, 5), (1000,), (2, 512, 4, 8)]
+    ws = [0.03125, 0.0625, 0.5, 1.0, 2.0]
+    a = [torch.randn(*s, device='cuda').to(dtype) for s in shapes]
+    a[0] = a[0].contiguous(memory_format=torch.channels_last)
+    b = [torch.randn_like(t) for t in a]
+    b[1] = a[1].clone()  # exact ties: sign(0) = 0
+    for t in a:
+        t.requires_grad_(True)
+    loss = weighted_l1(a, b, ws)
+    ar = [t.detach().float().requires_grad_(True) for t in a]
+    ref = sum(w * F.l1_loss(x, y.float()) for w, x, y in zip(ws, ar, b))
+    assert abs(loss.item() - ref.item()) <= 1e-4 * max(1.0, abs(ref.item()))
+    loss.backward(torch.tensor(1.5, device='cuda'))
+    (ref * 1.5).backward()
+    for x, xr in zip(a, ar):
+        assert x.grad.dtype == dtype and x.grad.stride() == x.stride()
+        assert torch.allclose(x.grad.float(), xr.grad, rtol=1e-2, atol=1e-8)
+    # deterministic: the same value twice
+    assert weighted_l1(a, b, ws).item() == weighted_l1(a, b, ws).item()
