@@ -63,6 +63,9 @@ def parse():
                         'print GPU time per (op, input shapes) to stderr')
     p.add_argument('--op-profile', action='store_true',
                    help='like --conv-profile but for every aten op (self device time)')
+    p.add_argument('--conv-log', action='store_true',
+                   help='after warm-up, time every conv kernel call of one eager step (device '
+                        'events) and print time / TF/s per (kind, shape, kernel) to stderr')
     p.add_argument('--op-stack', action='store_true',
                    help='with --op-profile: group the small elementwise ops by Python call site')
     return p.parse_args()
@@ -161,8 +164,8 @@ def main():
     # steady-state iteration: hipGraph-captured (world size 1) after max(1, W-2) eager
     # warm-up steps, so with W >= 2 the timed steps are all replays
     from imaginaire_amd.utils.cuda_graph import make_trainer_step
-    use_graph = on_gpu and not (args.no_graph or args.eager or args.profile_phases) and \
-        args.warmup >= 2
+    use_graph = on_gpu and not (args.no_graph or args.eager or args.profile_phases or
+                                args.conv_log) and args.warmup >= 2
     run_step, graphed = make_trainer_step(trainer, warmup=min(3, max(1, args.warmup - 2)),
                                           enabled=use_graph)
 
@@ -184,6 +187,33 @@ def main():
             torch.cuda.synchronize()
         print(prof.key_averages().table(sort_by='self_cpu_time_total', row_limit=45),
               flush=True)
+
+    if args.conv_log and rank == 0:
+        from imaginaire_amd.ops import conv as conv_ops
+        torch.cuda.synchronize()
+        conv_ops.enable_conv_log(True)
+        t0 = time.perf_counter()
+        step(args.warmup)
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) * 1e3
+        rows = conv_ops.conv_log_summary()
+        conv_ops.enable_conv_log(False)
+        tot = sum(r[4] for r in rows)
+        fl = sum(r[5] * r[4] * 1e9 for r in rows)
+        print('conv kernels in one eager step: %.2f ms of %.1f ms wall, %.1f TFLOP, %.0f TF/s' % (
+            tot, wall, fl / 1e12, fl / max(tot, 1e-9) / 1e9))
+        by_kind = {}
+        for r in rows:
+            k = by_kind.setdefault((r[0], r[1]), [0, 0.0, 0.0])
+            k[0] += r[3]
+            k[1] += r[4]
+            k[2] += r[5] * r[4] * 1e9
+        for (kind, path), (n, ms, f) in sorted(by_kind.items(), key=lambda kv: -kv[1][1]):
+            print('  %-6s %-7s %4d calls %8.2f ms %6.0f TF/s' % (kind, path, n, ms,
+                                                              f / max(ms, 1e-9) / 1e9))
+        for kind, path, desc, n, ms, tfs in rows:
+            print('%8.3f ms %3d  %-6s %-7s %5.0f TF/s  %s' % (ms, n, kind, path, tfs, desc))
+        sys.stdout.flush()
 
     if (args.conv_profile or args.op_profile) and rank == 0:
         from torch.profiler import ProfilerActivity, profile

@@ -1,10 +1,16 @@
 """SPADE discriminator: PatchGAN pyramid + FPSE (reference discriminators/spade.py:15-117).
 
 In the D update real and fake are run as ONE batched forward (concatenated
-along the batch axis) instead of two separate passes: the same math (no
+along the batch axis) instead of two separate passes: the same network math (no
 batch-coupled layers, activation_norm_type is 'none'), half the kernel launches
 and twice the parallelism per conv. In the G update (gradient flows through the
 fake branch only) the passes stay separate so the backward skips the real half.
+
+``dis.batch_real_fake`` (default True) selects this. The batched D update runs ONE
+spectral-norm power iteration where the reference's two sequential passes run two
+(the fake pass there sees the σ refreshed by the real pass,
+reference discriminators/spade.py:91-117); ``batch_real_fake: False`` restores
+the reference order exactly (tests/test_spade_dis_semantics_cpu.py).
 """
 import torch
 import torch.nn as nn
@@ -34,7 +40,8 @@ class Discriminator(nn.Module):
         activation_norm_type = getattr(dis_cfg, 'activation_norm_type', 'none')
         weight_norm_type = getattr(dis_cfg, 'weight_norm_type', 'spectral')
         num_input_channels = image_channels + num_labels
-        self.batched = activation_norm_type in ('none', '', 'instance') and \
+        self.batched = getattr(dis_cfg, 'batch_real_fake', True) and \
+            activation_norm_type in ('none', '', 'instance') and \
             getattr(dis_cfg, 'fpse_activation_norm_type', 'none') in ('none', '', 'instance')
         self.discriminators = nn.ModuleList()
         for _ in range(num_discriminators):
@@ -98,8 +105,8 @@ class Discriminator(nn.Module):
         # work), so the two passes run separately there, as in the reference.
         grad_through_fake = torch.is_grad_enabled() and fake.requires_grad
         if self.batched and real.shape == fake.shape and not grad_through_fake:
-            # NOTE: one spectral-norm power iteration per D call (the reference's
-            # two sequential passes take two); σ estimates converge identically.
+            # one spectral-norm power iteration per D call (the reference's two sequential
+            # passes take two; dis.batch_real_fake=False runs them)
             n = real.shape[0]
             fake = fake.to(real.dtype)
             images = torch.cat([real, fake], 0)

@@ -10,13 +10,27 @@ through the host.
 
 Semantics are unchanged: a point's colour is fixed the first time it is
 seen; rendering writes the stored colour of every visible point and a 255
-mask where the point has been seen.
+mask where the point has been seen. Duplicate targets (one point id listed
+twice in a frame, two points projecting to one pixel) resolve as numpy's
+fancy-index assignment does — the LAST row wins (reference render.py:87-97,
+138) — by a scatter-max of row numbers that keeps only each target's winning
+row before a duplicate-free index_put (a plain device index_put with duplicate
+indices has an undefined write order).
 """
 import json
 import os
 
 import numpy as np
 import torch
+
+
+def _last_rows(target, size):
+    """Boolean mask of the rows of ``target`` (1-D long) that are the last occurrence of their
+    value: numpy's last-write-wins order for ``a[target] = values``, made deterministic."""
+    rows = torch.arange(target.numel(), device=target.device)
+    last = torch.full((size,), -1, dtype=torch.long, device=target.device)
+    last.scatter_reduce_(0, target, rows, reduce='amax')
+    return last[target] == rows
 
 
 class SplatRenderer(object):
@@ -60,6 +74,8 @@ class SplatRenderer(object):
         self.call_idx += 1
         i, j, pid = self._as_index(point_info, device)
         self._resize_arrays(int(pid.max()) + 1, device)
+        keep = _last_rows(pid, self.colors.shape[0])
+        i, j, pid = i[keep], j[keep], pid[keep]
         seen = self.seen_mask[pid]
         self.colors[pid] = seen * self.colors[pid] + (1 - seen) * image[i, j].to(torch.uint8)
         self.seen_time[pid] = seen.int() * self.seen_time[pid] + \
@@ -73,6 +89,8 @@ class SplatRenderer(object):
         if point_info is not None and len(point_info) != 0:
             i, j, pid = self._as_index(point_info, device)
             self._resize_arrays(int(pid.max()) + 1, device)
+            keep = _last_rows(i * w + j, h * w)
+            i, j, pid = i[keep], j[keep], pid[keep]
             output[i, j] = self.colors[pid]
             mask[i, j] = 255 * self.seen_mask[pid]
         output, mask = output.cpu().numpy(), mask.cpu().numpy()

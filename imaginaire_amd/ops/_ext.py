@@ -25,7 +25,44 @@ def load():
     except ImportError as e:  # pragma: no cover - depends on build state
         _ERR = e
         _EXT = None
+    if _EXT is not None:
+        _check_provenance()
     return _EXT
+
+
+def build_info():
+    """The manifest ``_build`` wrote next to ``_C.so`` (arch, sources digest, compiler)."""
+    import json
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        '_C.build.json')
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+def _check_provenance():
+    """A _C.so built from different sources than the tree it sits in (stale build shipped to
+    a GPU box) is an error: its kernels would not be the ones the Python side expects.
+    ``IMAGINAIRE_AMD_ALLOW_STALE_EXT=1`` downgrades it to a warning."""
+    info = build_info()
+    if info is None:
+        return
+    from imaginaire_amd import _build
+    try:
+        digest = _build.sources_digest()
+    except OSError:  # sources not shipped alongside the binary
+        return
+    if info.get('sources_sha1') != digest:
+        msg = ('imaginaire_amd._C was built from sources %s but the tree holds %s: rebuild '
+               'with `python -m imaginaire_amd._build`' % (
+                   str(info.get('sources_sha1'))[:12], digest[:12]))
+        if os.environ.get('IMAGINAIRE_AMD_ALLOW_STALE_EXT', '0') == '1':
+            import warnings
+            warnings.warn(msg)
+        else:
+            raise ImportError(msg)
 
 
 def available():

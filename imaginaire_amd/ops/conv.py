@@ -38,6 +38,61 @@ _MFMA_MIN_DGRAD_BLOCKS = int(os.environ.get('IMAGINAIRE_AMD_MFMA_MIN_DGRAD_BLOCK
 _MFMA_WGRAD = os.environ.get('IMAGINAIRE_AMD_MFMA_WGRAD', '1')
 
 
+# ---- per-call conv log (IMAGINAIRE_AMD_CONV_LOG=1 or enable_conv_log()): every k10 / k11 /
+# MIOpen call of the steps that follow is timed with a pair of device events and recorded with
+# its GEMM shape, so bench.py --conv-log can print time and TF/s per (kind, shape, kernel).
+_CONV_LOG = [] if os.environ.get('IMAGINAIRE_AMD_CONV_LOG', '0') == '1' else None
+
+
+def enable_conv_log(on=True):
+    global _CONV_LOG
+    _CONV_LOG = [] if on else None
+
+
+class _Logged(object):
+    """Context manager timing one conv kernel call into ``_CONV_LOG``."""
+    __slots__ = ('rec',)
+
+    def __init__(self, kind, path, flops, desc):
+        self.rec = None
+        if _CONV_LOG is not None and not torch.cuda.is_current_stream_capturing():
+            self.rec = [kind, path, flops, desc, torch.cuda.Event(enable_timing=True),
+                        torch.cuda.Event(enable_timing=True)]
+
+    def __enter__(self):
+        if self.rec is not None:
+            self.rec[4].record()
+        return self
+
+    def __exit__(self, *exc):
+        if self.rec is not None:
+            self.rec[5].record()
+            _CONV_LOG.append(self.rec)
+        return False
+
+
+def conv_log_summary(reset=True):
+    """[(kind, path, desc, calls, ms, TF/s)] sorted by total time (synchronises)."""
+    if _CONV_LOG is None:
+        return []
+    torch.cuda.synchronize()
+    agg = {}
+    for kind, path, flops, desc, e0, e1 in _CONV_LOG:
+        a = agg.setdefault((kind, path, desc), [0, 0.0, 0.0])
+        a[0] += 1
+        a[1] += e0.elapsed_time(e1)
+        a[2] += flops
+    if reset:
+        del _CONV_LOG[:]
+    rows = [(k[0], k[1], k[2], v[0], v[1], v[2] / max(v[1], 1e-9) / 1e9) for k, v in agg.items()]
+    rows.sort(key=lambda r: -r[4])
+    return rows
+
+
+def _gemm_desc(x, w, stride, padding):
+    return '%s x %s s%s p%s' % (list(x.shape), list(w.shape), stride[0], padding[0])
+
+
 def _mfma_enabled():
     return os.environ.get('IMAGINAIRE_AMD_MFMA_CONV', '1') == '1' and not _ext.force_eager()
 
@@ -155,8 +210,12 @@ class _MfmaConv2d(torch.autograd.Function):
         cp, op = _round_up(cin, 64), _round_up(cout, 64)
         xb = _pad_channels(x.to(torch.bfloat16), cp)
         wb = _pad_rows(_pad_channels(w.to(torch.bfloat16), cp), op)
-        y = _ext.ext().conv2d_mfma(xb, wb, _pad_rows(bias, op), stride[0], stride[1],
-                                   padding[0], padding[1], dilation[0], dilation[1], float(slope))
+        ho, wo = _out_hw(x.shape[2], x.shape[3], w.shape[2:], stride, padding, dilation)
+        with _Logged('fwd', 'k10', 2.0 * x.shape[0] * ho * wo * op * cp * w.shape[2] * w.shape[3],
+                     _gemm_desc(xb, wb, stride, padding)):
+            y = _ext.ext().conv2d_mfma(xb, wb, _pad_rows(bias, op), stride[0], stride[1],
+                                       padding[0], padding[1], dilation[0], dilation[1],
+                                       float(slope))
         ctx.conf = (stride, padding, dilation, float(slope), cin, cout, x.dtype, w.dtype,
                     None if bias is None else bias.dtype, x.shape[1])
         # the output is needed only for a fused activation's mask: with slope 1 it is not
@@ -187,14 +246,18 @@ class _MfmaConv2d(torch.autograd.Function):
                 (cp // (128 if cp % 128 == 0 else 64))
             # the dgrad GEMM has N = Cin (few tiles, K = taps x Cout for the SPADE γ/β convs):
             # k10 splits K over the grid's y dimension for those
+            fl = 2.0 * dy.shape[0] * dy.shape[2] * dy.shape[3] * wb.numel()
             if stride == (1, 1) and pt[0] >= 0 and pt[1] >= 0 and \
                     dblocks >= _MFMA_MIN_DGRAD_BLOCKS:
-                dx = _ext.ext().conv2d_mfma(dy, _flip_t(wb), None, 1, 1, pt[0], pt[1],
-                                            dilation[0], dilation[1], 1.0)
+                wt = _flip_t(wb)
+                with _Logged('dgrad', 'k10', fl, _gemm_desc(dy, wt, (1, 1), pt)):
+                    dx = _ext.ext().conv2d_mfma(dy, wt, None, 1, 1, pt[0], pt[1],
+                                                dilation[0], dilation[1], 1.0)
             else:
-                dx = torch.ops.aten.convolution_backward(
-                    dy, xb, wb, None, stride, padding, dilation, False, [0, 0], 1,
-                    [True, False, False])[0]
+                with _Logged('dgrad', 'miopen', fl, _gemm_desc(dy, wb, stride, padding)):
+                    dx = torch.ops.aten.convolution_backward(
+                        dy, xb, wb, None, stride, padding, dilation, False, [0, 0], 1,
+                        [True, False, False])[0]
             if dx.shape[1] != xc:
                 dx = dx[:, :xc]
             dx = dx.to(xdt)
@@ -225,10 +288,14 @@ def _wgrad(dy, xb, wb, stride, padding, dilation):
             [False, True, False])[1]
 
     mode = _MFMA_WGRAD
+    fl = 2.0 * dy.shape[0] * dy.shape[2] * dy.shape[3] * wb.numel()
+    desc = _gemm_desc(xb, wb, stride, padding)
     if mode == '1':
-        return k11()
+        with _Logged('wgrad', 'k11', fl, desc):
+            return k11()
     if mode == '0':
-        return miopen()
+        with _Logged('wgrad', 'miopen', fl, desc):
+            return miopen()
     key = (tuple(dy.shape), tuple(xb.shape), tuple(wb.shape), stride, padding, dilation)
     choice = _WGRAD_CHOICE.get(key)
     if choice is None:
@@ -253,7 +320,8 @@ def _wgrad(dy, xb, wb, stride, padding, dilation):
             times = {'k11': float(t[0]), 'miopen': float(t[1])}
         choice = min(times, key=times.get)
         _WGRAD_CHOICE[key] = choice
-    return k11() if choice == 'k11' else miopen()
+    with _Logged('wgrad', choice, fl, desc):
+        return k11() if choice == 'k11' else miopen()
 
 
 def conv2d_act(x, weight, bias=None, stride=1, padding=0, dilation=1, slope=1.0):

@@ -94,9 +94,14 @@ def interpolate(x, size=None, scale_factor=None, mode='nearest', align_corners=N
     if mode == 'nearest' and x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and \
             torch.is_autocast_enabled('cuda'):
         with torch.autocast('cuda', enabled=False):
-            return F.interpolate(x, size, scale_factor, mode, align_corners,
-                                 recompute_scale_factor)
-    return F.interpolate(x, size, scale_factor, mode, align_corners, recompute_scale_factor)
+            y = F.interpolate(x, size, scale_factor, mode, align_corners,
+                              recompute_scale_factor)
+    else:
+        y = F.interpolate(x, size, scale_factor, mode, align_corners, recompute_scale_factor)
+    valid = getattr(x, '_iamd_valid_channels', None)
+    if valid is not None:  # resizes act per channel: a zero channel tail stays zero
+        y._iamd_valid_channels = valid
+    return y
 
 
 class Upsample(nn.Module):

@@ -306,7 +306,9 @@ class BaseTrainer(object):
             print('Save output images to {}'.format(path))
             save_image_grid(vis_images, path, nrow=1, padding=0, normalize=True)
             if self.cfg.trainer.image_to_tensorboard:
-                self.image_meter.write_image(vis_images[0], self.current_iteration)
+                # the same grid as the PNG (nrow=1, padding=0: samples stacked vertically)
+                grid = torch.cat(list(vis_images), dim=1)
+                self.image_meter.write_image(grid, self.current_iteration)
         self.net_G.train()
 
     def write_metrics(self):

@@ -69,8 +69,9 @@ def add_hparams(hparam_dict=None, metric_dict=None):
     lw = LOG_WRITER
     if lw is None:
         return
-    for k, v in metric_dict.items():
-        lw.add_scalar('hparams/' + k, v, 0)
+    # both writers (torch's and the native one) emit the hparams plugin's experiment /
+    # session-start / session-end summaries plus the metric scalars
+    lw.add_hparams(hparam_dict, metric_dict)
 
 
 class Meter(object):

@@ -1,10 +1,13 @@
 """Minimal TensorBoard event-file writer (no tensorboard/tensorflow dependency).
 
 Writes ``events.out.tfevents.*`` records (TFRecord framing with masked
-CRC32-C, hand-encoded ``Event``/``Summary`` protobufs) for scalars, so the
-reference's TensorBoard scalar logging (utils/meters.py:54-104) keeps working
-on images that ship without tensorboard. Images/hparams are written as scalar
-placeholders + PNG files next to the event file.
+CRC32-C, hand-encoded ``Event``/``Summary`` protobufs) so the reference's
+TensorBoard logging (utils/meters.py:54-159: scalars, histograms, the
+"Visualizations" image grid and the hparams plugin's experiment / session
+start / session end summaries) keeps working on images that ship without
+tensorboard. Field numbers follow tensorflow's ``summary.proto`` /
+``histogram.proto`` and tensorboard's ``plugins/hparams/{api,plugin_data}.proto``.
+``read_events`` parses the records back (tests).
 """
 import os
 import socket
@@ -71,9 +74,92 @@ def _event(step, wall_time, summary=None, file_version=None):
     return msg
 
 
+def _double(num, v):
+    return _field(num, 1, struct.pack('<d', float(v)))
+
+
 def _scalar_summary(tag, value):
     val = _bytes_field(1, tag.encode()) + _field(2, 5, struct.pack('<f', float(value)))
     return _bytes_field(1, val)
+
+
+def _image_summary(tag, png, height, width, channels):
+    # Summary.Image {height=1, width=2, colorspace=3, encoded_image_string=4}
+    img = (_field(1, 0, _varint(height)) + _field(2, 0, _varint(width)) +
+           _field(3, 0, _varint(channels)) + _bytes_field(4, png))
+    return _bytes_field(1, _bytes_field(1, tag.encode()) + _bytes_field(4, img))
+
+
+def _histogram_summary(tag, values, bins=64):
+    import numpy as np
+    v = np.asarray(values, dtype=np.float64).reshape(-1)
+    v = v[np.isfinite(v)]
+    if v.size == 0:
+        v = np.zeros(1)
+    counts, edges = np.histogram(v, bins=bins)
+    # HistogramProto {min=1, max=2, num=3, sum=4, sum_squares=5, bucket_limit=6, bucket=7};
+    # bucket i counts values in (bucket_limit[i-1], bucket_limit[i]]
+    limits = struct.pack('<%dd' % bins, *edges[1:].tolist())
+    buckets = struct.pack('<%dd' % bins, *counts.astype(np.float64).tolist())
+    h = (_double(1, v.min()) + _double(2, v.max()) + _double(3, v.size) + _double(4, v.sum()) +
+         _double(5, (v * v).sum()) + _bytes_field(6, limits) + _bytes_field(7, buckets))
+    return _bytes_field(1, _bytes_field(1, tag.encode()) + _bytes_field(5, h))
+
+
+def _pb_value(v):
+    """google.protobuf.Value {number_value=2, string_value=3, bool_value=4}."""
+    if isinstance(v, bool):
+        return _field(4, 0, _varint(int(v)))
+    if isinstance(v, (int, float)):
+        return _double(2, v)
+    return _bytes_field(3, str(v).encode())
+
+
+def _hparams_summaries(hparam_dict, metric_dict):
+    """The three summaries of tensorboard's hparams plugin (what
+    ``torch.utils.tensorboard.summary.hparams`` returns; reference meters.py:67-104)."""
+    infos = b''
+    for k, v in hparam_dict.items():
+        # HParamInfo {name=1, type=4}: DATA_TYPE_STRING=1, BOOL=2, FLOAT64=3
+        dtype = 2 if isinstance(v, bool) else 3 if isinstance(v, (int, float)) else 1
+        infos += _bytes_field(4, _bytes_field(1, k.encode()) + _field(4, 0, _varint(dtype)))
+    for k in metric_dict:
+        # MetricInfo {name=1: MetricName {tag=2}}
+        infos += _bytes_field(5, _bytes_field(1, _bytes_field(2, k.encode())))
+    experiment = infos
+    ssi = b''
+    for k, v in hparam_dict.items():
+        ssi += _bytes_field(1, _bytes_field(1, k.encode()) + _bytes_field(2, _pb_value(v)))
+    ssi += _double(5, time.time())
+    sei = _field(1, 0, _varint(1)) + _double(2, time.time())  # STATUS_SUCCESS
+
+    def wrap(tag, field, payload):
+        plugin_content = _field(1, 0, _varint(0)) + _bytes_field(field, payload)
+        meta = _bytes_field(1, _bytes_field(1, b'hparams') + _bytes_field(2, plugin_content))
+        return _bytes_field(1, _bytes_field(1, tag.encode()) + _bytes_field(9, meta))
+
+    return [wrap('_hparams_/experiment', 2, experiment),
+            wrap('_hparams_/session_start_info', 3, ssi),
+            wrap('_hparams_/session_end_info', 4, sei)]
+
+
+def _encode_png(img):
+    """[C,H,W] / [H,W,C] / [H,W] float (0..1) or uint8 image -> (png bytes, H, W, C)."""
+    import io
+
+    import numpy as np
+    from PIL import Image
+    a = img.detach().float().cpu().numpy() if hasattr(img, 'detach') else np.asarray(img)
+    if a.ndim == 3 and a.shape[0] in (1, 3, 4) and a.shape[2] not in (1, 3, 4):
+        a = a.transpose(1, 2, 0)
+    if a.ndim == 2:
+        a = a[:, :, None]
+    if a.dtype != np.uint8:
+        a = (np.clip(a, 0, 1) * 255 + 0.5).astype(np.uint8)
+    h, w, c = a.shape
+    buf = io.BytesIO()
+    Image.fromarray(a[:, :, 0] if c == 1 else a).save(buf, format='PNG')
+    return buf.getvalue(), h, w, c
 
 
 class SummaryWriter(object):
@@ -94,17 +180,24 @@ class SummaryWriter(object):
         self._write(_event(int(step), time.time(), summary=_scalar_summary(tag, value)))
         self._f.flush()
 
-    def add_histogram(self, tag, values, step):
-        import numpy as np
-        v = np.asarray(values.detach().cpu() if hasattr(values, 'detach') else values)
-        self.add_scalar(tag + '/mean', float(v.mean()), step)
-        self.add_scalar(tag + '/std', float(v.std()), step)
+    def add_histogram(self, tag, values, step, bins=64):
+        if hasattr(values, 'detach'):
+            values = values.detach().float().cpu().numpy()
+        self._write(_event(int(step), time.time(), summary=_histogram_summary(tag, values, bins)))
+        self._f.flush()
 
     def add_image(self, tag, img, step):
-        from imaginaire_amd.utils.visualization.common import tensor2pilimage
-        path = os.path.join(self.log_dir, 'images', '%s_%09d.png' % (tag, step))
-        os.makedirs(os.path.dirname(path), exist_ok=True)
-        tensor2pilimage(img, minus1to1_normalized=False).save(path)
+        """``img``: [C,H,W] in [0,1] (torch's ``dataformats='CHW'`` default) or uint8."""
+        png, h, w, c = _encode_png(img)
+        self._write(_event(int(step), time.time(), summary=_image_summary(tag, png, h, w, c)))
+        self._f.flush()
+
+    def add_hparams(self, hparam_dict, metric_dict):
+        for summ in _hparams_summaries(hparam_dict, metric_dict):
+            self._write(_event(0, time.time(), summary=summ))
+        for k, v in metric_dict.items():
+            self.add_scalar(k, v, 0)
+        self._f.flush()
 
     def flush(self):
         self._f.flush()
@@ -113,36 +206,92 @@ class SummaryWriter(object):
         self._f.close()
 
 
-def read_scalars(path):
-    """Parse scalars back from an event file (used by tests)."""
-    out = []
+def _records(path):
     with open(path, 'rb') as f:
         data = f.read()
     pos = 0
     while pos + 12 <= len(data):
         (n,) = struct.unpack('<Q', data[pos:pos + 8])
+        if struct.unpack('<I', data[pos + 8:pos + 12])[0] != _masked_crc(data[pos:pos + 8]):
+            raise ValueError('corrupt record header at %d' % pos)
         rec = data[pos + 12:pos + 12 + n]
+        if struct.unpack('<I', data[pos + 12 + n:pos + 16 + n])[0] != _masked_crc(rec):
+            raise ValueError('corrupt record at %d' % pos)
         pos += 12 + n + 4
-        # extremely small protobuf walker for Event.summary.value.{tag, simple_value}
-        i, step = 0, None
-        while i < len(rec):
-            key, i = _read_varint(rec, i)
-            num, wire = key >> 3, key & 7
-            if wire == 0:
-                val, i = _read_varint(rec, i)
-                if num == 2:
-                    step = val
-            elif wire == 1:
-                i += 8
-            elif wire == 5:
-                i += 4
-            elif wire == 2:
-                ln, i = _read_varint(rec, i)
-                payload = rec[i:i + ln]
-                i += ln
-                if num == 5:
-                    out.extend((t, v, step) for t, v in _parse_summary(payload))
+        yield rec
+
+
+def _fields(buf):
+    """Generic protobuf walk: yields (field number, wire type, value) — value is an int
+    (varint), raw bytes (fixed64/fixed32) or the payload (length-delimited)."""
+    i = 0
+    while i < len(buf):
+        key, i = _read_varint(buf, i)
+        num, wire = key >> 3, key & 7
+        if wire == 0:
+            val, i = _read_varint(buf, i)
+        elif wire == 1:
+            val, i = buf[i:i + 8], i + 8
+        elif wire == 5:
+            val, i = buf[i:i + 4], i + 4
+        elif wire == 2:
+            ln, i = _read_varint(buf, i)
+            val, i = buf[i:i + ln], i + ln
+        else:
+            raise ValueError('unsupported wire type %d' % wire)
+        yield num, wire, val
+
+
+def read_events(path):
+    """All summary values of an event file as dicts {step, tag, kind, ...}: kind 'scalar'
+    (value), 'image' (height, width, channels, png), 'histogram' (min, max, num, sum,
+    buckets) or 'plugin' (plugin, content)."""
+    out = []
+    for rec in _records(path):
+        step, summary = 0, None
+        for num, wire, val in _fields(rec):
+            if num == 2 and wire == 0:
+                step = val
+            elif num == 5 and wire == 2:
+                summary = val
+        if summary is None:
+            continue
+        for num, _, value in _fields(summary):
+            if num != 1:
+                continue
+            ev = {'step': step}
+            for vn, vw, vv in _fields(value):
+                if vn == 1:
+                    ev['tag'] = vv.decode()
+                elif vn == 2 and vw == 5:
+                    ev.update(kind='scalar', value=struct.unpack('<f', vv)[0])
+                elif vn == 4:
+                    img = {n: v for n, _, v in _fields(vv)}
+                    ev.update(kind='image', height=img.get(1), width=img.get(2),
+                              channels=img.get(3), png=img.get(4))
+                elif vn == 5:
+                    h = {}
+                    for hn, _, hv in _fields(vv):
+                        h[hn] = hv
+                    bk = h.get(7, b'')
+                    ev.update(kind='histogram', min=struct.unpack('<d', h[1])[0],
+                              max=struct.unpack('<d', h[2])[0],
+                              num=struct.unpack('<d', h[3])[0],
+                              sum=struct.unpack('<d', h[4])[0],
+                              buckets=list(struct.unpack('<%dd' % (len(bk) // 8), bk)))
+                elif vn == 9:
+                    pd = dict((n, v) for n, _, v in _fields(vv)).get(1, b'')
+                    pdd = dict((n, v) for n, _, v in _fields(pd))
+                    ev.update(kind='plugin', plugin=pdd.get(1, b'').decode(),
+                              content=pdd.get(2, b''))
+            out.append(ev)
     return out
+
+
+def read_scalars(path):
+    """(tag, value, step) of every scalar in an event file (used by tests)."""
+    return [(e['tag'], e['value'], e['step']) for e in read_events(path)
+            if e.get('kind') == 'scalar']
 
 
 def _read_varint(b, i):
@@ -154,32 +303,3 @@ def _read_varint(b, i):
         if not byte & 0x80:
             return result, i
         shift += 7
-
-
-def _parse_summary(payload):
-    res = []
-    i = 0
-    while i < len(payload):
-        key, i = _read_varint(payload, i)
-        ln, i = _read_varint(payload, i)
-        val = payload[i:i + ln]
-        i += ln
-        j, tag, sv = 0, None, None
-        while j < len(val):
-            k, j = _read_varint(val, j)
-            num, wire = k >> 3, k & 7
-            if wire == 2:
-                l2, j = _read_varint(val, j)
-                if num == 1:
-                    tag = val[j:j + l2].decode()
-                j += l2
-            elif wire == 5:
-                if num == 2:
-                    sv = struct.unpack('<f', val[j:j + 4])[0]
-                j += 4
-            elif wire == 0:
-                _, j = _read_varint(val, j)
-            elif wire == 1:
-                j += 8
-        res.append((tag, sv))
-    return res

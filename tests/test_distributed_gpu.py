@@ -1,0 +1,185 @@
+"""Multi-rank correctness of the HIP SyncBN and the bucketed DDP on the GPU.
+
+Two ranks share the one GPU of the test box (gloo process group; RCCL cannot place two ranks
+on one device). Reference semantics:
+  * SyncBN: torch.nn.SyncBatchNorm (reference layers/activation_norm.py:403-410) — the
+    sync_batch fused norm on per-rank halves must equal batch norm over the concatenated batch;
+  * DDP: torch DDP (reference utils/trainer.py:206-214) — gradients after backward equal the
+    single-process gradients of the whole batch (mean losses, SyncBN statistics), on both the
+    fp32 and the bf16 wire.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _init(rank, world, port):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    return dist
+
+
+def _spawn(target, world, *args):
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
+    finally:
+        for p in procs:
+            p.join(120)
+            if p.is_alive():
+                p.kill()
+    for p in procs:
+        assert p.exitcode == 0
+    return res
+
+
+def _bn_inputs(dtype):
+    g = torch.Generator().manual_seed(0)
+    N, C, H, W = 4, 64, 8, 12
+    x = torch.randn(N, C, H, W, generator=g) * 2 + 0.5
+    gb = torch.randn(N, 2 * C, H, W, generator=g) * 0.3
+    gout = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(C, generator=g) * 0.5 + 1
+    b = torch.randn(C, generator=g) * 0.1
+    return x.to(dtype), gb.to(dtype), gout, w, b
+
+
+def _syncbn_worker(rank, world, port, q, dtype):
+    dist = _init(rank, world, port)
+    from imaginaire_amd.ops.norm import fused_norm_act
+    x, gb, gout, w, b = _bn_inputs(dtype)
+    n = x.shape[0] // world
+    sl = slice(rank * n, (rank + 1) * n)
+    cl = torch.channels_last
+    xr = x[sl].cuda().contiguous(memory_format=cl).requires_grad_(True)
+    gbr = gb[sl].cuda().contiguous(memory_format=cl).requires_grad_(True)
+    wr = w.cuda().requires_grad_(True)
+    br = b.cuda().requires_grad_(True)
+    rm = torch.zeros(x.shape[1], device='cuda')
+    rv = torch.ones(x.shape[1], device='cuda')
+    y = fused_norm_act(xr, 'sync_batch', wr, br, gb=gbr, running_mean=rm, running_var=rv,
+                       training=True, momentum=0.1, slope=0.2)
+    y.backward(gout[sl].cuda().to(y.dtype).contiguous(memory_format=cl))
+    torch.cuda.synchronize()
+    q.put((rank, y.float().cpu(), xr.grad.float().cpu(), gbr.grad.float().cpu(),
+           wr.grad.cpu(), br.grad.cpu(), rm.cpu(), rv.cpu()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_hip_syncbn_world2_matches_full_batch(dtype):
+    res = _spawn(_syncbn_worker, 2, dtype)
+    x, gb, gout, w, b = _bn_inputs(dtype)
+    C = x.shape[1]
+    xr = x.float().requires_grad_(True)
+    gbr = gb.float().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    rm, rv = torch.zeros(C), torch.ones(C)
+    yr = F.batch_norm(xr, rm, rv, wr, br, True, 0.1, 1e-5)
+    yr = F.leaky_relu(yr * (1 + gbr[:, :C]) + gbr[:, C:], 0.2)
+    yr.backward(gout)
+    tol = 3e-2 if dtype == torch.bfloat16 else 1e-4
+    y = torch.cat([r[1] for r in res])
+    dx = torch.cat([r[2] for r in res])
+    dgb = torch.cat([r[3] for r in res])
+    assert torch.allclose(y, yr, atol=tol * 4, rtol=tol), (y - yr).abs().max()
+    sc = float(xr.grad.abs().max())
+    assert torch.allclose(dx, xr.grad, atol=tol * 4 * sc, rtol=tol * 4), (dx - xr.grad).abs().max()
+    assert torch.allclose(dgb, gbr.grad, atol=tol * 4, rtol=tol * 4)
+    # per-rank affine gradients are partial sums over the rank's pixels (DDP averages them)
+    dw = res[0][4] + res[1][4]
+    db = res[0][5] + res[1][5]
+    assert torch.allclose(dw, wr.grad, atol=tol * 20, rtol=tol * 4), (dw - wr.grad).abs().max()
+    assert torch.allclose(db, br.grad, atol=tol * 20, rtol=tol * 4)
+    for r in res:  # running statistics of the GLOBAL batch on every rank
+        assert torch.allclose(r[6], rm, atol=1e-4, rtol=1e-3)
+        assert torch.allclose(r[7], rv, atol=1e-4, rtol=1e-3)
+
+
+def _spade_grads(rank, world, comm):
+    """G gradients of one SPADE G update (fp32, HIP path), rank's half of a 2-sample batch."""
+    from imaginaire_amd.config import Config
+    from imaginaire_amd.datasets.synthetic import DeviceBatchSource
+    from imaginaire_amd.utils.trainer import get_model_optimizer_and_scheduler, get_trainer
+    cfg = Config(os.path.join(ROOT, 'configs', 'unit_test', 'spade.yaml'))
+    cfg.logdir = '/tmp/iamd_ddp_test_%d' % rank
+    cfg.speed_benchmark = False
+    cfg.trainer.amp = 'O0'
+    cfg.trainer.model_average = False
+    cfg.trainer.ddp_bucket_mb = 1  # many buckets: exercises the per-bucket launch order
+    if comm:
+        cfg.trainer.ddp_comm_dtype = comm
+    nets = get_model_optimizer_and_scheduler(cfg, seed=0)
+    tr = get_trainer(cfg, *nets, train_data_loader=[], val_data_loader=None)
+    enc = tr.net_G_module.style_encoder
+    enc.freeze_random = True
+    style_dims = cfg.gen.style_dims
+    eps = torch.randn(2, style_dims, generator=torch.Generator().manual_seed(5)).cuda()
+    src = DeviceBatchSource(cfg, 2, torch.device('cuda', 0), pool=1, seed=0)
+    data = src.next()
+    n = 2 // world
+    sl = slice(rank * n, (rank + 1) * n)
+    data = {k: (v[sl].clone() if torch.is_tensor(v) and v.dim() > 0 and v.shape[0] == 2 else v)
+            for k, v in data.items()}
+    enc.eps = eps[sl]
+    data = tr.start_of_iteration(data, 0)
+    tr.gen_update(data)
+    torch.cuda.synchronize()
+    names, grads = [], []
+    for name, p in tr.net_G_module.named_parameters():
+        if p.grad is not None:
+            names.append(name)
+            grads.append(p.grad.detach().float().reshape(-1).cpu())
+    return names, torch.cat(grads)
+
+
+def _ddp_worker(rank, world, port, q, comm):
+    dist = _init(rank, world, port)
+    names, g = _spade_grads(rank, world, comm)
+    q.put((rank, names, g))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _ref_worker(rank, world, port, q):
+    torch.cuda.set_device(0)
+    names, g = _spade_grads(0, 1, None)
+    q.put((0, names, g))
+
+
+@pytest.mark.parametrize('comm', [None, 'bf16'])
+def test_ddp_spade_world2_grads_match_single_process(comm):
+    res = _spawn(_ddp_worker, 2, comm)
+    ref = _spawn(_ref_worker, 1)[0]
+    (_, n0, g0), (_, n1, g1) = res
+    assert n0 == n1 == ref[1], 'different parameter sets received gradients'
+    # both ranks hold the same (averaged) gradient
+    assert torch.equal(g0, g1)
+    gr = ref[2]
+    rel = float((g0 - gr).norm() / gr.norm())
+    assert rel < (2e-2 if comm else 2e-3), rel

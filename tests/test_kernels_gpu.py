@@ -496,3 +496,81 @@ def test_multi_tensor_l1_k13(dtype):
         assert torch.allclose(x.grad.float(), xr.grad, rtol=1e-2, atol=1e-8)
     # deterministic: the same value twice
     assert weighted_l1(a, b, ws).item() == weighted_l1(a, b, ws).item()
+
+
+@pytest.mark.parametrize('kernel_size', [1, 2])
+@pytest.mark.parametrize('layout', ['cl', 'nchw'])
+def test_resample2d_backward(kernel_size, layout):
+    """k7 backward (input gradient scatter + flow gradient) vs autograd through the fp32
+    reference warp (reference third_party/resample2d/src/resample2d_kernel.cu:79-203)."""
+    from imaginaire_amd.ops.flownet_ops import _Resample2dFn, resample2d_reference
+    torch.manual_seed(7)
+    img = torch.randn(2, 5, 19, 29, device='cuda')
+    if layout == 'cl':
+        img = img.contiguous(memory_format=torch.channels_last)
+    # fractional flows away from integer positions (the reference's flow gradient is
+    # discontinuous there) and partly out of frame (edge clamping)
+    flow = torch.randn(2, 2, 19, 29, device='cuda') * 4
+    flow = flow.round() + 0.1 + 0.8 * torch.rand_like(flow)
+    img.requires_grad_(True)
+    flow.requires_grad_(True)
+    out = _Resample2dFn.apply(img, flow, kernel_size)
+    ir = img.detach().clone().requires_grad_(True)
+    fr = flow.detach().clone().requires_grad_(True)
+    ref = resample2d_reference(ir, fr, kernel_size)
+    assert torch.allclose(out, ref, atol=1e-4, rtol=1e-4)
+    g = torch.randn_like(ref)
+    out.backward(g)
+    ref.backward(g)
+    assert torch.allclose(img.grad, ir.grad, atol=1e-4, rtol=1e-4), \
+        (img.grad - ir.grad).abs().max()
+    assert torch.allclose(flow.grad, fr.grad, atol=1e-3, rtol=1e-3), \
+        (flow.grad - fr.grad).abs().max()
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_partial_conv_renorm_backward(dtype):
+    """k3 renormalisation backward (raw and bias gradients) vs autograd of the reference."""
+    from imaginaire_amd.ops.partial_conv import partial_conv_renorm, _mask_stats_reference
+    torch.manual_seed(8)
+    raw = torch.randn(2, 16, 10, 12, device='cuda').to(dtype).requires_grad_(True)
+    mask = (torch.rand(2, 1, 10, 12, device='cuda') > 0.4).float()
+    bias = torch.randn(16, device='cuda', requires_grad=True)
+    out, upd = partial_conv_renorm(raw, mask, bias, 3, 1, 1, 1, 9.0)
+    ratio, update = _mask_stats_reference(mask, (3, 3), (1, 1), (1, 1), (1, 1), 9.0, 1e-6)
+    rr = raw.detach().float().requires_grad_(True)
+    br = bias.detach().clone().requires_grad_(True)
+    ref = (rr * ratio + br.view(1, -1, 1, 1)) * update
+    tol = 3e-2 if dtype == torch.bfloat16 else 1e-5
+    assert torch.allclose(out.float(), ref, atol=tol, rtol=tol)
+    g = torch.randn_like(ref)
+    out.backward(g.to(out.dtype))
+    ref.backward(g)
+    assert torch.allclose(raw.grad.float(), rr.grad, atol=tol * 4, rtol=tol * 4)
+    assert torch.allclose(bias.grad, br.grad, atol=tol * 40, rtol=tol * 4)
+
+
+def test_correlation_flownetc_shape():
+    """The FlowNetC configuration (reference flownet2/networks/flownet_c.py: Correlation(
+    pad_size=20, kernel_size=1, max_displacement=20, stride1=1, stride2=2) on 256-channel
+    conv3 features of a 512x1024 frame pair -> 64x128), bf16 through the MFMA forward."""
+    from imaginaire_amd.ops.flownet_ops import _CorrelationFn, correlation_reference
+    torch.manual_seed(9)
+    N, C, H, W = 1, 256, 64, 128
+    a = torch.randn(N, C, H, W, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last).requires_grad_(True)
+    b = torch.randn(N, C, H, W, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last).requires_grad_(True)
+    params = (20, 1, 20, 1, 2)
+    out = _CorrelationFn.apply(a, b, *params)
+    ar = a.detach().float().requires_grad_(True)
+    br = b.detach().float().requires_grad_(True)
+    ref = correlation_reference(ar, br, *params)
+    assert out.shape == ref.shape == (N, 441, H, W)
+    assert torch.allclose(out.float(), ref, atol=1e-2, rtol=2e-2), (out.float() - ref).abs().max()
+    go = torch.randn_like(ref) * 0.01
+    out.backward(go.to(torch.bfloat16))
+    ref.backward(go)
+    for got, want in ((a.grad, ar.grad), (b.grad, br.grad)):
+        err = (got.float() - want).abs().max() / want.abs().max()
+        assert err < 2e-2, err

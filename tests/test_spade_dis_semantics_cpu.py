@@ -1,0 +1,116 @@
+"""SPADE discriminator D-update semantics: ``dis.batch_real_fake`` (reference
+discriminators/spade.py:91-117 runs the real pass, then the fake pass, each refreshing the
+spectral-norm u/v once)."""
+import copy
+import os
+
+import pytest
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _dis(batch_real_fake, device='cpu'):
+    from imaginaire_amd.config import Config
+    from imaginaire_amd.discriminators.spade import Discriminator
+    cfg = Config(os.path.join(HERE, '..', 'configs', 'unit_test', 'spade.yaml'))
+    cfg.dis.num_filters = 8
+    cfg.dis.num_layers = 3
+    cfg.dis.batch_real_fake = batch_real_fake
+    torch.manual_seed(0)
+    return Discriminator(cfg.dis, cfg.data).to(device), cfg
+
+
+def _inputs(cfg, device='cpu', n=2, h=64, w=64):
+    from imaginaire_amd.utils.data import (get_paired_input_image_channel_number,
+                                           get_paired_input_label_channel_number)
+    g = torch.Generator().manual_seed(1)
+    c_img = get_paired_input_image_channel_number(cfg.data)
+    c_lab = get_paired_input_label_channel_number(cfg.data)
+    label = (torch.rand(n, c_lab, h, w, generator=g) > 0.8).float().to(device)
+    real = (torch.rand(n, c_img, h, w, generator=g) * 2 - 1).to(device)
+    fake = (torch.rand(n, c_img, h, w, generator=g) * 2 - 1).to(device)
+    return {'label': label, 'images': real}, {'fake_images': fake}
+
+
+def _sn_state(net):
+    return {k: v.clone() for k, v in net.state_dict().items()
+            if k.endswith(('weight_u', 'weight_v'))}
+
+
+def test_two_pass_matches_reference_order():
+    d, cfg = _dis(False)
+    assert not d.batched
+    ref = copy.deepcopy(d)
+    data, gout = _inputs(cfg)
+    with torch.no_grad():
+        out = d(data, gout)
+        # reference order: real pass, then fake pass, each one SN power iteration
+        r_out, r_feat = ref._single_forward(data['label'], data['images'])
+        f_out, f_feat = ref._single_forward(data['label'], gout['fake_images'])
+    for a, b in zip(out['real_outputs'], r_out):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+    for a, b in zip(out['fake_outputs'], f_out):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+    sa, sb = _sn_state(d), _sn_state(ref)
+    assert sa.keys() == sb.keys() and len(sa) > 0
+    for k in sa:
+        torch.testing.assert_close(sa[k], sb[k], rtol=0, atol=0)
+
+
+def test_batched_runs_one_power_iteration_per_update():
+    d2, cfg = _dis(False)
+    d1 = copy.deepcopy(d2)
+    d1.batched = True
+    u0 = _sn_state(d1)
+    data, gout = _inputs(cfg)
+    with torch.no_grad():
+        out1 = d1(data, gout)
+        out2 = d2(data, gout)
+    # real half of the batched pass == the reference's real pass (same single iteration)
+    for a, b in zip(out1['real_outputs'], out2['real_outputs']):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
+    # the two-pass path iterated u/v twice, the batched path once: states differ
+    one = _sn_state(d1)
+    two = _sn_state(d2)
+    assert any(not torch.equal(one[k], two[k]) for k in one)
+    assert any(not torch.equal(one[k], u0[k]) for k in one)
+    # the fake-pass outputs agree up to the (tiny) change of σ between iterations
+    for a, b in zip(out1['fake_outputs'], out2['fake_outputs']):
+        torch.testing.assert_close(a, b, rtol=5e-2, atol=5e-2)
+
+
+def test_g_update_never_batches():
+    d, cfg = _dis(True)
+    assert d.batched
+    data, gout = _inputs(cfg)
+    gout['fake_images'].requires_grad_(True)
+    out = d(data, gout)
+    loss = sum(o.mean() for o in out['fake_outputs'])
+    loss.backward()
+    assert gout['fake_images'].grad is not None
+    assert out['real_outputs'][0].shape[0] == data['images'].shape[0]
+
+
+@pytest.mark.gpu
+def test_two_pass_order_with_batched_sn_hook_gpu():
+    """On the GPU the network-level batched SN hook serves the FIRST pass; the second pass
+    of the same forward must fall back to its own power iteration (reference order)."""
+    if not torch.cuda.is_available():
+        pytest.skip('needs a GPU')
+    from imaginaire_amd.layers.spectral_norm import install_batched_spectral_norm
+    d_cpu, cfg = _dis(False)
+    d_gpu = copy.deepcopy(d_cpu).cuda()
+    assert install_batched_spectral_norm(d_gpu) > 0
+    data, gout = _inputs(cfg)
+    gdata = {k: v.cuda() for k, v in data.items()}
+    ggout = {k: v.cuda() for k, v in gout.items()}
+    with torch.no_grad():
+        oc = d_cpu(data, gout)
+        og = d_gpu(gdata, ggout)
+    for key in ('real_outputs', 'fake_outputs'):
+        for a, b in zip(oc[key], og[key]):
+            torch.testing.assert_close(b.float().cpu(), a, rtol=2e-3, atol=2e-3)
+    sc, sg = _sn_state(d_cpu), _sn_state(d_gpu)
+    for k in sc:
+        torch.testing.assert_close(sg[k].cpu(), sc[k], rtol=1e-3, atol=1e-4)
