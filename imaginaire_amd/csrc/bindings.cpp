@@ -55,6 +55,10 @@ at::Tensor resize_bilinear_fwd(const at::Tensor& x, int64_t Ho, int64_t Wo, doub
                                const c10::optional<at::Tensor>& add);
 at::Tensor resize_bilinear_bwd(const at::Tensor& dy, int64_t H, int64_t W, double scale_h,
                                double scale_w, bool align_corners);
+at::Tensor resize_nearest_fwd(const at::Tensor& x, int64_t Ho, int64_t Wo, double scale_h,
+                              double scale_w);
+at::Tensor resize_nearest_bwd(const at::Tensor& dy, int64_t H, int64_t W, double scale_h,
+                              double scale_w);
 bool stream_capturing();
 void mt_scale(const std::vector<at::Tensor>& xs, const at::Tensor& s);
 at::Tensor mt_sqnorm(const std::vector<at::Tensor>& xs);
@@ -80,7 +84,14 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
                        double slope);
 at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t KH, int64_t KW,
                              int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh,
-                             int64_t dw);
+                             int64_t dw, int64_t out_cout, int64_t out_cin, bool out_bf16);
+at::Tensor conv2d_dgrad_strided_mfma(const at::Tensor& dy, const at::Tensor& w, int64_t H,
+                                     int64_t W, int64_t s, int64_t ph, int64_t pw);
+// conv_aux.hip
+at::Tensor conv_weight_flip_t(const at::Tensor& w, int64_t s, int64_t qy, int64_t qx);
+at::Tensor wgrad_finalize(const at::Tensor& part, int64_t S, int64_t Cop, int64_t Cip,
+                          int64_t Cout, int64_t Cin, int64_t KH, int64_t KW,
+                          at::ScalarType dtype);
 at::Tensor sn_scale_backward(const at::Tensor& grad_in, const at::Tensor& weight,
                              const at::Tensor& u, const at::Tensor& v, const at::Tensor& sigma);
 void register_lmdb(pybind11::module_& m);
@@ -98,7 +109,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mt_sn_scale_cast", &iamd::mt_sn_scale_cast, "batched W/sigma -> bf16 (k5c)");
   m.def("profile_marker", &iamd::profile_marker, "named no-op kernel for trace phase splits");
   m.def("conv2d_mfma", &iamd::conv2d_mfma, "MFMA implicit-GEMM NHWC conv + bias + act (k10)");
-  m.def("conv2d_wgrad_mfma", &iamd::conv2d_wgrad_mfma, "MFMA conv weight gradient (k11)");
+  m.def("conv2d_wgrad_mfma", &iamd::conv2d_wgrad_mfma, "MFMA conv weight gradient (k11)",
+        py::arg("dy"), py::arg("x"), py::arg("KH"), py::arg("KW"), py::arg("sh"), py::arg("sw"),
+        py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("out_cout") = -1,
+        py::arg("out_cin") = -1, py::arg("out_bf16") = false);
+  m.def("conv2d_dgrad_strided_mfma", &iamd::conv2d_dgrad_strided_mfma,
+        "stride-s conv data gradient on k10 (s*s phase convs, strided epilogue)");
+  m.def("conv_weight_flip_t", &iamd::conv_weight_flip_t,
+        "flipped, in/out-transposed channels-last conv weight (dgrad-as-conv); s/qy/qx select "
+        "the taps of one stride-s phase", py::arg("w"), py::arg("s") = 1, py::arg("qy") = 0,
+        py::arg("qx") = 0);
   m.def("sn_scale_backward", &iamd::sn_scale_backward, "spectral-norm W/sigma backward (k5d)");
   m.def("norm_stats", &iamd::norm_stats, "per-(group,channel) statistics (k1)");
   m.def("norm_apply", &iamd::norm_apply, "norm + SPADE modulation + activation (k1 fwd)");
@@ -127,6 +147,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("resize_bilinear_fwd", &iamd::resize_bilinear_fwd,
         "NHWC bilinear resize (+ residual) (k12)");
   m.def("resize_bilinear_bwd", &iamd::resize_bilinear_bwd, "k12 backward (gather)");
+  m.def("resize_nearest_fwd", &iamd::resize_nearest_fwd, "NHWC nearest resize (k12)");
+  m.def("resize_nearest_bwd", &iamd::resize_nearest_bwd, "k12 nearest backward (gather)");
   m.def("flow_warp_fwd", &iamd::flow_warp_fwd, "bilinear flow warp, border (k9)");
   m.def("flow_warp_bwd", &iamd::flow_warp_bwd, "k9 backward");
   m.def("resample2d_forward", &iamd::resample2d_forward, "FlowNet2 Resample2d (k7)");

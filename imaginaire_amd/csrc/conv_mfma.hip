@@ -57,7 +57,20 @@ struct ConvArgs {
   int kps;          // k-steps per split (split-K: blockIdx.y = split)
   float* part;      // split-K fp32 partial slabs [S][M][Cout] (nullptr: direct epilogue)
   float slope;
+  // output-pixel mapping (phase-decomposed stride-2 data gradient): GEMM row m = (b, oh, ow)
+  // is stored at pixel (b, oh * osy + ory, ow * osx + orx) of a [B, oH, oW, Cout] tensor.
+  // omode 0: identity (row m is pixel m)
+  int omode, oH, oW, osy, osx, ory, orx;
 };
+
+// destination pixel (row of the NHWC output) of GEMM row m
+__device__ __forceinline__ size_t out_row(const ConvArgs& a, int m) {
+  if (!a.omode) return (size_t)m;
+  const int HoWo = a.Ho * a.Wo;
+  const int b = m / HoWo, r = m - b * HoWo;
+  const int oh = r / a.Wo, ow = r - oh * a.Wo;
+  return ((size_t)b * a.oH + oh * a.osy + a.ory) * a.oW + ow * a.osx + a.orx;
+}
 
 // BM = 128 (4 waves, 2 blocks/CU) or 256 (8 waves, 1 block/CU: the B tile is shared by twice
 // the pixels, 25% fewer L2->LDS bytes per MFMA); waves form a (BM/64) x 2 grid.
@@ -241,7 +254,7 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_fwd_mfma(ConvA
     const int m = m0 + rl;
     if (m < a.M) {
       const uint4 v = *reinterpret_cast<const uint4*>(E + rl * kEpiStride + ch * 16);
-      *reinterpret_cast<uint4*>(a.y + (size_t)m * a.Cout + n0 + ch * 8) = v;
+      *reinterpret_cast<uint4*>(a.y + out_row(a, m) * a.Cout + n0 + ch * 8) = v;
     }
   }
 #endif  // __HIP_DEVICE_COMPILE__
@@ -437,7 +450,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v2(ConvArgs a) {
     const int m = m0 + rl;
     if (m < a.M) {
       const uint4 v = *reinterpret_cast<const uint4*>(E + rl * kEpiStride + ch * 16);
-      *reinterpret_cast<uint4*>(a.y + (size_t)m * a.Cout + n0 + ch * 8) = v;
+      *reinterpret_cast<uint4*>(a.y + out_row(a, m) * a.Cout + n0 + ch * 8) = v;
     }
   }
 #endif  // __HIP_DEVICE_COMPILE__
@@ -690,7 +703,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v3(ConvArgs a) {
       const int m = m0 + rl;
       if (m < a.M) {
         const uint4 v = *reinterpret_cast<const uint4*>(E + rl * kEpiStride + ch * 16);
-        *reinterpret_cast<uint4*>(a.y + (size_t)m * a.Cout + n0 + half * 128 + ch * 8) = v;
+        *reinterpret_cast<uint4*>(a.y + out_row(a, m) * a.Cout + n0 + half * 128 + ch * 8) = v;
       }
     }
     __syncthreads();
@@ -701,7 +714,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v3(ConvArgs a) {
 // y = act(sum_s part[s] + bias) in bf16, 8 channels per thread.
 __global__ void __launch_bounds__(256)
 conv_splitk_reduce(const float* __restrict__ part, const float* __restrict__ bias,
-                   __hip_bfloat16* __restrict__ y, int S, int64_t MC, int C, float slope) {
+                   __hip_bfloat16* __restrict__ y, int S, int64_t MC, int C, float slope,
+                   ConvArgs map) {
   for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < MC / 8;
        v += (int64_t)gridDim.x * blockDim.x) {
     const int64_t e = v * 8;
@@ -722,56 +736,19 @@ conv_splitk_reduce(const float* __restrict__ part, const float* __restrict__ bia
       float t = acc[k] + (bias ? bias[c + k] : 0.f);
       acc[k] = t > 0.f ? t : t * slope;
     }
-    store_vec<__hip_bfloat16, 8>(y + e, acc);
+    const int64_t m = e / C;
+    store_vec<__hip_bfloat16, 8>(y + out_row(map, (int)m) * C + (e - m * C), acc);
   }
 }
 
 }  // namespace
 
-// y[B, Cout, Ho, Wo] (channels-last) = act(conv2d(x, w) + bias), x/w channels-last bf16.
-at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
-                       int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
-                       double slope) {
-  IAMD_CHECK(x.is_cuda() && w.is_cuda(), "conv2d_mfma: CUDA tensors expected");
-  IAMD_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16,
-             "conv2d_mfma: bf16 operands expected");
-  IAMD_CHECK(x.dim() == 4 && w.dim() == 4, "conv2d_mfma: 4-D tensors expected");
-  IAMD_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
-                 w.is_contiguous(at::MemoryFormat::ChannelsLast),
-             "conv2d_mfma: packed channels-last operands expected");
-  const int B = (int)x.size(0), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
-  const int Cout = (int)w.size(0), KH = (int)w.size(2), KW = (int)w.size(3);
-  IAMD_CHECK(w.size(1) == Cin, "conv2d_mfma: channel mismatch ", w.size(1), " vs ", Cin);
-  IAMD_CHECK(Cin % kBK == 0, "conv2d_mfma: Cin must be a multiple of 64, got ", Cin);
-  IAMD_CHECK(Cout % 64 == 0, "conv2d_mfma: Cout must be a multiple of 64, got ", Cout);
-  IAMD_CHECK(sh >= 1 && sw >= 1 && dh >= 1 && dw >= 1 && ph >= 0 && pw >= 0, "conv2d_mfma: bad geometry");
-  const int Ho = (int)((H + 2 * ph - dh * (KH - 1) - 1) / sh + 1);
-  const int Wo = (int)((W + 2 * pw - dw * (KW - 1) - 1) / sw + 1);
-  IAMD_CHECK(Ho > 0 && Wo > 0, "conv2d_mfma: empty output");
-  IAMD_CHECK((int64_t)B * H * W * Cin * 2 < kOobOffset && w.numel() * 2 < kOobOffset &&
-                 (int64_t)B * Ho * Wo * Cout < (1ll << 31),
-             "conv2d_mfma: tensor too large for 32-bit buffer offsets");
-  IAMD_CHECK(KH <= 32 && KW <= 32, "conv2d_mfma: filter larger than 32x32");
-  auto y = at::empty({B, Cout, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  at::Tensor bf;
-  if (bias.has_value() && bias->defined()) {
-    IAMD_CHECK(bias->numel() == Cout, "conv2d_mfma: bias size");
-    bf = bias->to(at::kFloat).contiguous();
-  }
-  ConvArgs a;
-  a.x = reinterpret_cast<const __hip_bfloat16*>(x.data_ptr());
-  a.w = reinterpret_cast<const __hip_bfloat16*>(w.data_ptr());
-  a.bias = bf.defined() ? bf.data_ptr<float>() : nullptr;
-  a.y = reinterpret_cast<__hip_bfloat16*>(y.data_ptr());
-  a.xbytes = (int)(x.numel() * 2);
-  a.wbytes = (int)(w.numel() * 2);
-  a.KH = KH;
-  a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
-  a.KW = KW; a.sh = (int)sh; a.sw = (int)sw; a.ph = (int)ph; a.pw = (int)pw; a.dh = (int)dh; a.dw = (int)dw;
-  a.M = B * Ho * Wo;
-  a.cpt = Cin / kBK;
-  a.nk = KH * KW * a.cpt;
-  a.slope = (float)slope;
+namespace {
+
+// Kernel choice, split-K and launch for a filled-in ConvArgs (x supplies the tensor options of
+// the split-K slabs).
+void run_conv(ConvArgs& a, const at::Tensor& x) {
+  const int Cout = a.Cout, KH = a.KH, KW = a.KW;
   const bool bn128 = Cout % 128 == 0;
   // Kernel choice (IMAGINAIRE_AMD_CONV_V = 0 auto | 1 | 2 | 3 forces one):
   //  v3 — 8-phase 256 x 256 (Cout % 256 == 0) or 512 x 128 (Cout % 128 == 0) tile, one block
@@ -881,10 +858,130 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
     const int64_t MC = (int64_t)a.M * Cout;
     const int blocks = (int)std::min<int64_t>((MC / 8 + 255) / 256, 8192);
     hipLaunchKernelGGL(conv_splitk_reduce, dim3(blocks), dim3(256), 0, stream(), a.part, a.bias,
-                       a.y, S, MC, Cout, a.slope);
+                       a.y, S, MC, Cout, a.slope, a);
   }
   IAMD_LAUNCH_CHECK();
+}
+
+}  // namespace
+
+// y[B, Cout, Ho, Wo] (channels-last) = act(conv2d(x, w) + bias), x/w channels-last bf16.
+at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                       int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
+                       double slope) {
+  IAMD_CHECK(x.is_cuda() && w.is_cuda(), "conv2d_mfma: CUDA tensors expected");
+  IAMD_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16,
+             "conv2d_mfma: bf16 operands expected");
+  IAMD_CHECK(x.dim() == 4 && w.dim() == 4, "conv2d_mfma: 4-D tensors expected");
+  IAMD_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                 w.is_contiguous(at::MemoryFormat::ChannelsLast),
+             "conv2d_mfma: packed channels-last operands expected");
+  const int B = (int)x.size(0), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int Cout = (int)w.size(0), KH = (int)w.size(2), KW = (int)w.size(3);
+  IAMD_CHECK(w.size(1) == Cin, "conv2d_mfma: channel mismatch ", w.size(1), " vs ", Cin);
+  IAMD_CHECK(Cin % kBK == 0, "conv2d_mfma: Cin must be a multiple of 64, got ", Cin);
+  IAMD_CHECK(Cout % 64 == 0, "conv2d_mfma: Cout must be a multiple of 64, got ", Cout);
+  IAMD_CHECK(sh >= 1 && sw >= 1 && dh >= 1 && dw >= 1 && ph >= 0 && pw >= 0, "conv2d_mfma: bad geometry");
+  const int Ho = (int)((H + 2 * ph - dh * (KH - 1) - 1) / sh + 1);
+  const int Wo = (int)((W + 2 * pw - dw * (KW - 1) - 1) / sw + 1);
+  IAMD_CHECK(Ho > 0 && Wo > 0, "conv2d_mfma: empty output");
+  IAMD_CHECK((int64_t)B * H * W * Cin * 2 < kOobOffset && w.numel() * 2 < kOobOffset &&
+                 (int64_t)B * Ho * Wo * Cout < (1ll << 31),
+             "conv2d_mfma: tensor too large for 32-bit buffer offsets");
+  IAMD_CHECK(KH <= 32 && KW <= 32, "conv2d_mfma: filter larger than 32x32");
+  auto y = at::empty({B, Cout, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor bf;
+  if (bias.has_value() && bias->defined()) {
+    IAMD_CHECK(bias->numel() == Cout, "conv2d_mfma: bias size");
+    bf = bias->to(at::kFloat).contiguous();
+  }
+  ConvArgs a;
+  a.x = reinterpret_cast<const __hip_bfloat16*>(x.data_ptr());
+  a.w = reinterpret_cast<const __hip_bfloat16*>(w.data_ptr());
+  a.bias = bf.defined() ? bf.data_ptr<float>() : nullptr;
+  a.y = reinterpret_cast<__hip_bfloat16*>(y.data_ptr());
+  a.xbytes = (int)(x.numel() * 2);
+  a.wbytes = (int)(w.numel() * 2);
+  a.KH = KH;
+  a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
+  a.KW = KW; a.sh = (int)sh; a.sw = (int)sw; a.ph = (int)ph; a.pw = (int)pw; a.dh = (int)dh; a.dw = (int)dw;
+  a.M = B * Ho * Wo;
+  a.cpt = Cin / kBK;
+  a.nk = KH * KW * a.cpt;
+  a.slope = (float)slope;
+  a.omode = 0;
+  a.oH = Ho; a.oW = Wo; a.osy = 1; a.osx = 1; a.ory = 0; a.orx = 0;
+  run_conv(a, x);
   return y;
+}
+
+// conv_aux.hip
+at::Tensor conv_weight_flip_t(const at::Tensor& w, int64_t s, int64_t qy, int64_t qx);
+
+// Data gradient of a stride-s conv (s = sh = sw > 1, dilation 1) on k10 by phase decomposition:
+// output pixel (s*a + ry, s*c + rx) of dx only receives the taps kh = qy + s*j (qy = (ry + ph)
+// mod s) and kw = qx + s*j, so each of the s*s phases is a STRIDE-1 conv of dy with the
+// sub-kernel w[:, :, qy::s, qx::s] (flipped, in/out transposed) whose outputs the epilogue
+// scatters to the strided pixel positions (ConvArgs output mapping). Replaces MIOpen's
+// stride-2 backward-data kernels (~200 TF/s on the SPADE discriminator / style-encoder shapes,
+// profiles/spade_step_conv_log_mi355x.txt).
+// dy [B, Cout, Ho, Wo] bf16 CL, w [Cout, Cin, KH, KW] bf16 CL (Cin, Cout % 64 == 0) -> dx
+// [B, Cin, H, W] bf16 CL.
+at::Tensor conv2d_dgrad_strided_mfma(const at::Tensor& dy, const at::Tensor& w, int64_t H,
+                                     int64_t W, int64_t s, int64_t ph, int64_t pw) {
+  IAMD_CHECK(dy.is_cuda() && w.is_cuda() && dy.scalar_type() == at::kBFloat16 &&
+                 w.scalar_type() == at::kBFloat16 && dy.dim() == 4 && w.dim() == 4,
+             "conv2d_dgrad_strided_mfma: bf16 4-D CUDA tensors expected");
+  IAMD_CHECK(dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                 w.is_contiguous(at::MemoryFormat::ChannelsLast),
+             "conv2d_dgrad_strided_mfma: packed channels-last dy / w expected");
+  const int B = (int)dy.size(0), Cout = (int)dy.size(1), Ho = (int)dy.size(2), Wo = (int)dy.size(3);
+  const int Cin = (int)w.size(1), K_h = (int)w.size(2), K_w = (int)w.size(3);
+  IAMD_CHECK(w.size(0) == Cout && Cin % 64 == 0 && Cout % 64 == 0 && s >= 2 && s <= 4,
+             "conv2d_dgrad_strided_mfma: channels must be multiples of 64, stride 2..4");
+  IAMD_CHECK(Ho == (H + 2 * ph - K_h) / s + 1 && Wo == (W + 2 * pw - K_w) / s + 1,
+             "conv2d_dgrad_strided_mfma: dy size does not match the conv geometry");
+  IAMD_CHECK((int64_t)B * Ho * Wo * Cout * 2 < kOobOffset && (int64_t)B * H * W * Cin < (1ll << 31),
+             "conv2d_dgrad_strided_mfma: tensor too large for 32-bit offsets");
+  bool empty_phase = false;
+  for (int r = 0; r < s; ++r)
+    if ((r + ph) % s >= K_h || (r + pw) % s >= K_w) empty_phase = true;
+  auto opts = dy.options().memory_format(at::MemoryFormat::ChannelsLast);
+  auto dx = empty_phase ? at::zeros({B, Cin, H, W}, opts) : at::empty({B, Cin, H, W}, opts);
+  for (int ry = 0; ry < s; ++ry) {
+    const int qy = (int)((ry + ph) % s);
+    const int Jy = qy < K_h ? (K_h - qy + (int)s - 1) / (int)s : 0;
+    const int Ay = (int)((H - ry + s - 1) / s);
+    for (int rx = 0; rx < s; ++rx) {
+      const int qx = (int)((rx + pw) % s);
+      const int Jx = qx < K_w ? (K_w - qx + (int)s - 1) / (int)s : 0;
+      const int Ax = (int)((W - rx + s - 1) / s);
+      if (Jy == 0 || Jx == 0 || Ay <= 0 || Ax <= 0) continue;
+      const int cy = (int)((ry + ph - qy) / s), cx = (int)((rx + pw - qx) / s);
+      // wsub[ci][j'y][j'x][co] = w[co][qy + s (Jy-1-j'y)][qx + s (Jx-1-j'x)][ci]
+      auto wsub = conv_weight_flip_t(w, s, qy, qx);
+      ConvArgs a;
+      a.x = reinterpret_cast<const __hip_bfloat16*>(dy.data_ptr());
+      a.w = reinterpret_cast<const __hip_bfloat16*>(wsub.data_ptr());
+      a.bias = nullptr;
+      a.y = reinterpret_cast<__hip_bfloat16*>(dx.data_ptr());
+      a.xbytes = (int)(dy.numel() * 2);
+      a.wbytes = (int)(wsub.numel() * 2);
+      a.H = Ho; a.W = Wo; a.Cin = Cout; a.Cout = Cin;
+      a.Ho = Ay; a.Wo = Ax;
+      a.KH = Jy; a.KW = Jx;
+      a.sh = 1; a.sw = 1; a.dh = 1; a.dw = 1;
+      a.ph = Jy - 1 - cy; a.pw = Jx - 1 - cx;
+      a.M = B * Ay * Ax;
+      a.cpt = Cout / kBK;
+      a.nk = Jy * Jx * a.cpt;
+      a.slope = 1.f;
+      a.omode = 1;
+      a.oH = (int)H; a.oW = (int)W; a.osy = (int)s; a.osx = (int)s; a.ory = ry; a.orx = rx;
+      run_conv(a, dy);
+    }
+  }
+  return dx;
 }
 
 }  // namespace iamd

@@ -19,7 +19,8 @@
 // out-of-range offset and read as zeros; when Wo % 64 == 0 a k-step is one output-row
 // segment and its pixel coordinates are wave-uniform scalars. Partial sums per split are
 // written as fp32 slabs [S][Cout][taps][Cin] and summed by a second, bandwidth-bound kernel
-// (one slab, S == 1, is written straight into dW).
+// that also crops padded channels and casts to the parameter dtype (conv_aux.hip
+// wgrad_finalize); one fp32 uncropped slab (S == 1) is written straight into dW.
 //
 // Reference: the reference's weight gradients come from cuDNN through nn.Conv2d autograd
 // (layers/conv.py:59-91); there is no hand-written conv in the reference.
@@ -247,25 +248,193 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma(WgradArgs a) {
 #endif  // __HIP_DEVICE_COMPILE__
 }
 
-__global__ void sum_splits(const float4* __restrict__ P, float4* __restrict__ out, int S,
-                           int64_t n4) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    float4 s = P[i];
-    for (int k = 1; k < S; ++k) {
-      const float4 v = P[k * n4 + i];
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-    }
-    out[i] = s;
+// ---- k11 multi-tap: one block computes ALL KW taps of one filter row ------------------------
+//
+// For a stride-1 conv whose output rows are whole 64-pixel k-steps (Wo % 64 == 0), the KW taps
+// (ky, 0..KW-1) of one filter row read the SAME dy tile and the same input row shifted by kx
+// pixels. The block stages the dy tile (64 px x BNO) and ONE input-row window of 64 + KW - 1
+// pixels x BC once per k-step and runs the KW tap products from LDS (the x fragment of tap kx is
+// the window read kx rows further down), so every staged byte feeds KW times the MFMAs of the
+// one-tap kernel: 3x / 5x fewer L2 -> LDS bytes per FLOP on the 3x3 / 5x5 SPADE convs, and the dy
+// fragments are read from LDS once for all taps. Accumulators: KW x (BNO/2 x BC/2) per wave
+// (tiles: 3 taps 128 x 64, 5 taps 64 x 64 — the 256-VGPR budget of 2 waves / SIMD, no spills).
+template <int BNO, int BC, int NT>
+__global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma_mt(WgradArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  constexpr int RA = BNO * 2, RX = BC * 2;        // image row bytes
+  constexpr int kAbytes = kBP * RA;
+  constexpr int kXrows = kBP + 1024 / RX;           // window + one extra wave-DMA of halo rows
+  static_assert(NT - 1 <= 1024 / RX, "halo rows must fit one extra wave DMA");
+  constexpr int kXbytes = kXrows * RX;
+  constexpr int kStage = kAbytes + kXbytes;
+  constexpr int MI = BNO / 32, NI = BC / 32;
+  constexpr int CPA = RA / 16, CPX = RX / 16;
+  constexpr int LA = kBP * CPA / kThreads;
+  constexpr int LX = kBP * CPX / kThreads;
+  constexpr int RSA = kThreads / CPA, RSX = kThreads / CPX;
+  __shared__ __attribute__((aligned(16))) char smem[2 * kStage];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tiles = a.KK / a.KW * a.nNt * a.nCt;    // (ky, n-tile, c-tile)
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / tiles;
+  const int tile = bid - split * tiles;
+  const int ky = tile / (a.nNt * a.nCt);
+  const int r2 = tile - ky * a.nNt * a.nCt;
+  const int nt = r2 / a.nCt, ct = r2 - nt * a.nCt;
+  const int n0 = nt * BNO, c0 = ct * BC;
+  const int ks0 = split * a.kps;
+  const int ks1 = min(a.nks, ks0 + a.kps);
+
+  const __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__hip_bfloat16*>(a.dy), 0, a.dybytes, kBufCfg);
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__hip_bfloat16*>(a.x), 0, a.xbytes, kBufCfg);
+  const int arow0 = tid / CPA, apos = tid % CPA;
+  const int xrow0 = tid / CPX, xpos = tid % CPX;
+  const int dyc = n0 + ((apos ^ swz<RA>(arow0)) << 3);
+  const int xc = c0 + ((xpos ^ swz<RX>(xrow0)) << 3);
+  int dy_off[LA];
+#pragma unroll
+  for (int i = 0; i < LA; ++i) dy_off[i] = ((arow0 + i * RSA) * a.Cout + dyc) * 2;
+  const int dy_step = kBP * a.Cout * 2;
+  // halo rows 64.. of the window: wave 0 only, one lane-linear 1 KB DMA
+  const int hrow = kBP + lane / CPX;
+  const int hxc = c0 + (((lane % CPX) ^ swz<RX>(hrow)) << 3);
+  const int HoWo = a.Ho * a.Wo;
+  int sb, soh, sow;
+  {
+    const int m = ks0 * kBP;
+    sb = m / HoWo;
+    const int r = m - sb * HoWo;
+    soh = r / a.Wo;
+    sow = r - soh * a.Wo;
   }
+
+  auto issue = [&](int ks, int buf) {
+    char* As = smem + buf * kStage;
+    char* Xs = As + kAbytes;
+#pragma unroll
+    for (int i = 0; i < LA; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(dyr, (lds_ptr_t)(As + i * 4096 + wid * 1024), 16,
+                                               dy_off[i], ks * dy_step, 0, 0);
+    const int ih = soh * a.sh - a.ph + ky * a.dh;
+    const bool rowok = sb < a.Bn && (unsigned)ih < (unsigned)a.H;
+    const int soff = rowok ? (sb * a.H + ih) * a.W * a.Cin * 2 : 0;
+    const int iw0 = sow - a.pw;  // input column of window row 0 (stride 1)
+#pragma unroll
+    for (int i = 0; i < LX; ++i) {
+      const int iw = iw0 + xrow0 + i * RSX;
+      const bool ok = rowok && (unsigned)iw < (unsigned)a.W;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(Xs + i * 4096 + wid * 1024), 16,
+                                               ok ? (iw * a.Cin + xc) * 2 : kOobOffset, soff, 0,
+                                               0);
+    }
+    if (wid == 0) {
+      const int iw = iw0 + hrow;
+      const bool ok = rowok && (unsigned)iw < (unsigned)a.W;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(Xs + kBP * RX), 16,
+                                               ok ? (iw * a.Cin + hxc) * 2 : kOobOffset, soff, 0,
+                                               0);
+    }
+  };
+  auto advance = [&]() {
+    sow += kBP;
+    if (sow >= a.Wo) {
+      sow = 0;
+      if (++soh >= a.Ho) { soh = 0; ++sb; }
+    }
+  };
+
+  f32x4 acc[NT][MI][NI];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  auto a_addr = [&](int row, int colblk) {
+    return row * RA + ((((colblk + (p >> 1)) ^ swz<RA>(row))) << 4) + ((p & 1) << 3);
+  };
+  auto x_addr = [&](int row, int colblk) {
+    return row * RX + ((((colblk + (p >> 1)) ^ swz<RX>(row))) << 4) + ((p & 1) << 3);
+  };
+
+  issue(ks0, 0);
+  for (int ks = ks0; ks < ks1; ++ks) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (ks + 1 < ks1) {
+      advance();
+      issue(ks + 1, (ks + 1 - ks0) & 1);
+    }
+    const char* As = smem + ((ks - ks0) & 1) * kStage;
+    const char* Xs = As + kAbytes;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int r0 = kk * 32 + g * 8 + q;
+      bf16x8 af[MI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int cb = (wm * (BNO / 2) + i * 16) >> 3;
+        const bf16x4 lo = tr_read(As + a_addr(r0, cb));
+        const bf16x4 hi = tr_read(As + a_addr(r0 + 4, cb));
+        af[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        bf16x8 xf[NI];
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int cb = (wn * (BC / 2) + j * 16) >> 3;
+          const bf16x4 lo = tr_read(Xs + x_addr(r0 + t, cb));
+          const bf16x4 hi = tr_read(Xs + x_addr(r0 + t + 4, cb));
+          xf[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], xf[j], acc[t][i][j],
+                                                                   0, 0, 0);
+      }
+    }
+  }
+
+  float* o = a.out + (size_t)split * a.Cout * a.KK * a.Cin;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int tap = ky * a.KW + t;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = n0 + wm * (BNO / 2) + i * 16 + g * 4 + r;
+          const int ci = c0 + wn * (BC / 2) + j * 16 + (lane & 15);
+          o[((size_t)n * a.KK + tap) * a.Cin + ci] = acc[t][i][j][r];
+        }
+  }
+#endif  // __HIP_DEVICE_COMPILE__
 }
 
 }  // namespace
 
-// dW [Cout, Cin, KH, KW] fp32 (channels-last memory = [Cout][KH][KW][Cin]).
+// conv_aux.hip: split-K sum + channel crop + dtype cast of the slabs
+at::Tensor wgrad_finalize(const at::Tensor& part, int64_t S, int64_t Cop, int64_t Cip,
+                          int64_t Cout, int64_t Cin, int64_t KH, int64_t KW,
+                          at::ScalarType dtype);
+
+// dW [out_cout, out_cin, KH, KW] (channels-last memory = [Cout][KH][KW][Cin]) in fp32, or bf16
+// when out_bf16; out_cout / out_cin < 0 keep the (padded) channel counts of dy / x. Cropping
+// and casting ride in the split-K reduction (wgrad_finalize) instead of separate copies.
 at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t KH, int64_t KW,
                              int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh,
-                             int64_t dw) {
+                             int64_t dw, int64_t out_cout, int64_t out_cin, bool out_bf16) {
   IAMD_CHECK(dy.is_cuda() && x.is_cuda(), "conv2d_wgrad_mfma: CUDA tensors expected");
   IAMD_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16,
              "conv2d_wgrad_mfma: bf16 operands expected");
@@ -296,12 +465,21 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
   a.nks = ceil_div(a.M, kBP);
   a.nNt = Cout / (bno128 ? 128 : 64);
   a.nCt = Cin / (bc128 ? 128 : 64);
-  const int tiles = KK * a.nNt * a.nCt;
+  // multi-tap kernel: stride-1, undilated, whole-row k-steps, KW in {3, 5}
+  const char* mt_env = std::getenv("IMAGINAIRE_AMD_WGRAD_MT");
+  const bool mt = (mt_env == nullptr || mt_env[0] != '0') && Wo % kBP == 0 && sw == 1 &&
+                  dw == 1 && (KW == 3 || KW == 5);
+  if (mt) {  // tiles sized to the 256-VGPR budget of 2 waves / SIMD without spills:
+    // 3 taps 128 x 64 (or 64 x 64), 5 taps 64 x 64
+    a.nNt = Cout / ((KW == 3 && bno128) ? 128 : 64);
+    a.nCt = Cin / 64;
+  }
+  const int tiles = (mt ? (int)KH : KK) * a.nNt * a.nCt;
   // split-K factor: fill the chip in whole rounds of co-resident blocks (2 / 3 / 5 blocks
   // per CU for the 64 / 48 / 32 KB LDS variants): a 2.3-round grid leaves the last round a
   // third full (measured: 1200 blocks ran at 28% MFMA issue vs 44% for k10,
   // profiles/pmc_conv_mi355x.txt)
-  const int slots = 256 * ((bno128 && bc128) ? 2 : (bno128 || bc128) ? 3 : 5);
+  const int slots = mt ? 512 : 256 * ((bno128 && bc128) ? 2 : (bno128 || bc128) ? 3 : 5);
   int S = 1;
   if (tiles < slots) {
     const int smax = std::max(1, std::min(64, a.nks / 4));
@@ -316,14 +494,17 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
   }
   a.kps = ceil_div(a.nks, S);
   S = ceil_div(a.nks, a.kps);  // no empty split
-  auto dW = at::empty({Cout, Cin, KH, KW},
-                      x.options().dtype(at::kFloat).memory_format(at::MemoryFormat::ChannelsLast));
-  at::Tensor part;
-  if (S > 1) {
-    part = at::empty({(int64_t)S * dW.numel()}, x.options().dtype(at::kFloat));
-    a.out = part.data_ptr<float>();
-  } else {
+  const int64_t oc = out_cout < 0 ? Cout : out_cout, oi = out_cin < 0 ? Cin : out_cin;
+  IAMD_CHECK(oc <= Cout && oi <= Cin, "conv2d_wgrad_mfma: crop larger than the operands");
+  const bool direct = S == 1 && !out_bf16 && oc == Cout && oi == Cin;
+  at::Tensor dW, part;
+  if (direct) {
+    dW = at::empty({Cout, Cin, KH, KW},
+                   x.options().dtype(at::kFloat).memory_format(at::MemoryFormat::ChannelsLast));
     a.out = dW.data_ptr<float>();
+  } else {
+    part = at::empty({(int64_t)S * Cout * KK * Cin}, x.options().dtype(at::kFloat));
+    a.out = part.data_ptr<float>();
   }
   const int64_t grid = (int64_t)tiles * S;
   IAMD_CHECK(grid < (1ll << 31), "conv2d_wgrad_mfma: grid too large");
@@ -340,20 +521,29 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
   };
   using I64 = std::integral_constant<int, 64>;
   using I128 = std::integral_constant<int, 128>;
-  if (bno128 && bc128) launch(I128(), I128());
+  auto launch_mt = [&](auto bv, auto cv, auto tv) {
+    constexpr int BNO = decltype(bv)::value;
+    constexpr int BC = decltype(cv)::value;
+    constexpr int NT = decltype(tv)::value;
+    hipLaunchKernelGGL((conv_wgrad_mfma_mt<BNO, BC, NT>), dim3((unsigned)grid), dim3(kThreads),
+                       0, stream(), a);
+  };
+  if (mt) {
+    using T3 = std::integral_constant<int, 3>;
+    using T5 = std::integral_constant<int, 5>;
+    if (KW == 3) {
+      if (bno128) launch_mt(I128(), I64(), T3());
+      else launch_mt(I64(), I64(), T3());
+    } else {
+      launch_mt(I64(), I64(), T5());
+    }
+  } else if (bno128 && bc128) launch(I128(), I128());
   else if (bno128) launch(I128(), I64());
   else if (bc128) launch(I64(), I128());
   else launch(I64(), I64());
   IAMD_LAUNCH_CHECK();
-  if (S > 1) {
-    const int64_t n4 = dW.numel() / 4;
-    const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 4096);
-    hipLaunchKernelGGL(sum_splits, dim3(blocks), dim3(256), 0, stream(),
-                       reinterpret_cast<const float4*>(part.data_ptr<float>()),
-                       reinterpret_cast<float4*>(dW.data_ptr<float>()), S, n4);
-    IAMD_LAUNCH_CHECK();
-  }
-  return dW;
+  if (direct) return dW;
+  return wgrad_finalize(part, S, Cout, Cin, oc, oi, KH, KW, out_bf16 ? at::kBFloat16 : at::kFloat);
 }
 
 }  // namespace iamd

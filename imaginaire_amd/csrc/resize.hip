@@ -1,4 +1,4 @@
-// k12: bilinear resize of NHWC (channels-last) activations, bf16 / fp32 I/O, fp32 math.
+// k12: bilinear and nearest resizes of NHWC (channels-last) activations, bf16 / fp32 I/O.
 //
 // Replaces the two bilinear resizes of the SPADE discriminator (reference
 // discriminators/spade.py:86-88: the 0.5x input pyramid, align_corners=True;
@@ -9,6 +9,10 @@
 //     residual in the same pass (FPSE: up(top) + lateral), and writes the input dtype;
 //   * the backward is a GATHER: every input pixel collects the (at most a few) output pixels
 //     whose taps touch it — no atomics, deterministic, one 16-byte store per 8 channels.
+// Nearest (the SPADE generator's 2x upsampling between blocks and the per-resolution label
+// maps; reference generators/spade.py:237-399 uses nn.Upsample / F.interpolate) is a 16-byte
+// gather in the input dtype with a gather backward (PyTorch's NHWC nearest kernels ran at ~1/5
+// of HBM bandwidth on MI355X, profiles/spade_step_op_shapes_mi355x.txt).
 // The source-coordinate rule is PyTorch's area_pixel_compute_source_index (align_corners:
 // src = scale * dst; otherwise src = max(scale * (dst + 0.5) - 0.5, 0)) with the caller's
 // scale, so results match F.interpolate bit-for-bit up to the output rounding.
@@ -147,6 +151,82 @@ resize_bwd(const T* __restrict__ dy, T* __restrict__ dx, int B, int C, Axis ay, 
   }
 }
 
+// ---- nearest (PyTorch's nearest_idx: exact 2x -> o >> 1, same size -> o, otherwise
+// min(floor(o * scale), in - 1) in float) --------------------------------------------------
+__device__ __forceinline__ int nearest_src(const Axis& a, int o) {
+  if (a.out == a.in) return o;
+  if (a.out == 2 * a.in) return o >> 1;
+  return min((int)floorf((float)o * a.scale), a.in - 1);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kThreads)
+nearest_fwd(const T* __restrict__ x, T* __restrict__ y, int B, int C, Axis ay, Axis ax) {
+  const int cv = C / 8;
+  const int64_t n = (int64_t)B * ay.out * ax.out * cv;
+  for (int64_t t = blockIdx.x * (int64_t)kThreads + threadIdx.x; t < n;
+       t += (int64_t)gridDim.x * kThreads) {
+    const int c8 = (int)(t % cv);
+    int64_t p = t / cv;
+    const int ox = (int)(p % ax.out);
+    p /= ax.out;
+    const int oy = (int)(p % ay.out);
+    const int b = (int)(p / ay.out);
+    const int64_t src = (((int64_t)b * ay.in + nearest_src(ay, oy)) * ax.in +
+                         nearest_src(ax, ox)) * C + c8 * 8;
+    *reinterpret_cast<Pack<T, 8>*>(y + t * 8) = *reinterpret_cast<const Pack<T, 8>*>(x + src);
+  }
+}
+
+// outputs along one axis whose nearest source is input index i
+__device__ __forceinline__ int nearest_list(const Axis& a, int i, int (&idx)[kMaxTaps]) {
+  int lo = 0, hi = a.out - 1;
+  if (a.out == a.in) {
+    lo = hi = i;
+  } else if (a.out == 2 * a.in) {
+    lo = 2 * i;
+    hi = 2 * i + 1;
+  } else if (a.scale > 0.f) {
+    lo = max(0, (int)floorf((float)i / a.scale) - 1);
+    hi = min(a.out - 1, (int)ceilf((float)(i + 1) / a.scale) + 1);
+  }
+  int n = 0;
+  for (int o = lo; o <= hi && n < kMaxTaps; ++o)
+    if (nearest_src(a, o) == i) idx[n++] = o;
+  return n;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kThreads)
+nearest_bwd(const T* __restrict__ dy, T* __restrict__ dx, int B, int C, Axis ay, Axis ax) {
+  const int cv = C / 8;
+  const int64_t n = (int64_t)B * ay.in * ax.in * cv;
+  for (int64_t t = blockIdx.x * (int64_t)kThreads + threadIdx.x; t < n;
+       t += (int64_t)gridDim.x * kThreads) {
+    const int c8 = (int)(t % cv);
+    int64_t p = t / cv;
+    const int ix = (int)(p % ax.in);
+    p /= ax.in;
+    const int iy = (int)(p % ay.in);
+    const int b = (int)(p / ay.in);
+    int oys[kMaxTaps], oxs[kMaxTaps];
+    const int ny = nearest_list(ay, iy, oys);
+    const int nx = nearest_list(ax, ix, oxs);
+    float acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+    const T* base = dy + (int64_t)b * ay.out * ax.out * C + c8 * 8;
+    for (int a = 0; a < ny; ++a)
+      for (int c = 0; c < nx; ++c) {
+        float g[8];
+        load_vec<T, 8>(base + ((int64_t)oys[a] * ax.out + oxs[c]) * C, g);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += g[k];
+      }
+    store_vec<T, 8>(dx + t * 8, acc);
+  }
+}
+
 Axis make_axis(int64_t in, int64_t out, double scale, bool ac) {
   Axis a;
   a.in = (int)in;
@@ -220,6 +300,53 @@ at::Tensor resize_bilinear_bwd(const at::Tensor& dy, int64_t H, int64_t W, doubl
                        reinterpret_cast<__hip_bfloat16*>(dx.data_ptr()), B, C, ay, ax);
   else
     hipLaunchKernelGGL((resize_bwd<float>), dim3(grid_for(n)), dim3(kThreads), 0, stream(),
+                       dy.data_ptr<float>(), dx.data_ptr<float>(), B, C, ay, ax);
+  IAMD_LAUNCH_CHECK();
+  return dx;
+}
+
+// y[B, C, Ho, Wo] (channels-last) = nearest(x); scale_* = PyTorch's source scale (in / out or
+// 1 / scale_factor). A pure gather of 16-byte channel chunks in the input dtype.
+at::Tensor resize_nearest_fwd(const at::Tensor& x, int64_t Ho, int64_t Wo, double scale_h,
+                              double scale_w) {
+  check_nhwc(x, "resize_nearest_fwd");
+  const int B = (int)x.size(0), C = (int)x.size(1);
+  auto y = at::empty({B, C, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const Axis ay = make_axis(x.size(2), Ho, scale_h, false);
+  const Axis ax = make_axis(x.size(3), Wo, scale_w, false);
+  const int64_t n = (int64_t)B * Ho * Wo * (C / 8);
+  if (n == 0) return y;
+  if (x.scalar_type() == at::kBFloat16)
+    hipLaunchKernelGGL((nearest_fwd<__hip_bfloat16>), dim3(grid_for(n)), dim3(kThreads), 0,
+                       stream(), reinterpret_cast<const __hip_bfloat16*>(x.data_ptr()),
+                       reinterpret_cast<__hip_bfloat16*>(y.data_ptr()), B, C, ay, ax);
+  else
+    hipLaunchKernelGGL((nearest_fwd<float>), dim3(grid_for(n)), dim3(kThreads), 0, stream(),
+                       reinterpret_cast<const float*>(x.data_ptr()),
+                       reinterpret_cast<float*>(y.data_ptr()), B, C, ay, ax);
+  IAMD_LAUNCH_CHECK();
+  return y;
+}
+
+// dx[B, C, H, W] = sum of dy over the outputs that copied each input pixel (gather form)
+at::Tensor resize_nearest_bwd(const at::Tensor& dy, int64_t H, int64_t W, double scale_h,
+                              double scale_w) {
+  check_nhwc(dy, "resize_nearest_bwd");
+  const int B = (int)dy.size(0), C = (int)dy.size(1);
+  const Axis ay = make_axis(H, dy.size(2), scale_h, false);
+  const Axis ax = make_axis(W, dy.size(3), scale_w, false);
+  IAMD_CHECK((ay.out <= 2 * ay.in || (scale_h > 0.0 && 1.0 / scale_h + 3.0 <= kMaxTaps)) &&
+                 (ax.out <= 2 * ax.in || (scale_w > 0.0 && 1.0 / scale_w + 3.0 <= kMaxTaps)),
+             "resize_nearest_bwd: upsampling factor above 5 unsupported");
+  auto dx = at::empty({B, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int64_t n = (int64_t)B * H * W * (C / 8);
+  if (n == 0) return dx;
+  if (dy.scalar_type() == at::kBFloat16)
+    hipLaunchKernelGGL((nearest_bwd<__hip_bfloat16>), dim3(grid_for(n)), dim3(kThreads), 0,
+                       stream(), reinterpret_cast<const __hip_bfloat16*>(dy.data_ptr()),
+                       reinterpret_cast<__hip_bfloat16*>(dx.data_ptr()), B, C, ay, ax);
+  else
+    hipLaunchKernelGGL((nearest_bwd<float>), dim3(grid_for(n)), dim3(kThreads), 0, stream(),
                        dy.data_ptr<float>(), dx.data_ptr<float>(), B, C, ay, ax);
   IAMD_LAUNCH_CHECK();
   return dx;

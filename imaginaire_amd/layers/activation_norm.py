@@ -23,7 +23,7 @@ from imaginaire_amd.ops import conv as nhwc_conv
 from torch import nn
 from torch.nn import functional as F
 
-from imaginaire_amd.ops.norm import fused_norm_act
+from imaginaire_amd.ops.norm import fused_norm_act, prefetch_sync_stats
 from imaginaire_amd.ops.resize import interpolate
 from .conv import LinearBlock, Conv2dBlock, HyperConv2d, PartialConv2dBlock
 from .misc import PartialSequential
@@ -62,11 +62,19 @@ class LabelMapCache(object):
         key = (id(t), t.data_ptr(), tuple(size), mode, pad)
         out = cache.store.get(key) if cache is not None else None
         if out is None:
-            out = t if same else interpolate(t, size=size, mode=mode)
+            src = t
             if pad:
-                c = out.shape[1]
-                out = nhwc_conv.mark_zero_tail(nhwc_conv._pad_channels(out, (c + 63) // 64 * 64),
-                                               c)
+                # pad ONCE at the source resolution (cached), then resize the padded map: the
+                # zero tail stays zero and the NHWC resize kernels need channels % 8 == 0
+                pkey = (id(t), t.data_ptr(), 'padded')
+                src = cache.store.get(pkey) if cache is not None else None
+                if src is None:
+                    c = t.shape[1]
+                    src = nhwc_conv.mark_zero_tail(
+                        nhwc_conv._pad_channels(t, (c + 63) // 64 * 64), c)
+                    if cache is not None:
+                        cache.store[pkey] = src
+            out = src if same else interpolate(src, size=size, mode=mode)
             if cache is not None:
                 cache.store[key] = out
         return out
@@ -261,6 +269,33 @@ class AdaptiveNorm(nn.Module):
         return out
 
 
+class _Cat0View(torch.autograd.Function):
+    """``cat([a, b], 0)`` of two channels-last tensors that already sit back to back in one
+    storage (the γ and β conv weights of a SPADE layer written consecutively into the k5c
+    spectral-norm buffer): a view, no copy; the backward splits the gradient."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        ctx.n = a.shape[0]
+        shape = (a.shape[0] + b.shape[0],) + tuple(a.shape[1:])
+        return a.as_strided(shape, a.stride(), a.storage_offset())
+
+    @staticmethod
+    def backward(ctx, g):
+        return g[:ctx.n], g[ctx.n:]
+
+
+def cat0(a, b):
+    cl = torch.channels_last
+    if a.is_cuda and a.dim() == 4 and b.dim() == 4 and a.dtype == b.dtype and \
+            a.shape[1:] == b.shape[1:] and a.stride() == b.stride() and \
+            a.is_contiguous(memory_format=cl) and b.is_contiguous(memory_format=cl) and \
+            a.untyped_storage().data_ptr() == b.untyped_storage().data_ptr() and \
+            b.storage_offset() == a.storage_offset() + a.numel():
+        return _Cat0View.apply(a, b)
+    return torch.cat([a, b], 0)
+
+
 class SpatiallyAdaptiveNorm(nn.Module):
     """SPADE (activation_norm.py:109-234), fused on MI355X (see module docstring)."""
 
@@ -317,7 +352,7 @@ class SpatiallyAdaptiveNorm(nn.Module):
             hidden = self.mlps[i](label_map)
             cg = self.gammas[i].layers.conv
             cb = self.betas[i].layers.conv
-            w = torch.cat([get_weight(cg), get_weight(cb)], 0)
+            w = cat0(get_weight(cg), get_weight(cb))
             b = torch.cat([cg.bias, cb.bias], 0) if cg.bias is not None else None
             return nhwc_conv.conv2d(hidden, w, b, cg.stride, cg.padding, cg.dilation, cg.groups,
                                     cg.padding_mode)
@@ -326,6 +361,11 @@ class SpatiallyAdaptiveNorm(nn.Module):
     def forward(self, x, *cond_inputs, act_slope=1.0, **kwargs):
         active = [i for i in range(len(cond_inputs)) if cond_inputs[i] is not None]
         size = x.shape[2:]
+        if isinstance(self.norm, SyncBatchNorm) and self.training and \
+                self.norm._effective_mode() == 'sync_batch' and not self.norm.affine:
+            # start the cross-rank statistics exchange of x now: it rides xGMI while the γ|β
+            # convolutions below (independent of it) run
+            prefetch_sync_stats(x, self.norm.eps, self.norm.process_group)
         gbs = []
         for i in active:
             label_map = LabelMapCache.resize(cond_inputs[i], size,

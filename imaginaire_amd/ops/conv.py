@@ -36,6 +36,8 @@ _MFMA_MIN_DGRAD_BLOCKS = int(os.environ.get('IMAGINAIRE_AMD_MFMA_MIN_DGRAD_BLOCK
 # profiles/conv_mfma_probe_mi355x.txt, and it compiles nothing at first call), '0' = MIOpen,
 # 'auto' = per-shape faster of the two (timed once; the choice is agreed across ranks)
 _MFMA_WGRAD = os.environ.get('IMAGINAIRE_AMD_MFMA_WGRAD', '1')
+# stride-2..4 data gradients as s*s phase convs on k10 (0: MIOpen backward-data)
+_MFMA_STRIDED_DGRAD = os.environ.get('IMAGINAIRE_AMD_MFMA_STRIDED_DGRAD', '0') == '1'
 
 
 # ---- per-call conv log (IMAGINAIRE_AMD_CONV_LOG=1 or enable_conv_log()): every k10 / k11 /
@@ -187,7 +189,10 @@ def mfma_eligible(x, w, stride, padding, dilation, groups):
 
 
 def _flip_t(w):
-    """[Cout, Cin, KH, KW] -> [Cin, Cout, KH, KW] spatially flipped (dgrad-as-conv weight)."""
+    """[Cout, Cin, KH, KW] -> [Cin, Cout, KH, KW] spatially flipped (dgrad-as-conv weight):
+    one pass of the conv_aux.hip transpose kernel (PyTorch: flip + strided copy)."""
+    if w.is_cuda and w.dtype == torch.bfloat16 and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0:
+        return _ext.ext().conv_weight_flip_t(nhwc(w))
     return w.flip(2, 3).transpose(0, 1).contiguous(memory_format=_CL)
 
 
@@ -253,6 +258,12 @@ class _MfmaConv2d(torch.autograd.Function):
                 with _Logged('dgrad', 'k10', fl, _gemm_desc(dy, wt, (1, 1), pt)):
                     dx = _ext.ext().conv2d_mfma(dy, wt, None, 1, 1, pt[0], pt[1],
                                                 dilation[0], dilation[1], 1.0)
+            elif stride[0] == stride[1] and 2 <= stride[0] <= 4 and dilation == (1, 1) and \
+                    _MFMA_STRIDED_DGRAD and dblocks >= _MFMA_MIN_DGRAD_BLOCKS * stride[0] ** 2:
+                # s*s phase convs on k10 (csrc/conv_mfma.hip conv2d_dgrad_strided_mfma)
+                with _Logged('dgrad', 'k10s', fl, _gemm_desc(dy, wb, stride, padding)):
+                    dx = _ext.ext().conv2d_dgrad_strided_mfma(
+                        dy, wb, xb.shape[2], xb.shape[3], stride[0], padding[0], padding[1])
             else:
                 with _Logged('dgrad', 'miopen', fl, _gemm_desc(dy, wb, stride, padding)):
                     dx = torch.ops.aten.convolution_backward(
@@ -262,7 +273,7 @@ class _MfmaConv2d(torch.autograd.Function):
                 dx = dx[:, :xc]
             dx = dx.to(xdt)
         if need_w:
-            dw = _wgrad(dy, xb, wb, stride, padding, dilation)
+            dw = _wgrad(dy, xb, wb, stride, padding, dilation, cout, cin, wdt)
             if dw.shape[0] != cout or dw.shape[1] != cin:
                 dw = dw[:cout, :cin]
             dw = dw.to(wdt)
@@ -274,13 +285,15 @@ class _MfmaConv2d(torch.autograd.Function):
 _WGRAD_CHOICE = {}
 
 
-def _wgrad(dy, xb, wb, stride, padding, dilation):
+def _wgrad(dy, xb, wb, stride, padding, dilation, cout=-1, cin=-1, wdt=torch.float32):
     """Weight gradient: k11 or MIOpen wrw, whichever measured faster for this shape (timed
-    once per shape, both paths warm; ``IMAGINAIRE_AMD_MFMA_WGRAD`` = auto | 1 | 0)."""
+    once per shape, both paths warm; ``IMAGINAIRE_AMD_MFMA_WGRAD`` = auto | 1 | 0). k11
+    returns the gradient already cropped to (cout, cin) and in the weight's dtype (bf16 for
+    the bf16 spectral-norm / autocast weights): the crop and cast ride in its split-K sum."""
     def k11():
         return _ext.ext().conv2d_wgrad_mfma(dy, xb, wb.shape[2], wb.shape[3], stride[0],
                                             stride[1], padding[0], padding[1], dilation[0],
-                                            dilation[1])
+                                            dilation[1], cout, cin, wdt == torch.bfloat16)
 
     def miopen():
         return torch.ops.aten.convolution_backward(

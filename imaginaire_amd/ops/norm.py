@@ -43,6 +43,57 @@ def _merge_stats(cnt, mean, var, group):
     return n.reshape(1, -1), mean_g.reshape(1, -1), var_g.reshape(1, -1)
 
 
+# ---- per-tensor batch-statistics cache ---------------------------------------------------
+# In a SPADE residual block norm_0 and norm_s normalise the SAME tensor with the same
+# (param-free) settings: the second layer reuses the first one's statistics — for sync-BN that
+# is one cross-rank exchange per block input instead of two. The cache lives on the tensor
+# (freed with it) and is keyed by its version counter, eps and the process group. For sync-BN
+# the exchange can also be started early (prefetch_sync_stats: launched before the SPADE γ|β
+# convolutions, which do not depend on it, and joined when the norm applies).
+
+def _stats_key(x, eps, group, sync):
+    return (x._version, float(eps), id(group), bool(sync))
+
+
+def _cached_stats(x, key):
+    c = getattr(x, '_iamd_bn_stats', None)
+    if c is None or c[0] != key:
+        return None
+    if c[1] == 'pending':
+        work, bufs, local = c[2], c[3], c[4]
+        work.wait()
+        stats = _merge_gathered(bufs, local)
+        x._iamd_bn_stats = (key, 'done', stats)
+        return stats
+    return c[2]
+
+
+def _merge_gathered(bufs, local=None):
+    allst = torch.stack(bufs, 0)  # [W, 3, C]
+    n_i, m_i, v_i = allst[:, 0], allst[:, 1], allst[:, 2]
+    n = n_i.sum(0)
+    mean_g = (n_i * m_i).sum(0) / n.clamp_min(1)
+    m2 = (n_i * (v_i + (m_i - mean_g) ** 2)).sum(0)
+    var_g = m2 / n.clamp_min(1)
+    return n.reshape(1, -1), mean_g.reshape(1, -1), var_g.reshape(1, -1)
+
+
+def prefetch_sync_stats(x, eps, group):
+    """Compute this rank's batch statistics of ``x`` and START their all-gather (async); the
+    sync-BN forward that later normalises ``x`` joins it. No-op unless the HIP path runs with
+    more than one rank."""
+    if not (_ext.use_native(x) and _world(group) > 1 and x.dim() == 4):
+        return
+    key = _stats_key(x, eps, group, True)
+    if getattr(x, '_iamd_bn_stats', (None,))[0] == key:
+        return
+    count, mean, var, _, _ = _ext.ext().norm_stats(x, False, eps, None, None, True)
+    stacked = torch.stack([count.reshape(-1), mean.reshape(-1), var.reshape(-1)], 0).contiguous()
+    bufs = [torch.empty_like(stacked) for _ in range(_world(group))]
+    work = dist.all_gather(bufs, stacked, group=group, async_op=True)
+    x._iamd_bn_stats = (key, 'pending', work, bufs, stacked)
+
+
 def _update_running(running_mean, running_var, mean, var, count, factor):
     if running_mean is None:
         return
@@ -101,15 +152,28 @@ class _FusedNormActFn(torch.autograd.Function):
             count = None
         elif cfg.use_batch_stats:
             sync = cfg.mode == 'sync_batch' and _world(cfg.group) > 1
-            count, mean, var, scale, shift = ext.norm_stats(x, per_instance, cfg.eps, wf, bf, sync)
-            if sync:
-                count, mean, var = _merge_stats(count, mean, var, cfg.group)
-            rstd = torch.rsqrt(var + cfg.eps)
-            if sync:
-                a = wf.reshape(1, C) if wf is not None else 1.0
-                b = bf.reshape(1, C) if bf is not None else 0.0
-                scale = (rstd * a).contiguous()
-                shift = (b - mean * scale).contiguous()
+            shareable = not per_instance and wf is None and bf is None
+            key = _stats_key(x, cfg.eps, cfg.group, sync)
+            cached = _cached_stats(x, key) if shareable else None
+            if cached is not None and len(cached) == 6:  # a previous layer's full result
+                count, mean, var, rstd, scale, shift = cached
+            else:
+                if cached is not None:  # merged statistics of a prefetched exchange
+                    count, mean, var = cached
+                    scale = None
+                else:
+                    count, mean, var, scale, shift = ext.norm_stats(x, per_instance, cfg.eps, wf,
+                                                                    bf, sync)
+                    if sync:
+                        count, mean, var = _merge_stats(count, mean, var, cfg.group)
+                rstd = torch.rsqrt(var + cfg.eps)
+                if sync or scale is None:
+                    a = wf.reshape(1, C) if wf is not None else 1.0
+                    b = bf.reshape(1, C) if bf is not None else 0.0
+                    scale = (rstd * a).contiguous()
+                    shift = (b - mean * scale).contiguous()
+                if shareable:
+                    x._iamd_bn_stats = (key, 'done', (count, mean, var, rstd, scale, shift))
             if cfg.training and not per_instance:
                 _update_running(running_mean, running_var, mean, var, count, cfg.momentum)
         else:  # eval with running statistics

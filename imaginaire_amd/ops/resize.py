@@ -52,6 +52,36 @@ class _BilinearNHWC(torch.autograd.Function):
             None, None, None, None, None
 
 
+class _NearestNHWC(torch.autograd.Function):
+    """k12 nearest resize (16-byte gathers in the activation dtype); gather-form backward."""
+
+    @staticmethod
+    def forward(ctx, x, ho, wo, sh, sw):
+        ctx.conf = (x.shape[2], x.shape[3], sh, sw)
+        return _ext.ext().resize_nearest_fwd(x, ho, wo, sh, sw)
+
+    @staticmethod
+    def backward(ctx, dy):
+        h, w, sh, sw = ctx.conf
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        return _ext.ext().resize_nearest_bwd(dy, h, w, sh, sw), None, None, None, None
+
+
+def _nearest(x, size, scale_factor):
+    h, w = x.shape[2], x.shape[3]
+    sfh, sfw = _pair(scale_factor) if scale_factor is not None else (None, None)
+    if size is not None:
+        ho, wo = _pair(size)
+        sfh = sfw = None
+    else:
+        ho, wo = int(math.floor(h * sfh)), int(math.floor(w * sfw))
+    # the backward's gather lists cover up to 5x upsampling per axis
+    if ho > 5 * h or wo > 5 * w:
+        return None
+    return _NearestNHWC.apply(x, ho, wo, _src_scale(h, ho, False, sfh),
+                              _src_scale(w, wo, False, sfw))
+
+
 def _bilinear_native_ok(x):
     return x.is_cuda and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float32) and \
         x.shape[1] % 8 == 0 and x.is_contiguous(memory_format=torch.channels_last) and \
@@ -91,6 +121,13 @@ def interpolate(x, size=None, scale_factor=None, mode='nearest', align_corners=N
     # run an fp32 resize whose backward is an atomic scatter)
     if mode == 'bilinear' and not recompute_scale_factor and _bilinear_native_ok(x):
         return _bilinear(x, size, scale_factor, align_corners)
+    if mode == 'nearest' and not recompute_scale_factor and _bilinear_native_ok(x):
+        y = _nearest(x, size, scale_factor)
+        if y is not None:
+            valid = getattr(x, '_iamd_valid_channels', None)
+            if valid is not None:
+                y._iamd_valid_channels = valid
+            return y
     if mode == 'nearest' and x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and \
             torch.is_autocast_enabled('cuda'):
         with torch.autocast('cuda', enabled=False):

@@ -29,11 +29,18 @@ def _free_port():
 
 
 def _init(rank, world, port):
+    import faulthandler
+    import sys
     import torch.distributed as dist
+    # a hung collective must end the child (and print where) well inside the box's 180 s
+    # silence limit: the parent then sees a non-zero exit code instead of waiting
+    faulthandler.dump_traceback_later(150, exit=True, file=sys.__stderr__)
+    print('[dist-test] rank %d starting' % rank, file=sys.__stderr__, flush=True)
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     torch.cuda.set_device(0)
     dist.init_process_group('gloo', rank=rank, world_size=world)
+    print('[dist-test] rank %d joined the gloo group' % rank, file=sys.__stderr__, flush=True)
     return dist
 
 
@@ -45,10 +52,10 @@ def _spawn(target, world, *args):
     for p in procs:
         p.start()
     try:
-        res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
+        res = sorted([q.get(timeout=170) for _ in range(world)], key=lambda t: t[0])
     finally:
         for p in procs:
-            p.join(120)
+            p.join(30)
             if p.is_alive():
                 p.kill()
     for p in procs:
@@ -84,7 +91,7 @@ def _syncbn_worker(rank, world, port, q, dtype):
                        training=True, momentum=0.1, slope=0.2)
     y.backward(gout[sl].cuda().to(y.dtype).contiguous(memory_format=cl))
     torch.cuda.synchronize()
-    q.put((rank, y.float().cpu(), xr.grad.float().cpu(), gbr.grad.float().cpu(),
+    q.put((rank, y.detach().float().cpu(), xr.grad.float().cpu(), gbr.grad.float().cpu(),
            wr.grad.cpu(), br.grad.cpu(), rm.cpu(), rv.cpu()))
     dist.barrier()
     dist.destroy_process_group()
@@ -167,6 +174,9 @@ def _ddp_worker(rank, world, port, q, comm):
 
 
 def _ref_worker(rank, world, port, q):
+    import faulthandler
+    import sys
+    faulthandler.dump_traceback_later(150, exit=True, file=sys.__stderr__)
     torch.cuda.set_device(0)
     names, g = _spade_grads(0, 1, None)
     q.put((0, names, g))

@@ -319,6 +319,11 @@ _CONV_CASES = [
     (2, 3, 64, 16, 24, 3, 1, 1, 1),         # RGB in: Cin padded 3 -> 64
     (2, 64, 3, 16, 24, 3, 1, 1, 1),         # RGB out: Cout padded 3 -> 64
     (1, 128, 100, 12, 12, 3, 1, 1, 1),      # Cout padded 100 -> 128
+    # stride-2 data gradients: k10 phase decomposition (conv2d_dgrad_strided_mfma)
+    (2, 64, 128, 15, 17, 3, 2, 1, 1),       # 3x3 s2, odd sizes: 1x1 / 1x2 / 2x1 / 2x2 phases
+    (1, 128, 64, 9, 14, 1, 2, 0, 1),        # 1x1 s2: three phases receive no taps (zeros)
+    (1, 64, 128, 11, 13, 5, 2, 2, 1),       # 5x5 s2
+    (2, 256, 128, 8, 16, 4, 2, 1, 1),       # PatchGAN 4x4 s2 at a small map
 ]
 
 
@@ -331,6 +336,7 @@ def test_conv2d_mfma_fwd_bwd(case, slope, bias):
     C._MFMA_MIN_BLOCKS = 0
     C._MFMA_MIN_DGRAD_BLOCKS = 0
     C._MFMA_WGRAD = 'auto' if slope == 0.0 else '1'
+    C._MFMA_STRIDED_DGRAD = True  # stride-2 cases: k10 phase decomposition
     B, cin, cout, H, W, k, s, p, d = case
     torch.manual_seed(1)
     x = torch.randn(B, cin, H, W, device='cuda').to(torch.bfloat16).contiguous(
@@ -574,3 +580,131 @@ def test_correlation_flownetc_shape():
     for got, want in ((a.grad, ar.grad), (b.grad, br.grad)):
         err = (got.float() - want).abs().max() / want.abs().max()
         assert err < 2e-2, err
+
+
+def test_conv_weight_flip_t():
+    from imaginaire_amd.ops import _ext
+    torch.manual_seed(11)
+    for cout, cin, k in ((128, 192, 5), (64, 64, 3), (1024, 128, 5), (72, 200, 4)):
+        w = torch.randn(cout, cin, k, k, device='cuda').to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        got = _ext.ext().conv_weight_flip_t(w)
+        ref = w.flip(2, 3).transpose(0, 1)
+        assert got.shape == ref.shape and got.is_contiguous(memory_format=torch.channels_last)
+        assert torch.equal(got, ref)
+        for st, qy, qx in ((2, 0, 1), (2, 1, 0), (3, 2, 1)):  # one stride-st phase's taps
+            if qy >= k or qx >= k:
+                continue
+            got = _ext.ext().conv_weight_flip_t(w, st, qy, qx)
+            ref = w[:, :, qy::st, qx::st].flip(2, 3).transpose(0, 1)
+            assert got.shape == ref.shape and torch.equal(got, ref)
+
+
+@pytest.mark.parametrize('case', [(2, 185, 128, 12, 20, 5, 1, 2), (2, 64, 3, 16, 24, 3, 1, 1),
+                                  (2, 128, 128, 16, 24, 3, 1, 1)])
+def test_conv2d_mfma_fp32_weight_under_autocast(case):
+    """Autocast with fp32 master weights: the k11 gradient comes back fp32 and cropped."""
+    from imaginaire_amd.ops import conv as C
+    C._MFMA_MIN_BLOCKS = 0
+    C._MFMA_MIN_DGRAD_BLOCKS = 0
+    B, cin, cout, H, W, k, s, p = case
+    torch.manual_seed(12)
+    x = torch.randn(B, cin, H, W, device='cuda').contiguous(
+        memory_format=torch.channels_last).requires_grad_(True)
+    w = (torch.randn(cout, cin, k, k, device='cuda') / (cin * k * k) ** 0.5).contiguous(
+        memory_format=torch.channels_last).requires_grad_(True)
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        y = C.conv2d(x, w, None, s, p)
+    assert y.dtype == torch.bfloat16
+    xr = x.detach().to(torch.bfloat16).float().requires_grad_(True)
+    wr = w.detach().to(torch.bfloat16).float().requires_grad_(True)
+    yr = F.conv2d(xr, wr, None, s, p)
+    go = torch.randn_like(yr)
+    y.backward(go.to(y.dtype))
+    yr.backward(go)
+    assert w.grad.dtype == torch.float32 and w.grad.shape == w.shape
+    e = (w.grad - wr.grad).abs().max().item()
+    assert e <= 2e-2 * max(1.0, wr.grad.abs().max().item()), e
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('case', [
+    # (N, C, H, W, size, scale)
+    (2, 256, 16, 32, None, 2.0),     # SPADE G 2x upsampling between blocks
+    (1, 192, 64, 128, (16, 32), None),  # label map to a lower resolution
+    (1, 64, 7, 9, (20, 13), None),   # non-integer ratios
+    (2, 8, 5, 6, None, 3.0),
+])
+def test_nearest_resize_k12(dtype, case):
+    from imaginaire_amd.ops.resize import interpolate
+    N, C, H, W, size, sf = case
+    torch.manual_seed(13)
+    x = torch.randn(N, C, H, W, device='cuda').to(dtype).contiguous(
+        memory_format=torch.channels_last).requires_grad_(True)
+    y = interpolate(x, size=size, scale_factor=sf, mode='nearest')
+    xr = x.detach().float().requires_grad_(True)
+    yr = F.interpolate(xr, size=size, scale_factor=sf, mode='nearest')
+    assert y.shape == yr.shape and y.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(y.float(), yr)
+    g = torch.randn_like(yr)
+    y.backward(g.to(dtype))
+    yr.backward(g.to(dtype).float())
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    assert torch.allclose(x.grad.float(), xr.grad, atol=tol, rtol=tol)
+
+
+@pytest.mark.parametrize('case', [
+    # B, Cin, Cout, H, W, k, pad   (W = Wo multiple of 64: whole-row k-steps)
+    (2, 128, 256, 6, 64, 3, 1),     # multi-tap 3x3, 128 x 64 tiles
+    (1, 64, 64, 5, 128, 3, 1),      # multi-tap 3x3, 64 x 64 tiles
+    (2, 192, 128, 4, 64, 5, 2),     # multi-tap 5x5 (SPADE mlp_shared shape family)
+    (1, 128, 64, 3, 64, 5, 2),
+    (1, 64, 128, 7, 64, 3, 0),      # no padding: Wo = 62 -> one-tap kernel fallback
+])
+def test_conv2d_wgrad_multitap(case):
+    """k11 multi-tap weight gradient (all KW taps of a filter row per block, shifted LDS
+    window) vs fp32 autograd; also vs the one-tap kernel (IMAGINAIRE_AMD_WGRAD_MT=0)."""
+    import os
+    from imaginaire_amd.ops import _ext
+    B, cin, cout, H, W, k, p = case
+    torch.manual_seed(14)
+    x = torch.randn(B, cin, H, W, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    Ho, Wo = H + 2 * p - k + 1, W + 2 * p - k + 1
+    dy = torch.randn(B, cout, Ho, Wo, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    got = _ext.ext().conv2d_wgrad_mfma(dy, x, k, k, 1, 1, p, p, 1, 1)
+    os.environ['IMAGINAIRE_AMD_WGRAD_MT'] = '0'
+    try:
+        one = _ext.ext().conv2d_wgrad_mfma(dy, x, k, k, 1, 1, p, p, 1, 1)
+    finally:
+        os.environ.pop('IMAGINAIRE_AMD_WGRAD_MT')
+    ref = torch.nn.grad.conv2d_weight(x.float(), (cout, cin, k, k), dy.float(), 1, p)
+    scale = max(1.0, ref.abs().max().item())
+    assert (got - ref).abs().max().item() <= 2e-3 * scale
+    assert torch.allclose(got, one, atol=1e-3 * scale, rtol=1e-3)
+
+
+def test_cat0_view_of_adjacent_weights():
+    """γ|β weights adjacent in the spectral-norm buffer concatenate as a view (no copy),
+    with the gradient split back; non-adjacent operands fall back to torch.cat."""
+    from imaginaire_amd.layers.activation_norm import cat0
+    n = 64 * 32 * 9
+
+    def views(flat):  # two adjacent [64, 32, 3, 3] channels-last weights
+        return (flat[:n].view(64, 3, 3, 32).permute(0, 3, 1, 2),
+                flat[n:2 * n].view(64, 3, 3, 32).permute(0, 3, 1, 2))
+
+    x = torch.randn(2 * n + 8, device='cuda', requires_grad=True)
+    xa, xb = views(x)
+    assert xa.is_contiguous(memory_format=torch.channels_last)
+    y = cat0(xa, xb)
+    assert y.data_ptr() == xa.data_ptr(), 'expected a zero-copy view'
+    assert torch.equal(y.detach(), torch.cat([xa, xb], 0).detach())
+    g = torch.randn_like(y)
+    y.backward(g)
+    assert torch.equal(x.grad[:2 * n].view(128, 3, 3, 32).permute(0, 3, 1, 2), g)
+    assert torch.count_nonzero(x.grad[2 * n:]) == 0
+    fa, fb = views(x.detach())
+    c = cat0(fb, fa)  # wrong order: not adjacent -> plain cat
+    assert c.data_ptr() != fb.data_ptr() and torch.equal(c, torch.cat([fb, fa], 0))

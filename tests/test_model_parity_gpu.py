@@ -57,6 +57,11 @@ def _iteration(config, amp, eager, tmp, seq_len=None, overrides=()):
         cfg.logdir = str(tmp)
         cfg.speed_benchmark = False
         cfg.trainer.amp = amp
+        # lr 0: the G update sees the D both runs started from. Adam's first step moves every
+        # weight by ~lr whatever the gradient's magnitude, so the sign flips of near-zero bf16
+        # vs fp32 gradients would otherwise decorrelate the two D's before the G update.
+        cfg.gen_opt.lr = 0.0
+        cfg.dis_opt.lr = 0.0
         for key, val in overrides:
             node = cfg
             for k in key.split('.')[:-1]:
