@@ -85,8 +85,6 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
 at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t KH, int64_t KW,
                              int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh,
                              int64_t dw, int64_t out_cout, int64_t out_cin, bool out_bf16);
-at::Tensor conv2d_dgrad_strided_mfma(const at::Tensor& dy, const at::Tensor& w, int64_t H,
-                                     int64_t W, int64_t s, int64_t ph, int64_t pw);
 // conv_aux.hip
 at::Tensor conv_weight_flip_t(const at::Tensor& w, int64_t s, int64_t qy, int64_t qx);
 at::Tensor wgrad_finalize(const at::Tensor& part, int64_t S, int64_t Cop, int64_t Cip,
@@ -113,8 +111,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dy"), py::arg("x"), py::arg("KH"), py::arg("KW"), py::arg("sh"), py::arg("sw"),
         py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("out_cout") = -1,
         py::arg("out_cin") = -1, py::arg("out_bf16") = false);
-  m.def("conv2d_dgrad_strided_mfma", &iamd::conv2d_dgrad_strided_mfma,
-        "stride-s conv data gradient on k10 (s*s phase convs, strided epilogue)");
   m.def("conv_weight_flip_t", &iamd::conv_weight_flip_t,
         "flipped, in/out-transposed channels-last conv weight (dgrad-as-conv); s/qy/qx select "
         "the taps of one stride-s phase", py::arg("w"), py::arg("s") = 1, py::arg("qy") = 0,

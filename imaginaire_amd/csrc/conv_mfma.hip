@@ -915,73 +915,4 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
   return y;
 }
 
-// conv_aux.hip
-at::Tensor conv_weight_flip_t(const at::Tensor& w, int64_t s, int64_t qy, int64_t qx);
-
-// Data gradient of a stride-s conv (s = sh = sw > 1, dilation 1) on k10 by phase decomposition:
-// output pixel (s*a + ry, s*c + rx) of dx only receives the taps kh = qy + s*j (qy = (ry + ph)
-// mod s) and kw = qx + s*j, so each of the s*s phases is a STRIDE-1 conv of dy with the
-// sub-kernel w[:, :, qy::s, qx::s] (flipped, in/out transposed) whose outputs the epilogue
-// scatters to the strided pixel positions (ConvArgs output mapping). Replaces MIOpen's
-// stride-2 backward-data kernels (~200 TF/s on the SPADE discriminator / style-encoder shapes,
-// profiles/spade_step_conv_log_mi355x.txt).
-// dy [B, Cout, Ho, Wo] bf16 CL, w [Cout, Cin, KH, KW] bf16 CL (Cin, Cout % 64 == 0) -> dx
-// [B, Cin, H, W] bf16 CL.
-at::Tensor conv2d_dgrad_strided_mfma(const at::Tensor& dy, const at::Tensor& w, int64_t H,
-                                     int64_t W, int64_t s, int64_t ph, int64_t pw) {
-  IAMD_CHECK(dy.is_cuda() && w.is_cuda() && dy.scalar_type() == at::kBFloat16 &&
-                 w.scalar_type() == at::kBFloat16 && dy.dim() == 4 && w.dim() == 4,
-             "conv2d_dgrad_strided_mfma: bf16 4-D CUDA tensors expected");
-  IAMD_CHECK(dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
-                 w.is_contiguous(at::MemoryFormat::ChannelsLast),
-             "conv2d_dgrad_strided_mfma: packed channels-last dy / w expected");
-  const int B = (int)dy.size(0), Cout = (int)dy.size(1), Ho = (int)dy.size(2), Wo = (int)dy.size(3);
-  const int Cin = (int)w.size(1), K_h = (int)w.size(2), K_w = (int)w.size(3);
-  IAMD_CHECK(w.size(0) == Cout && Cin % 64 == 0 && Cout % 64 == 0 && s >= 2 && s <= 4,
-             "conv2d_dgrad_strided_mfma: channels must be multiples of 64, stride 2..4");
-  IAMD_CHECK(Ho == (H + 2 * ph - K_h) / s + 1 && Wo == (W + 2 * pw - K_w) / s + 1,
-             "conv2d_dgrad_strided_mfma: dy size does not match the conv geometry");
-  IAMD_CHECK((int64_t)B * Ho * Wo * Cout * 2 < kOobOffset && (int64_t)B * H * W * Cin < (1ll << 31),
-             "conv2d_dgrad_strided_mfma: tensor too large for 32-bit offsets");
-  bool empty_phase = false;
-  for (int r = 0; r < s; ++r)
-    if ((r + ph) % s >= K_h || (r + pw) % s >= K_w) empty_phase = true;
-  auto opts = dy.options().memory_format(at::MemoryFormat::ChannelsLast);
-  auto dx = empty_phase ? at::zeros({B, Cin, H, W}, opts) : at::empty({B, Cin, H, W}, opts);
-  for (int ry = 0; ry < s; ++ry) {
-    const int qy = (int)((ry + ph) % s);
-    const int Jy = qy < K_h ? (K_h - qy + (int)s - 1) / (int)s : 0;
-    const int Ay = (int)((H - ry + s - 1) / s);
-    for (int rx = 0; rx < s; ++rx) {
-      const int qx = (int)((rx + pw) % s);
-      const int Jx = qx < K_w ? (K_w - qx + (int)s - 1) / (int)s : 0;
-      const int Ax = (int)((W - rx + s - 1) / s);
-      if (Jy == 0 || Jx == 0 || Ay <= 0 || Ax <= 0) continue;
-      const int cy = (int)((ry + ph - qy) / s), cx = (int)((rx + pw - qx) / s);
-      // wsub[ci][j'y][j'x][co] = w[co][qy + s (Jy-1-j'y)][qx + s (Jx-1-j'x)][ci]
-      auto wsub = conv_weight_flip_t(w, s, qy, qx);
-      ConvArgs a;
-      a.x = reinterpret_cast<const __hip_bfloat16*>(dy.data_ptr());
-      a.w = reinterpret_cast<const __hip_bfloat16*>(wsub.data_ptr());
-      a.bias = nullptr;
-      a.y = reinterpret_cast<__hip_bfloat16*>(dx.data_ptr());
-      a.xbytes = (int)(dy.numel() * 2);
-      a.wbytes = (int)(wsub.numel() * 2);
-      a.H = Ho; a.W = Wo; a.Cin = Cout; a.Cout = Cin;
-      a.Ho = Ay; a.Wo = Ax;
-      a.KH = Jy; a.KW = Jx;
-      a.sh = 1; a.sw = 1; a.dh = 1; a.dw = 1;
-      a.ph = Jy - 1 - cy; a.pw = Jx - 1 - cx;
-      a.M = B * Ay * Ax;
-      a.cpt = Cout / kBK;
-      a.nk = Jy * Jx * a.cpt;
-      a.slope = 1.f;
-      a.omode = 1;
-      a.oH = (int)H; a.oW = (int)W; a.osy = (int)s; a.osx = (int)s; a.ory = ry; a.orx = rx;
-      run_conv(a, dy);
-    }
-  }
-  return dx;
-}
-
 }  // namespace iamd

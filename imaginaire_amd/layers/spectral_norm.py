@@ -170,4 +170,16 @@ def install_batched_spectral_norm(net):
     group = _SNGroup(net)
     if group.entries:
         net.register_forward_pre_hook(group)
+        net._iamd_sn_group = group
     return len(group.entries)
+
+
+def refresh_batched_spectral_norm(net):
+    """Run the batched power iteration of ``net`` again inside one forward — for a network
+    that calls its layers twice in one forward with the reference refreshing σ in between (the
+    SPADE discriminator's real then fake pass, reference discriminators/spade.py:91-117).
+    Without it each layer's second call falls back to its own per-layer power iteration
+    (~7 small kernels + an fp32 W/σ and a cast per layer)."""
+    group = getattr(net, '_iamd_sn_group', None)
+    if group is not None:
+        group(net, ())

@@ -36,8 +36,6 @@ _MFMA_MIN_DGRAD_BLOCKS = int(os.environ.get('IMAGINAIRE_AMD_MFMA_MIN_DGRAD_BLOCK
 # profiles/conv_mfma_probe_mi355x.txt, and it compiles nothing at first call), '0' = MIOpen,
 # 'auto' = per-shape faster of the two (timed once; the choice is agreed across ranks)
 _MFMA_WGRAD = os.environ.get('IMAGINAIRE_AMD_MFMA_WGRAD', '1')
-# stride-2..4 data gradients as s*s phase convs on k10 (0: MIOpen backward-data)
-_MFMA_STRIDED_DGRAD = os.environ.get('IMAGINAIRE_AMD_MFMA_STRIDED_DGRAD', '0') == '1'
 
 
 # ---- per-call conv log (IMAGINAIRE_AMD_CONV_LOG=1 or enable_conv_log()): every k10 / k11 /
@@ -121,6 +119,13 @@ def _round_up(c, m):
     return (c + m - 1) // m * m
 
 
+def _out_pad(cout):
+    """k10 output-channel padding (a multiple of 64: a 32-wide tile for the 3-channel RGB
+    output measured slower than the 64-wide one — the A-operand stream, not the wasted MFMA
+    columns, bounds those convs; profiles/spade_step_conv_log_mi355x.txt)."""
+    return _round_up(cout, 64)
+
+
 def _pad_channels(t, c):
     """Zero-pad dim 1 of a 4-D tensor to ``c`` channels (packed channels-last result)."""
     if t.shape[1] == c:
@@ -171,7 +176,7 @@ def mfma_eligible(x, w, stride, padding, dilation, groups):
     if _compute_dtype(x, w) != torch.bfloat16:
         return False
     cout, cin = w.shape[0], w.shape[1]
-    cp, op = _round_up(cin, 64), _round_up(cout, 64)
+    cp, op = _round_up(cin, 64), _out_pad(cout)
     # zero-padded channels cost MFMA work: allow ≤ 1/3 waste, except for the thin RGB-facing
     # convs (3-channel image in / out) where MIOpen's kernels run at ~1 TF/s and a 64-channel
     # padded MFMA tile is still an order of magnitude faster (profiles/spade_step_k10_k11)
@@ -184,7 +189,7 @@ def mfma_eligible(x, w, stride, padding, dilation, groups):
     if x.shape[0] * cp * x.shape[2] * x.shape[3] * 2 >= (1 << 30) or \
             x.shape[0] * op * ho * wo * 2 >= (1 << 30):
         return False
-    blocks = -(-x.shape[0] * ho * wo // 128) * (op // (128 if op % 128 == 0 else 64))
+    blocks = -(-x.shape[0] * ho * wo // 128) * max(1, op // (128 if op % 128 == 0 else 64))
     return blocks >= _MFMA_MIN_BLOCKS
 
 
@@ -212,7 +217,7 @@ class _MfmaConv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, bias, stride, padding, dilation, slope):
         cout, cin = w.shape[0], w.shape[1]
-        cp, op = _round_up(cin, 64), _round_up(cout, 64)
+        cp, op = _round_up(cin, 64), _out_pad(cout)
         xb = _pad_channels(x.to(torch.bfloat16), cp)
         wb = _pad_rows(_pad_channels(w.to(torch.bfloat16), cp), op)
         ho, wo = _out_hw(x.shape[2], x.shape[3], w.shape[2:], stride, padding, dilation)
@@ -258,12 +263,6 @@ class _MfmaConv2d(torch.autograd.Function):
                 with _Logged('dgrad', 'k10', fl, _gemm_desc(dy, wt, (1, 1), pt)):
                     dx = _ext.ext().conv2d_mfma(dy, wt, None, 1, 1, pt[0], pt[1],
                                                 dilation[0], dilation[1], 1.0)
-            elif stride[0] == stride[1] and 2 <= stride[0] <= 4 and dilation == (1, 1) and \
-                    _MFMA_STRIDED_DGRAD and dblocks >= _MFMA_MIN_DGRAD_BLOCKS * stride[0] ** 2:
-                # s*s phase convs on k10 (csrc/conv_mfma.hip conv2d_dgrad_strided_mfma)
-                with _Logged('dgrad', 'k10s', fl, _gemm_desc(dy, wb, stride, padding)):
-                    dx = _ext.ext().conv2d_dgrad_strided_mfma(
-                        dy, wb, xb.shape[2], xb.shape[3], stride[0], padding[0], padding[1])
             else:
                 with _Logged('dgrad', 'miopen', fl, _gemm_desc(dy, wb, stride, padding)):
                     dx = torch.ops.aten.convolution_backward(

@@ -319,7 +319,7 @@ _CONV_CASES = [
     (2, 3, 64, 16, 24, 3, 1, 1, 1),         # RGB in: Cin padded 3 -> 64
     (2, 64, 3, 16, 24, 3, 1, 1, 1),         # RGB out: Cout padded 3 -> 64
     (1, 128, 100, 12, 12, 3, 1, 1, 1),      # Cout padded 100 -> 128
-    # stride-2 data gradients: k10 phase decomposition (conv2d_dgrad_strided_mfma)
+    # more stride-2 shapes (forward on k10; data gradient on MIOpen)
     (2, 64, 128, 15, 17, 3, 2, 1, 1),       # 3x3 s2, odd sizes: 1x1 / 1x2 / 2x1 / 2x2 phases
     (1, 128, 64, 9, 14, 1, 2, 0, 1),        # 1x1 s2: three phases receive no taps (zeros)
     (1, 64, 128, 11, 13, 5, 2, 2, 1),       # 5x5 s2
@@ -336,7 +336,6 @@ def test_conv2d_mfma_fwd_bwd(case, slope, bias):
     C._MFMA_MIN_BLOCKS = 0
     C._MFMA_MIN_DGRAD_BLOCKS = 0
     C._MFMA_WGRAD = 'auto' if slope == 0.0 else '1'
-    C._MFMA_STRIDED_DGRAD = True  # stride-2 cases: k10 phase decomposition
     B, cin, cout, H, W, k, s, p, d = case
     torch.manual_seed(1)
     x = torch.randn(B, cin, H, W, device='cuda').to(torch.bfloat16).contiguous(
