@@ -87,6 +87,10 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
                              int64_t dw, int64_t out_cout, int64_t out_cin, bool out_bf16);
 // conv_aux.hip
 at::Tensor conv_weight_flip_t(const at::Tensor& w, int64_t s, int64_t qy, int64_t qx);
+at::Tensor pad_nhwc_fwd(const at::Tensor& x, int64_t pl, int64_t pr, int64_t pt, int64_t pb,
+                        int64_t mode);
+at::Tensor pad_nhwc_bwd(const at::Tensor& dy, int64_t H, int64_t W, int64_t pl, int64_t pr,
+                        int64_t pt, int64_t pb, int64_t mode);
 at::Tensor wgrad_finalize(const at::Tensor& part, int64_t S, int64_t Cop, int64_t Cip,
                           int64_t Cout, int64_t Cin, int64_t KH, int64_t KW,
                           at::ScalarType dtype);
@@ -111,6 +115,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dy"), py::arg("x"), py::arg("KH"), py::arg("KW"), py::arg("sh"), py::arg("sw"),
         py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("out_cout") = -1,
         py::arg("out_cin") = -1, py::arg("out_bf16") = false);
+  m.def("pad_nhwc_fwd", &iamd::pad_nhwc_fwd, "NHWC reflect / replicate padding");
+  m.def("pad_nhwc_bwd", &iamd::pad_nhwc_bwd, "NHWC reflect / replicate padding backward (gather)");
   m.def("conv_weight_flip_t", &iamd::conv_weight_flip_t,
         "flipped, in/out-transposed channels-last conv weight (dgrad-as-conv); s/qy/qx select "
         "the taps of one stride-s phase", py::arg("w"), py::arg("s") = 1, py::arg("qy") = 0,

@@ -11,7 +11,13 @@
 //   the parameter's dtype in its channels-last layout [Cout][KK][Cin] in the same pass, instead
 //   of sum -> slice copy -> dtype-cast copy.
 //
-// Reference: the reference gets both from cuDNN inside nn.Conv2d's autograd
+// * pad_nhwc — reflect / replicate padding of NHWC activations (the UNIT / MUNIT / FUNIT conv
+//   blocks, reference layers/conv.py:59-91 padding_mode='reflect'): a 16-byte gather forward and a
+//   GATHER backward (each input pixel sums the <= 4 padded pixels that copied it per axis pair).
+//   PyTorch's reflection_pad2d backward ran at ~1/50 of HBM bandwidth on channels-last bf16
+//   activations — a quarter of a MUNIT iteration (profiles/recipe_munit256_kernels_mi355x.txt).
+//
+// Reference: the reference gets the first two from cuDNN inside nn.Conv2d's autograd
 // (layers/conv.py:59-91); these kernels have no reference counterpart.
 #include "common.h"
 
@@ -99,7 +105,148 @@ wgrad_finalize_kernel(const float* __restrict__ part, T* __restrict__ out, int S
   }
 }
 
+// padded index o -> source index along one axis (mode 0 reflect, 1 replicate)
+__device__ __forceinline__ int pad_src(int o, int p, int n, int mode) {
+  int i = o - p;
+  if (mode == 0) {
+    if (i < 0) i = -i;
+    if (i >= n) i = 2 * (n - 1) - i;
+  } else {
+    i = min(max(i, 0), n - 1);
+  }
+  return i;
+}
+
+constexpr int kPadMax = 16;  // padded indices that may copy one source index (per axis)
+
+__device__ __forceinline__ int pad_list(int i, int p0, int p1, int n, int mode,
+                                        int (&idx)[kPadMax]) {
+  // candidates: the direct copy, its reflections across both edges, or (replicate) the whole
+  // edge band
+  int cnt = 0;
+  const int no = n + p0 + p1;
+  int lo = i + p0, hi = i + p0;
+  if (mode == 1) {
+    if (i == 0) lo = 0;
+    if (i == n - 1) hi = no - 1;
+    for (int o = lo; o <= hi && cnt < kPadMax; ++o) idx[cnt++] = o;
+    return cnt;
+  }
+  idx[cnt++] = i + p0;
+  const int a = p0 - i;                      // reflection across the leading edge
+  if (i > 0 && a >= 0) idx[cnt++] = a;
+  const int b = 2 * (n - 1) - i + p0;        // reflection across the trailing edge
+  if (i < n - 1 && b < no && b != i + p0) idx[cnt++] = b;
+  return cnt;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kT)
+pad_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int B, int C, int H, int W, int Ho,
+               int Wo, int pt, int pl, int mode) {
+  const int cv = C / 8;
+  const int64_t n = (int64_t)B * Ho * Wo * cv;
+  for (int64_t t = blockIdx.x * (int64_t)kT + threadIdx.x; t < n; t += (int64_t)gridDim.x * kT) {
+    const int c8 = (int)(t % cv);
+    int64_t p = t / cv;
+    const int ox = (int)(p % Wo);
+    p /= Wo;
+    const int oy = (int)(p % Ho);
+    const int b = (int)(p / Ho);
+    const int64_t src = (((int64_t)b * H + pad_src(oy, pt, H, mode)) * W +
+                         pad_src(ox, pl, W, mode)) * C + c8 * 8;
+    *reinterpret_cast<Pack<T, 8>*>(y + t * 8) = *reinterpret_cast<const Pack<T, 8>*>(x + src);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kT)
+pad_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int B, int C, int H, int W, int Ho,
+               int Wo, int pt, int pb, int pl, int pr, int mode) {
+  const int cv = C / 8;
+  const int64_t n = (int64_t)B * H * W * cv;
+  for (int64_t t = blockIdx.x * (int64_t)kT + threadIdx.x; t < n; t += (int64_t)gridDim.x * kT) {
+    const int c8 = (int)(t % cv);
+    int64_t p = t / cv;
+    const int ix = (int)(p % W);
+    p /= W;
+    const int iy = (int)(p % H);
+    const int b = (int)(p / H);
+    int ys[kPadMax], xs[kPadMax];
+    const int ny = pad_list(iy, pt, pb, H, mode, ys);
+    const int nx = pad_list(ix, pl, pr, W, mode, xs);
+    float acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+    const T* base = dy + (int64_t)b * Ho * Wo * C + c8 * 8;
+    for (int u = 0; u < ny; ++u)
+      for (int v = 0; v < nx; ++v) {
+        float g[8];
+        load_vec<T, 8>(base + ((int64_t)ys[u] * Wo + xs[v]) * C, g);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += g[k];
+      }
+    store_vec<T, 8>(dx + t * 8, acc);
+  }
+}
+
+int pad_grid(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + kT - 1) / kT, 65536)); }
+
 }  // namespace
+
+// x [B, C, H, W] channels-last (C % 8 == 0, bf16 / fp32) -> padded [B, C, H+pt+pb, W+pl+pr];
+// mode 0 reflect, 1 replicate.
+at::Tensor pad_nhwc_fwd(const at::Tensor& x, int64_t pl, int64_t pr, int64_t pt, int64_t pb,
+                        int64_t mode) {
+  IAMD_CHECK(x.is_cuda() && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                 x.size(1) % 8 == 0 &&
+                 (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat),
+             "pad_nhwc_fwd: packed channels-last bf16/fp32 tensor with C % 8 == 0 expected");
+  const int B = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  IAMD_CHECK(pl >= 0 && pr >= 0 && pt >= 0 && pb >= 0 && (mode == 1 ||
+             (pl < W && pr < W && pt < H && pb < H)), "pad_nhwc_fwd: bad padding");
+  const int Ho = (int)(H + pt + pb), Wo = (int)(W + pl + pr);
+  auto y = at::empty({B, C, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int64_t n = (int64_t)B * Ho * Wo * (C / 8);
+  if (n == 0) return y;
+  if (x.scalar_type() == at::kBFloat16)
+    hipLaunchKernelGGL(pad_fwd_kernel<__hip_bfloat16>, dim3(pad_grid(n)), dim3(kT), 0, stream(),
+                       reinterpret_cast<const __hip_bfloat16*>(x.data_ptr()),
+                       reinterpret_cast<__hip_bfloat16*>(y.data_ptr()), B, C, H, W, Ho, Wo,
+                       (int)pt, (int)pl, (int)mode);
+  else
+    hipLaunchKernelGGL(pad_fwd_kernel<float>, dim3(pad_grid(n)), dim3(kT), 0, stream(),
+                       x.data_ptr<float>(), y.data_ptr<float>(), B, C, H, W, Ho, Wo, (int)pt,
+                       (int)pl, (int)mode);
+  IAMD_LAUNCH_CHECK();
+  return y;
+}
+
+at::Tensor pad_nhwc_bwd(const at::Tensor& dy, int64_t H, int64_t W, int64_t pl, int64_t pr,
+                        int64_t pt, int64_t pb, int64_t mode) {
+  IAMD_CHECK(dy.is_cuda() && dy.dim() == 4 && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                 dy.size(1) % 8 == 0 && dy.size(2) == H + pt + pb && dy.size(3) == W + pl + pr,
+             "pad_nhwc_bwd: gradient shape / layout");
+  IAMD_CHECK(mode == 0 || (pt + 1 <= kPadMax && pb + 1 <= kPadMax && pl + 1 <= kPadMax &&
+                           pr + 1 <= kPadMax), "pad_nhwc_bwd: replicate padding above 15");
+  const int B = (int)dy.size(0), C = (int)dy.size(1);
+  auto dx = at::empty({B, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int64_t n = (int64_t)B * H * W * (C / 8);
+  if (n == 0) return dx;
+  if (dy.scalar_type() == at::kBFloat16)
+    hipLaunchKernelGGL(pad_bwd_kernel<__hip_bfloat16>, dim3(pad_grid(n)), dim3(kT), 0, stream(),
+                       reinterpret_cast<const __hip_bfloat16*>(dy.data_ptr()),
+                       reinterpret_cast<__hip_bfloat16*>(dx.data_ptr()), B, C, (int)H, (int)W,
+                       (int)dy.size(2), (int)dy.size(3), (int)pt, (int)pb, (int)pl, (int)pr,
+                       (int)mode);
+  else
+    hipLaunchKernelGGL(pad_bwd_kernel<float>, dim3(pad_grid(n)), dim3(kT), 0, stream(),
+                       dy.data_ptr<float>(), dx.data_ptr<float>(), B, C, (int)H, (int)W,
+                       (int)dy.size(2), (int)dy.size(3), (int)pt, (int)pb, (int)pl, (int)pr,
+                       (int)mode);
+  IAMD_LAUNCH_CHECK();
+  return dx;
+}
 
 // w: [Cout, Cin, KH, KW] bf16 channels-last -> [Cin, Cout, Jy, Jx] bf16 channels-last with
 // wt[ci][jy][jx][co] = w[co][qy + s (Jy-1-jy)][qx + s (Jx-1-jx)][ci], Jy = ceil((KH-qy)/s)

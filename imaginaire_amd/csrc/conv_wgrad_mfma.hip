@@ -257,7 +257,8 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma(WgradArgs a) {
 // the window read kx rows further down), so every staged byte feeds KW times the MFMAs of the
 // one-tap kernel: 3x / 5x fewer L2 -> LDS bytes per FLOP on the 3x3 / 5x5 SPADE convs, and the dy
 // fragments are read from LDS once for all taps. Accumulators: KW x (BNO/2 x BC/2) per wave
-// (tiles: 3 taps 128 x 64, 5 taps 64 x 64 — the 256-VGPR budget of 2 waves / SIMD, no spills).
+// (tiles: 3 taps 128 x 64, 5 / 7 taps 64 x 64 — the 256-VGPR budget of 2 waves / SIMD, no
+// spills).
 template <int BNO, int BC, int NT>
 __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma_mt(WgradArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -465,12 +466,12 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
   a.nks = ceil_div(a.M, kBP);
   a.nNt = Cout / (bno128 ? 128 : 64);
   a.nCt = Cin / (bc128 ? 128 : 64);
-  // multi-tap kernel: stride-1, undilated, whole-row k-steps, KW in {3, 5}
+  // multi-tap kernel: stride-1, undilated, whole-row k-steps, KW in {3, 5, 7}
   const char* mt_env = std::getenv("IMAGINAIRE_AMD_WGRAD_MT");
   const bool mt = (mt_env == nullptr || mt_env[0] != '0') && Wo % kBP == 0 && sw == 1 &&
-                  dw == 1 && (KW == 3 || KW == 5);
+                  dw == 1 && (KW == 3 || KW == 5 || KW == 7);
   if (mt) {  // tiles sized to the 256-VGPR budget of 2 waves / SIMD without spills:
-    // 3 taps 128 x 64 (or 64 x 64), 5 taps 64 x 64
+    // 3 taps 128 x 64 (or 64 x 64), 5 / 7 taps 64 x 64
     a.nNt = Cout / ((KW == 3 && bno128) ? 128 : 64);
     a.nCt = Cin / 64;
   }
@@ -482,7 +483,8 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
   const int slots = mt ? 512 : 256 * ((bno128 && bc128) ? 2 : (bno128 || bc128) ? 3 : 5);
   int S = 1;
   if (tiles < slots) {
-    const int smax = std::max(1, std::min(64, a.nks / 4));
+    // up to 1024 splits: a 1x1 conv's gradient is ONE 64 x 64 tile reduced over ~10^6 pixels
+    const int smax = std::max(1, std::min(1024, a.nks / 4));
     double best = -1.0;
     for (int s = 1; s <= smax; ++s) {
       const int blocks = tiles * s;
@@ -534,8 +536,10 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
     if (KW == 3) {
       if (bno128) launch_mt(I128(), I64(), T3());
       else launch_mt(I64(), I64(), T3());
-    } else {
+    } else if (KW == 5) {
       launch_mt(I64(), I64(), T5());
+    } else {
+      launch_mt(I64(), I64(), std::integral_constant<int, 7>());
     }
   } else if (bno128 && bc128) launch(I128(), I128());
   else if (bno128) launch(I128(), I64());

@@ -19,8 +19,10 @@
 //   * bf16 inputs with C % 32 == 0 (FlowNetC's 256-channel conv3 features) take the MFMA
 //     forward corr_fwd_mfma: a parity-split banded 16x48 v_mfma_f32_16x16x32_bf16 product per
 //     (row, displacement row, 16*stride2 pixels), fragments loaded straight from NHWC rows.
-//   * Backward is gather-form (one lane per (pixel, channel); displacement loop with
-//     broadcast reads of grad_out) so it needs no atomics and is deterministic.
+//   * Backward is gather-form, no atomics, deterministic. kernel_size 1 / stride1 1 (FlowNetC):
+//     corr_bwd_k1 stages, per (image row, displacement row), the two strips and grad_out rows the
+//     row's input gradients read in LDS and accumulates from there; other configurations use
+//     the per-element corr_bwd (one lane per (pixel, channel), 441-displacement loop).
 //   * Output is written channels-last [N, oH, oW, D*D] so the FlowNetC concat +
 //     conv3_1 that consume it stay NHWC.
 #include "common.h"
@@ -267,6 +269,107 @@ __global__ __launch_bounds__(256) void corr_bwd(
   g2[idx] = a2 * inv;
 }
 
+// Tiled backward for kernel_size == 1, stride1 == 1 (the FlowNetC configuration), gather form.
+// One workgroup owns 32 consecutive pixels of one image row and CC channels; per displacement
+// row tj it stages, in LDS, the two (32 + 2 R s2)-pixel strips the row's gradients read — the
+// second-image strip for d(in1), the first-image strip for d(in2) — plus the grad_out rows they
+// pair with, then each lane (pixel, CC/8 channels) accumulates its D displacements of this tj
+// from LDS. Every input / grad_out element is read from L2 once per (row, tj) instead of once
+// per (element, displacement) as in corr_bwd; deterministic, no atomics.
+constexpr int kBX = 32;       // pixels per workgroup
+constexpr int kBCC = 64;      // channels per workgroup (8 per lane)
+template <typename T>
+__global__ __launch_bounds__(256) void corr_bwd_k1(
+    const T* __restrict__ in1, const T* __restrict__ in2, const float* __restrict__ gout,
+    float* __restrict__ g1, float* __restrict__ g2, int H, int W, int C, int oH, int oW, int off,
+    int s2, int R, int D) {
+  extern __shared__ float smem[];
+  const int span = kBX + 2 * R * s2;
+  float* G1 = smem;                       // [kBX][D]
+  float* G2 = G1 + kBX * D;               // [span][D]
+  float* S2 = G2 + (span * D + 3) / 4 * 4;  // in2 strip [span][kBCC] (16-byte aligned)
+  float* S1 = S2 + span * kBCC;           // in1 strip [span][kBCC]
+  const int x0 = blockIdx.x * kBX, y = blockIdx.y;
+  const int nc = C / kBCC;
+  const int n = blockIdx.z / nc, c0 = (blockIdx.z - n * nc) * kBCC;
+  const int tid = threadIdx.x, px = tid >> 3, cl = (tid & 7) * 8;
+  const int DD = D * D;
+  const int ws = x0 - R * s2;             // image column of strip pixel 0
+  float a1[8], a2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) a1[k] = a2[k] = 0.f;
+  const int oy1 = y - off;                // output row paired with d(in1) of row y
+  for (int tj = 0; tj < D; ++tj) {
+    const int dy = (tj - R) * s2;
+    const int y2 = y + dy;                // in2 row read by d(in1)
+    const int yb = y - dy;                // in1 row (and output row yb - off) for d(in2)
+    const int oy2 = yb - off;
+    __syncthreads();
+    for (int e = tid; e < kBX * D; e += 256) {
+      const int p = e / D, ti = e - p * D;
+      const int ox = x0 + p - off;
+      float v = 0.f;
+      if ((unsigned)oy1 < (unsigned)oH && (unsigned)ox < (unsigned)oW)
+        v = gout[(((int64_t)n * oH + oy1) * oW + ox) * DD + tj * D + ti];
+      G1[e] = v;
+    }
+    for (int e = tid; e < span * D; e += 256) {
+      const int p = e / D, ti = e - p * D;
+      const int ox = ws + p - off;
+      float v = 0.f;
+      if ((unsigned)oy2 < (unsigned)oH && (unsigned)ox < (unsigned)oW)
+        v = gout[(((int64_t)n * oH + oy2) * oW + ox) * DD + tj * D + ti];
+      G2[e] = v;
+    }
+    for (int e = tid; e < span * (kBCC / 8); e += 256) {
+      const int p = e / (kBCC / 8), c8 = (e - p * (kBCC / 8)) * 8;
+      const int x = ws + p;
+      float v2[8], v1[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v2[k] = v1[k] = 0.f;
+      if ((unsigned)x < (unsigned)W) {
+        if ((unsigned)y2 < (unsigned)H)
+          load_vec<T, 8>(in2 + (((int64_t)n * H + y2) * W + x) * C + c0 + c8, v2);
+        if ((unsigned)yb < (unsigned)H)
+          load_vec<T, 8>(in1 + (((int64_t)n * H + yb) * W + x) * C + c0 + c8, v1);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        S2[p * kBCC + c8 + k] = v2[k];
+        S1[p * kBCC + c8 + k] = v1[k];
+      }
+    }
+    __syncthreads();
+    for (int ti = 0; ti < D; ++ti) {
+      const float w1 = G1[px * D + ti];
+      const int i1 = px + ti * s2;                 // strip index of x + (ti - R) s2
+      const int i2 = px + (2 * R - ti) * s2;       // strip index of x - (ti - R) s2
+      const float w2 = G2[i2 * D + ti];
+      const float4* r2 = reinterpret_cast<const float4*>(S2 + i1 * kBCC + cl);
+      const float4* r1 = reinterpret_cast<const float4*>(S1 + i2 * kBCC + cl);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const float4 b = r2[q], a = r1[q];
+        a1[4 * q + 0] += w1 * b.x; a1[4 * q + 1] += w1 * b.y;
+        a1[4 * q + 2] += w1 * b.z; a1[4 * q + 3] += w1 * b.w;
+        a2[4 * q + 0] += w2 * a.x; a2[4 * q + 1] += w2 * a.y;
+        a2[4 * q + 2] += w2 * a.z; a2[4 * q + 3] += w2 * a.w;
+      }
+    }
+  }
+  const int x = x0 + px;
+  if (x >= W) return;
+  const float inv = 1.f / (float)C;
+  const int64_t o = (((int64_t)n * H + y) * W + x) * C + c0 + cl;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    reinterpret_cast<float4*>(g1 + o)[q] =
+        make_float4(a1[4 * q] * inv, a1[4 * q + 1] * inv, a1[4 * q + 2] * inv, a1[4 * q + 3] * inv);
+    reinterpret_cast<float4*>(g2 + o)[q] =
+        make_float4(a2[4 * q] * inv, a2[4 * q + 1] * inv, a2[4 * q + 2] * inv, a2[4 * q + 3] * inv);
+  }
+}
+
 // ---- k8 channel norm (generic 4-D strides, fp32 accumulate) -------------------
 template <typename T>
 __global__ void chnorm_fwd(const T* __restrict__ x, T* __restrict__ out, int N, int C, int H,
@@ -376,6 +479,22 @@ std::vector<at::Tensor> correlation_backward(const at::Tensor& input1, const at:
   auto g2 = at::empty({N, C, H, W}, fopt);
   const int64_t total = (int64_t)N * H * W * C;
   if (total == 0) return {g1, g2};
+  const size_t span = (size_t)(kBX + 2 * R * s2);
+  const size_t lds = ((size_t)kBX * D + (span * D + 3) / 4 * 4 + 2 * span * kBCC) * sizeof(float);
+  const char* tb = std::getenv("IMAGINAIRE_AMD_CORR_BWD_TILED");
+  if ((tb == nullptr || tb[0] != '0') && ks == 1 && s1 == 1 && C % kBCC == 0 &&
+      lds <= 96 * 1024) {
+    IAMD_DISPATCH_FLOAT_TYPES(a.scalar_type(), "correlation_bwd_k1", [&] {
+      dim3 grid(ceil_div(W, kBX), H, N * (C / kBCC));
+      hipLaunchKernelGGL((corr_bwd_k1<scalar_t>), grid, dim3(256), lds, stream(),
+                         reinterpret_cast<const scalar_t*>(a.data_ptr()),
+                         reinterpret_cast<const scalar_t*>(b.data_ptr()), g.data_ptr<float>(),
+                         g1.data_ptr<float>(), g2.data_ptr<float>(), H, W, C, oH, oW,
+                         (int)(md - pad), (int)s2, R, D);
+    });
+    IAMD_LAUNCH_CHECK();
+    return {g1, g2};
+  }
   IAMD_DISPATCH_FLOAT_TYPES(a.scalar_type(), "correlation_bwd", [&] {
     hipLaunchKernelGGL((corr_bwd<scalar_t>), dim3(ceil_div(total, 256)), dim3(256), 0, stream(),
                        reinterpret_cast<const scalar_t*>(a.data_ptr()),

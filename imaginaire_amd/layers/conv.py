@@ -287,7 +287,7 @@ class HyperConv2d(nn.Module):
         if conv_bias is None and self.use_bias:
             raise ValueError('bias not provided but set to true during initialization')
         if self.padding_mode != 'zeros':
-            x = F.pad(x, [self.padding] * 4, mode=self.padding_mode)
+            x = nhwc_conv.pad(nhwc_conv.nhwc(x), [self.padding] * 4, self.padding_mode)
             padding = 0
         else:
             padding = self.padding

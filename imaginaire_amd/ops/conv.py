@@ -349,12 +349,45 @@ def conv2d_act(x, weight, bias=None, stride=1, padding=0, dilation=1, slope=1.0)
     return bias_act(conv2d(x, weight, None, stride, padding, dilation), bias, slope)
 
 
+class _PadNHWC(torch.autograd.Function):
+    """Reflect / replicate padding of NHWC activations (csrc/conv_aux.hip pad_nhwc_*)."""
+
+    @staticmethod
+    def forward(ctx, x, pad, mode):
+        ctx.conf = (x.shape[2], x.shape[3], pad, mode)
+        return _ext.ext().pad_nhwc_fwd(x, pad[0], pad[1], pad[2], pad[3], mode)
+
+    @staticmethod
+    def backward(ctx, dy):
+        h, w, pad, mode = ctx.conf
+        dy = dy.contiguous(memory_format=_CL)
+        return _ext.ext().pad_nhwc_bwd(dy, h, w, pad[0], pad[1], pad[2], pad[3], mode), \
+            None, None
+
+
+_PAD_MODES = {'reflect': 0, 'replicate': 1}
+
+
+def pad(x, pad_lrtb, mode):
+    """``F.pad(x, pad_lrtb, mode)`` for 4-D inputs; reflect / replicate padding of packed NHWC
+    activations (channels % 8 == 0) runs the HIP gather kernels (forward and backward)."""
+    m = _PAD_MODES.get(mode)
+    if m is not None and x.dim() == 4 and x.shape[1] % 8 == 0 and \
+            x.dtype in (torch.bfloat16, torch.float32) and _ext.use_native(x) and \
+            x.is_contiguous(memory_format=_CL) and len(pad_lrtb) == 4 and min(pad_lrtb) >= 0 and \
+            (m == 1 or (max(pad_lrtb[0], pad_lrtb[1]) < x.shape[3] and
+                        max(pad_lrtb[2], pad_lrtb[3]) < x.shape[2])) and \
+            (m == 0 or max(pad_lrtb) < 15):
+        return _PadNHWC.apply(x, tuple(int(p) for p in pad_lrtb), m)
+    return F.pad(x, pad_lrtb, mode=mode)
+
+
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1,
            padding_mode='zeros'):
     if groups == 1:
         weight = _match_channels(x, weight)
     if padding_mode != 'zeros' and padding_mode is not None:
-        x = F.pad(x, _pad_arg(padding), mode=padding_mode)
+        x = pad(nhwc(x), _pad_arg(padding), padding_mode)
         padding = 0
     if x.is_cuda and x.dim() == 4:
         st, pd, dl = _pair(stride), _pair(padding), _pair(dilation)

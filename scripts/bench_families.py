@@ -34,6 +34,9 @@ def main():
                    help='video families: frames per training sequence')
     p.add_argument('--pool', type=int, default=2)
     p.add_argument('--cpu', action='store_true', help='plumbing check on the CPU')
+    p.add_argument('--conv-log', action='store_true',
+                   help='after the timed steps, time every conv kernel call of one more '
+                        'iteration and print time / TF/s per (kind, shape, kernel) to stderr')
     p.add_argument('--set', nargs='*', default=[], metavar='KEY=VALUE',
                    help='dotted config overrides, e.g. gen.num_filters=64 '
                         'data.train.augmentations.random_crop_h_w=256,256 (scale a unit-test '
@@ -134,6 +137,21 @@ def main():
         data = step(args.warmup + it)
     sync()
     dt = (time.perf_counter() - t0) / args.steps
+    if args.conv_log and device.type == 'cuda':
+        from imaginaire_amd.ops import conv as conv_ops
+        conv_ops.enable_conv_log(True)
+        t1 = time.perf_counter()
+        step(args.warmup + args.steps)
+        sync()
+        wall = (time.perf_counter() - t1) * 1e3
+        rows = conv_ops.conv_log_summary()
+        conv_ops.enable_conv_log(False)
+        tot = sum(r[4] for r in rows)
+        fl = sum(r[5] * r[4] * 1e9 for r in rows)
+        print('conv kernels in one iteration: %.2f ms of %.1f ms wall, %.2f TFLOP, %.0f TF/s' % (
+            tot, wall, fl / 1e12, fl / max(tot, 1e-9) / 1e9))
+        for kind, path, desc, n, ms, tfs in rows[:40]:
+            print('%8.3f ms %3d  %-6s %-7s %5.0f TF/s  %s' % (ms, n, kind, path, tfs, desc))
     frames = 1
     if video:
         img = data.get('images') if isinstance(data, dict) else None

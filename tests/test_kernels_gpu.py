@@ -658,7 +658,9 @@ def test_nearest_resize_k12(dtype, case):
     (1, 64, 64, 5, 128, 3, 1),      # multi-tap 3x3, 64 x 64 tiles
     (2, 192, 128, 4, 64, 5, 2),     # multi-tap 5x5 (SPADE mlp_shared shape family)
     (1, 128, 64, 3, 64, 5, 2),
+    (2, 64, 64, 9, 70, 7, 0),       # multi-tap 7x7 (MUNIT reflect-padded input, p0: Wo = 64)
     (1, 64, 128, 7, 64, 3, 0),      # no padding: Wo = 62 -> one-tap kernel fallback
+    (1, 64, 64, 300, 256, 1, 0),    # 1x1: one tile, many pixel splits
 ])
 def test_conv2d_wgrad_multitap(case):
     """k11 multi-tap weight gradient (all KW taps of a filter row per block, shifted LDS
@@ -707,3 +709,23 @@ def test_cat0_view_of_adjacent_weights():
     fa, fb = views(x.detach())
     c = cat0(fb, fa)  # wrong order: not adjacent -> plain cat
     assert c.data_ptr() != fb.data_ptr() and torch.equal(c, torch.cat([fb, fa], 0))
+
+
+@pytest.mark.parametrize('mode', ['reflect', 'replicate'])
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('pad', [(3, 3, 3, 3), (1, 2, 0, 3), (1, 1, 1, 1)])
+def test_pad_nhwc(mode, dtype, pad):
+    """NHWC reflect / replicate padding (gather forward and backward) vs F.pad in fp32."""
+    from imaginaire_amd.ops.conv import pad as pad_nhwc
+    torch.manual_seed(15)
+    x = torch.randn(2, 16, 9, 11, device='cuda').to(dtype).contiguous(
+        memory_format=torch.channels_last).requires_grad_(True)
+    y = pad_nhwc(x, pad, mode)
+    xr = x.detach().float().requires_grad_(True)
+    yr = F.pad(xr, pad, mode=mode)
+    assert y.shape == yr.shape and torch.equal(y.float(), yr)
+    g = torch.randn_like(yr).to(dtype).float()
+    y.backward(g.to(dtype))
+    yr.backward(g)
+    tol = 3e-2 if dtype == torch.bfloat16 else 1e-5
+    assert torch.allclose(x.grad.float(), xr.grad, atol=tol, rtol=tol)
