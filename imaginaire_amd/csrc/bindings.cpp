@@ -81,12 +81,14 @@ std::vector<at::Tensor> resample2d_backward(const at::Tensor& in1, const at::Ten
 // conv_mfma.hip (k10)
 at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                        int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
-                       double slope);
+                       double slope, int64_t nb);
 at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t KH, int64_t KW,
                              int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh,
-                             int64_t dw, int64_t out_cout, int64_t out_cin, bool out_bf16);
+                             int64_t dw, int64_t out_cout, int64_t out_cin, bool out_bf16,
+                             int64_t nb);
 // conv_aux.hip
-at::Tensor conv_weight_flip_t(const at::Tensor& w, int64_t s, int64_t qy, int64_t qx);
+at::Tensor conv_weight_flip_t(const at::Tensor& w, int64_t s, int64_t qy, int64_t qx,
+                              int64_t nb);
 at::Tensor pad_nhwc_fwd(const at::Tensor& x, int64_t pl, int64_t pr, int64_t pt, int64_t pb,
                         int64_t mode);
 at::Tensor pad_nhwc_bwd(const at::Tensor& dy, int64_t H, int64_t W, int64_t pl, int64_t pr,
@@ -110,17 +112,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mt_sn_power", &iamd::mt_sn_power, "batched spectral-norm power iteration (k5b)");
   m.def("mt_sn_scale_cast", &iamd::mt_sn_scale_cast, "batched W/sigma -> bf16 (k5c)");
   m.def("profile_marker", &iamd::profile_marker, "named no-op kernel for trace phase splits");
-  m.def("conv2d_mfma", &iamd::conv2d_mfma, "MFMA implicit-GEMM NHWC conv + bias + act (k10)");
+  m.def("conv2d_mfma", &iamd::conv2d_mfma, "MFMA implicit-GEMM NHWC conv + bias + act (k10)",
+        py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("sh"), py::arg("sw"), py::arg("ph"),
+        py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("slope"), py::arg("nb") = 1);
   m.def("conv2d_wgrad_mfma", &iamd::conv2d_wgrad_mfma, "MFMA conv weight gradient (k11)",
         py::arg("dy"), py::arg("x"), py::arg("KH"), py::arg("KW"), py::arg("sh"), py::arg("sw"),
         py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("out_cout") = -1,
-        py::arg("out_cin") = -1, py::arg("out_bf16") = false);
+        py::arg("out_cin") = -1, py::arg("out_bf16") = false, py::arg("nb") = 1);
   m.def("pad_nhwc_fwd", &iamd::pad_nhwc_fwd, "NHWC reflect / replicate padding");
   m.def("pad_nhwc_bwd", &iamd::pad_nhwc_bwd, "NHWC reflect / replicate padding backward (gather)");
   m.def("conv_weight_flip_t", &iamd::conv_weight_flip_t,
         "flipped, in/out-transposed channels-last conv weight (dgrad-as-conv); s/qy/qx select "
-        "the taps of one stride-s phase", py::arg("w"), py::arg("s") = 1, py::arg("qy") = 0,
-        py::arg("qx") = 0);
+        "the taps of one stride-s phase; nb per-sample weights", py::arg("w"), py::arg("s") = 1,
+        py::arg("qy") = 0, py::arg("qx") = 0, py::arg("nb") = 1);
   m.def("sn_scale_backward", &iamd::sn_scale_backward, "spectral-norm W/sigma backward (k5d)");
   m.def("norm_stats", &iamd::norm_stats, "per-(group,channel) statistics (k1)");
   m.def("norm_apply", &iamd::norm_apply, "norm + SPADE modulation + activation (k1 fwd)");

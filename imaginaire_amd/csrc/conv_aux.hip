@@ -35,10 +35,13 @@ __global__ void __launch_bounds__(kT)
 flip_t_kernel(const __hip_bfloat16* __restrict__ w, __hip_bfloat16* __restrict__ wt, int Cout,
               int Cin, int KH, int KW, int Jy, int Jx, int s, int qy, int qx) {
   __shared__ __hip_bfloat16 tile[kTile * kLdsStride];
-  const int ci0 = blockIdx.x * kTile, co0 = blockIdx.y * kTile, tap = blockIdx.z;
+  const int KK = KH * KW, JJ = Jy * Jx;
+  const int ci0 = blockIdx.x * kTile, co0 = blockIdx.y * kTile;
+  const int nbz = blockIdx.z / JJ, tap = blockIdx.z - nbz * JJ;  // (sample, output tap)
+  w += (size_t)nbz * Cout * KK * Cin;
+  wt += (size_t)nbz * Cin * JJ * Cout;
   const int jy = tap / Jx, jx = tap - jy * Jx;
   const int ftap = (qy + s * (Jy - 1 - jy)) * KW + (qx + s * (Jx - 1 - jx));
-  const int KK = KH * KW, JJ = Jy * Jx;
   const int tid = threadIdx.x;
   // load: 64 co rows x 8 chunks of 8 ci
 #pragma unroll
@@ -251,18 +254,23 @@ at::Tensor pad_nhwc_bwd(const at::Tensor& dy, int64_t H, int64_t W, int64_t pl, 
 // w: [Cout, Cin, KH, KW] bf16 channels-last -> [Cin, Cout, Jy, Jx] bf16 channels-last with
 // wt[ci][jy][jx][co] = w[co][qy + s (Jy-1-jy)][qx + s (Jx-1-jx)][ci], Jy = ceil((KH-qy)/s)
 // (s = 1, q = 0: the spatially flipped, in/out-transposed weight of the stride-1 dgrad).
-at::Tensor conv_weight_flip_t(const at::Tensor& w, int64_t s, int64_t qy, int64_t qx) {
+// nb > 1: w holds nb per-sample weights [nb * Cout, ...] -> [nb * Cin, Cout, Jy, Jx].
+at::Tensor conv_weight_flip_t(const at::Tensor& w, int64_t s, int64_t qy, int64_t qx,
+                              int64_t nb) {
   IAMD_CHECK(w.is_cuda() && w.dim() == 4 && w.scalar_type() == at::kBFloat16,
              "conv_weight_flip_t: 4-D bf16 CUDA weight expected");
   IAMD_CHECK(w.is_contiguous(at::MemoryFormat::ChannelsLast),
              "conv_weight_flip_t: packed channels-last weight expected");
-  const int Cout = (int)w.size(0), Cin = (int)w.size(1), KH = (int)w.size(2), KW = (int)w.size(3);
+  IAMD_CHECK(nb >= 1 && w.size(0) % nb == 0, "conv_weight_flip_t: rows not divisible by nb");
+  const int Cout = (int)(w.size(0) / nb), Cin = (int)w.size(1), KH = (int)w.size(2),
+            KW = (int)w.size(3);
   IAMD_CHECK(Cout % 8 == 0 && Cin % 8 == 0, "conv_weight_flip_t: channels must be multiples of 8");
   IAMD_CHECK(s >= 1 && qy >= 0 && qx >= 0 && qy < KH && qx < KW, "conv_weight_flip_t: bad phase");
   const int Jy = (int)((KH - qy + s - 1) / s), Jx = (int)((KW - qx + s - 1) / s);
-  auto wt = at::empty({Cin, Cout, Jy, Jx}, w.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto wt = at::empty({nb * Cin, Cout, Jy, Jx},
+                      w.options().memory_format(at::MemoryFormat::ChannelsLast));
   if (wt.numel() == 0) return wt;
-  const dim3 grid(ceil_div(Cin, kTile), ceil_div(Cout, kTile), Jy * Jx);
+  const dim3 grid(ceil_div(Cin, kTile), ceil_div(Cout, kTile), (unsigned)(nb * Jy * Jx));
   hipLaunchKernelGGL(flip_t_kernel, grid, dim3(kT), 0, stream(),
                      reinterpret_cast<const __hip_bfloat16*>(w.data_ptr()),
                      reinterpret_cast<__hip_bfloat16*>(wt.data_ptr()), Cout, Cin, KH, KW, Jy, Jx,

@@ -61,6 +61,10 @@ struct ConvArgs {
   // is stored at pixel (b, oh * osy + ory, ow * osx + orx) of a [B, oH, oW, Cout] tensor.
   // omode 0: identity (row m is pixel m)
   int omode, oH, oW, osy, osx, ory, orx;
+  // batch of independent convs (per-sample weights: the fs-vid2vid hyper convolutions), one per
+  // blockIdx.z: operand / output / bias strides in elements between samples (v1 kernel only)
+  int64_t xbs, wbs, ybs;
+  int bbs, nz;
 };
 
 // destination pixel (row of the NHWC output) of GEMM row m
@@ -101,10 +105,11 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_fwd_mfma(ConvA
   // Buffer-resource loads straight into LDS: the per-lane 32-bit byte offset selects the
   // pixel row, the wave-uniform parts (tap, channel block, k-step) ride in SGPRs, and an
   // out-of-range offset (padding pixels, M tail) returns zeros from the buffer unit itself.
+  const int zb = blockIdx.z;  // sample of a batched (per-sample weight) launch
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<__hip_bfloat16*>(a.x), 0, a.xbytes, kBufCfg);
+      const_cast<__hip_bfloat16*>(a.x + (size_t)zb * a.xbs), 0, a.xbytes, kBufCfg);
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<__hip_bfloat16*>(a.w), 0, a.wbytes, kBufCfg);
+      const_cast<__hip_bfloat16*>(a.w + (size_t)zb * a.wbs), 0, a.wbytes, kBufCfg);
   const int lrow = tid >> 3;
   const int csw = (tid & 7) ^ (lrow & 7);
   const int HoWo = a.Ho * a.Wo;
@@ -212,8 +217,8 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_fwd_mfma(ConvA
     }
   }
 
-  if (a.part) {  // split-K: raw fp32 partials, bias/act/bf16 in conv_splitk_reduce
-    float* o = a.part + (size_t)blockIdx.y * a.M * a.Cout;
+  if (a.part) {  // split-K: raw fp32 partials [S][nz][M][Cout], bias/act/bf16 in the reduce
+    float* o = a.part + ((size_t)blockIdx.y * gridDim.z + zb) * a.M * a.Cout;
 #pragma unroll
     for (int j = 0; j < NI; ++j)
 #pragma unroll
@@ -229,10 +234,11 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_fwd_mfma(ConvA
   // ---- epilogue: bias + activation -> bf16 tile in LDS -> 16-byte row stores --------------
   __syncthreads();
   char* E = smem;
+  __hip_bfloat16* yz = a.y + (size_t)zb * a.ybs;
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
     const int cl = wn * (BN / 2) + j * 16 + (lane & 15);
-    const float bv = HAS_BIAS ? a.bias[n0 + cl] : 0.f;
+    const float bv = HAS_BIAS ? a.bias[zb * a.bbs + n0 + cl] : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -254,7 +260,7 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_fwd_mfma(ConvA
     const int m = m0 + rl;
     if (m < a.M) {
       const uint4 v = *reinterpret_cast<const uint4*>(E + rl * kEpiStride + ch * 16);
-      *reinterpret_cast<uint4*>(a.y + out_row(a, m) * a.Cout + n0 + ch * 8) = v;
+      *reinterpret_cast<uint4*>(yz + out_row(a, m) * a.Cout + n0 + ch * 8) = v;
     }
   }
 #endif  // __HIP_DEVICE_COMPILE__
@@ -731,13 +737,14 @@ conv_splitk_reduce(const float* __restrict__ part, const float* __restrict__ bia
       acc[4] += hi.x; acc[5] += hi.y; acc[6] += hi.z; acc[7] += hi.w;
     }
     const int c = (int)(e % C);
+    const int zb = (int)(e / ((int64_t)map.M * C));  // sample of a batched launch
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      float t = acc[k] + (bias ? bias[c + k] : 0.f);
+      float t = acc[k] + (bias ? bias[zb * map.bbs + c + k] : 0.f);
       acc[k] = t > 0.f ? t : t * slope;
     }
-    const int64_t m = e / C;
-    store_vec<__hip_bfloat16, 8>(y + out_row(map, (int)m) * C + (e - m * C), acc);
+    const int64_t m = e / C - (int64_t)zb * map.M;
+    store_vec<__hip_bfloat16, 8>(y + zb * map.ybs + out_row(map, (int)m) * C + (e % C), acc);
   }
 }
 
@@ -759,6 +766,7 @@ void run_conv(ConvArgs& a, const at::Tensor& x) {
   //       kept for probing only.
   int ver = 0;
   if (const char* e = std::getenv("IMAGINAIRE_AMD_CONV_V")) ver = std::atoi(e);
+  if (a.nz > 1) ver = 1;  // batched (per-sample weight) launches: v1 only
   const bool v3_ok = bn128 && KH * KW <= 31;
   const int v3_bn = Cout % 256 == 0 ? 256 : 128;
   const int v3_bm = v3_bn == 256 ? 256 : 512;
@@ -795,21 +803,22 @@ void run_conv(ConvArgs& a, const at::Tensor& x) {
       if (v == 128 || v == 256) bm = v;
     }
   }
+  if (a.nz > 1) bm = 128;
   const int64_t tiles = (int64_t)ceil_div(a.M, bm) * a.nNt;
   IAMD_CHECK(tiles < (1ll << 31), "conv2d_mfma: grid too large");
   // split-K over (tap, channel-block) k-steps when the tile grid cannot fill the chip (v1: 2
   // blocks per CU, v2 / v3: 1) — the wide-K / narrow-N data gradients of the SPADE gamma/beta
   // convs at 16x32 .. 64x128 and the 2048-channel head convs
-  int S = split_for(tiles, (v2 || v3) ? 256 : 512);
+  int S = split_for(tiles * a.nz, (v2 || v3) ? 256 : 512);
   a.kps = ceil_div(a.nk, S);
   S = ceil_div(a.nk, a.kps);
   at::Tensor part;
   a.part = nullptr;
   if (S > 1) {
-    part = at::empty({(int64_t)S * a.M * Cout}, x.options().dtype(at::kFloat));
+    part = at::empty({(int64_t)S * a.nz * a.M * Cout}, x.options().dtype(at::kFloat));
     a.part = part.data_ptr<float>();
   }
-  const dim3 grid((unsigned)tiles, (unsigned)S);
+  const dim3 grid((unsigned)tiles, (unsigned)S, (unsigned)a.nz);
   // main-loop schedule: VAR 2 (fragments up front + setprio) measured +1-5% over 0 / 1
   // (scripts/probe/conv_var_probe.py, profiles/conv_var_probe_mi355x.txt)
   int var = 2;
@@ -855,7 +864,7 @@ void run_conv(ConvArgs& a, const at::Tensor& x) {
   }
   if (S > 1) {
     IAMD_LAUNCH_CHECK();
-    const int64_t MC = (int64_t)a.M * Cout;
+    const int64_t MC = (int64_t)a.nz * a.M * Cout;
     const int blocks = (int)std::min<int64_t>((MC / 8 + 255) / 256, 8192);
     hipLaunchKernelGGL(conv_splitk_reduce, dim3(blocks), dim3(256), 0, stream(), a.part, a.bias,
                        a.y, S, MC, Cout, a.slope, a);
@@ -866,9 +875,11 @@ void run_conv(ConvArgs& a, const at::Tensor& x) {
 }  // namespace
 
 // y[B, Cout, Ho, Wo] (channels-last) = act(conv2d(x, w) + bias), x/w channels-last bf16.
+// nb > 1: a batch of nb independent convs with per-sample weights, w [nb * Cout, Cin, KH, KW]
+// (sample-major), bias [nb * Cout]: y[b] = act(conv2d(x[b], w[b]) + bias[b]).
 at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                        int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
-                       double slope) {
+                       double slope, int64_t nb) {
   IAMD_CHECK(x.is_cuda() && w.is_cuda(), "conv2d_mfma: CUDA tensors expected");
   IAMD_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16,
              "conv2d_mfma: bf16 operands expected");
@@ -877,7 +888,9 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
                  w.is_contiguous(at::MemoryFormat::ChannelsLast),
              "conv2d_mfma: packed channels-last operands expected");
   const int B = (int)x.size(0), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
-  const int Cout = (int)w.size(0), KH = (int)w.size(2), KW = (int)w.size(3);
+  IAMD_CHECK(nb >= 1 && (nb == 1 || B == nb) && w.size(0) % nb == 0,
+             "conv2d_mfma: per-sample weights need x batch == nb and w rows % nb == 0");
+  const int Cout = (int)(w.size(0) / nb), KH = (int)w.size(2), KW = (int)w.size(3);
   IAMD_CHECK(w.size(1) == Cin, "conv2d_mfma: channel mismatch ", w.size(1), " vs ", Cin);
   IAMD_CHECK(Cin % kBK == 0, "conv2d_mfma: Cin must be a multiple of 64, got ", Cin);
   IAMD_CHECK(Cout % 64 == 0, "conv2d_mfma: Cout must be a multiple of 64, got ", Cout);
@@ -892,7 +905,7 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
   auto y = at::empty({B, Cout, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   at::Tensor bf;
   if (bias.has_value() && bias->defined()) {
-    IAMD_CHECK(bias->numel() == Cout, "conv2d_mfma: bias size");
+    IAMD_CHECK(bias->numel() == Cout * nb, "conv2d_mfma: bias size");
     bf = bias->to(at::kFloat).contiguous();
   }
   ConvArgs a;
@@ -900,12 +913,17 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
   a.w = reinterpret_cast<const __hip_bfloat16*>(w.data_ptr());
   a.bias = bf.defined() ? bf.data_ptr<float>() : nullptr;
   a.y = reinterpret_cast<__hip_bfloat16*>(y.data_ptr());
-  a.xbytes = (int)(x.numel() * 2);
-  a.wbytes = (int)(w.numel() * 2);
+  a.xbytes = (int)(x.numel() / nb * 2);
+  a.wbytes = (int)(w.numel() / nb * 2);
+  a.nz = (int)nb;
+  a.xbs = nb > 1 ? (int64_t)H * W * Cin : 0;
+  a.wbs = nb > 1 ? (int64_t)Cout * KH * KW * Cin : 0;
+  a.ybs = nb > 1 ? (int64_t)Ho * Wo * Cout : 0;
+  a.bbs = nb > 1 ? Cout : 0;
   a.KH = KH;
   a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
   a.KW = KW; a.sh = (int)sh; a.sw = (int)sw; a.ph = (int)ph; a.pw = (int)pw; a.dh = (int)dh; a.dw = (int)dw;
-  a.M = B * Ho * Wo;
+  a.M = (B / (int)nb) * Ho * Wo;
   a.cpt = Cin / kBK;
   a.nk = KH * KW * a.cpt;
   a.slope = (float)slope;

@@ -51,6 +51,9 @@ struct WgradArgs {
   int Bn, H, W, Cin, Ho, Wo, Cout, KW, KK;
   int sh, sw, ph, pw, dh, dw;
   int M, nks, kps, nNt, nCt;
+  // batch of independent weight gradients (per-sample weights), one per blockIdx.y: operand
+  // strides in elements between samples; slabs are [S][nz][Cout][KK][Cin]
+  int64_t dybs, xbs;
 };
 
 // 16-byte chunk swizzle of a [64 pixel rows][RB bytes] image: the 8 rows read by one 32-lane
@@ -99,10 +102,11 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma(WgradArgs a) {
   // ---- DMA bookkeeping ------------------------------------------------------------------
   // buffer_load ... lds: per-lane 32-bit byte offsets, wave-uniform parts in SGPRs, and an
   // out-of-range offset (padding pixels, pixel tail) reads as zeros.
+  const int zb = blockIdx.y;  // sample of a batched (per-sample weight) launch
   const __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<__hip_bfloat16*>(a.dy), 0, a.dybytes, kBufCfg);
+      const_cast<__hip_bfloat16*>(a.dy + (size_t)zb * a.dybs), 0, a.dybytes, kBufCfg);
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<__hip_bfloat16*>(a.x), 0, a.xbytes, kBufCfg);
+      const_cast<__hip_bfloat16*>(a.x + (size_t)zb * a.xbs), 0, a.xbytes, kBufCfg);
   const int arow0 = tid / CPA, apos = tid % CPA;
   const int xrow0 = tid / CPX, xpos = tid % CPX;
   const int dyc = n0 + ((apos ^ swz<RA>(arow0)) << 3);  // rows arow0 + i*RSA share row&15
@@ -234,7 +238,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma(WgradArgs a) {
   }
 
   // ---- fp32 partial slab: row n (4 per lane), column ci (16 lanes contiguous) -------------
-  float* o = a.out + (size_t)split * a.Cout * a.KK * a.Cin;
+  float* o = a.out + ((size_t)split * gridDim.y + zb) * a.Cout * a.KK * a.Cin;
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -288,10 +292,11 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma_mt(WgradArgs a) {
   const int ks0 = split * a.kps;
   const int ks1 = min(a.nks, ks0 + a.kps);
 
+  const int zb = blockIdx.y;  // sample of a batched (per-sample weight) launch
   const __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<__hip_bfloat16*>(a.dy), 0, a.dybytes, kBufCfg);
+      const_cast<__hip_bfloat16*>(a.dy + (size_t)zb * a.dybs), 0, a.dybytes, kBufCfg);
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<__hip_bfloat16*>(a.x), 0, a.xbytes, kBufCfg);
+      const_cast<__hip_bfloat16*>(a.x + (size_t)zb * a.xbs), 0, a.xbytes, kBufCfg);
   const int arow0 = tid / CPA, apos = tid % CPA;
   const int xrow0 = tid / CPX, xpos = tid % CPX;
   const int dyc = n0 + ((apos ^ swz<RA>(arow0)) << 3);
@@ -405,7 +410,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma_mt(WgradArgs a) {
     }
   }
 
-  float* o = a.out + (size_t)split * a.Cout * a.KK * a.Cin;
+  float* o = a.out + ((size_t)split * gridDim.y + zb) * a.Cout * a.KK * a.Cin;
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int tap = ky * a.KW + t;
@@ -433,9 +438,11 @@ at::Tensor wgrad_finalize(const at::Tensor& part, int64_t S, int64_t Cop, int64_
 // dW [out_cout, out_cin, KH, KW] (channels-last memory = [Cout][KH][KW][Cin]) in fp32, or bf16
 // when out_bf16; out_cout / out_cin < 0 keep the (padded) channel counts of dy / x. Cropping
 // and casting ride in the split-K reduction (wgrad_finalize) instead of separate copies.
+// nb > 1: nb independent weight gradients (per-sample weights) -> [nb * Cout, Cin, KH, KW].
 at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t KH, int64_t KW,
                              int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh,
-                             int64_t dw, int64_t out_cout, int64_t out_cin, bool out_bf16) {
+                             int64_t dw, int64_t out_cout, int64_t out_cin, bool out_bf16,
+                             int64_t nb) {
   IAMD_CHECK(dy.is_cuda() && x.is_cuda(), "conv2d_wgrad_mfma: CUDA tensors expected");
   IAMD_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16,
              "conv2d_wgrad_mfma: bf16 operands expected");
@@ -446,6 +453,9 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
   const int B = (int)x.size(0), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
   const int Cout = (int)dy.size(1), Ho = (int)dy.size(2), Wo = (int)dy.size(3);
   IAMD_CHECK(dy.size(0) == B, "conv2d_wgrad_mfma: batch mismatch");
+  IAMD_CHECK(nb >= 1 && (nb == 1 || B == nb), "conv2d_wgrad_mfma: nb must be 1 or the batch");
+  IAMD_CHECK(nb == 1 || (out_cout < 0 && out_cin < 0),
+             "conv2d_wgrad_mfma: no channel crop for per-sample gradients");
   IAMD_CHECK(Cin % 64 == 0 && Cout % 64 == 0, "conv2d_wgrad_mfma: channels must be multiples of 64");
   IAMD_CHECK(Ho == (H + 2 * ph - dh * (KH - 1) - 1) / sh + 1 &&
                  Wo == (W + 2 * pw - dw * (KW - 1) - 1) / sw + 1,
@@ -457,12 +467,14 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
   WgradArgs a;
   a.dy = reinterpret_cast<const __hip_bfloat16*>(dy.data_ptr());
   a.x = reinterpret_cast<const __hip_bfloat16*>(x.data_ptr());
-  a.dybytes = (int)(dy.numel() * 2);
-  a.xbytes = (int)(x.numel() * 2);
-  a.Bn = B; a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
+  a.dybytes = (int)(dy.numel() / nb * 2);
+  a.xbytes = (int)(x.numel() / nb * 2);
+  a.dybs = nb > 1 ? dy.numel() / nb : 0;
+  a.xbs = nb > 1 ? x.numel() / nb : 0;
+  a.Bn = (int)(B / nb); a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
   a.KW = (int)KW; a.KK = KK;
   a.sh = (int)sh; a.sw = (int)sw; a.ph = (int)ph; a.pw = (int)pw; a.dh = (int)dh; a.dw = (int)dw;
-  a.M = B * Ho * Wo;
+  a.M = a.Bn * Ho * Wo;
   a.nks = ceil_div(a.M, kBP);
   a.nNt = Cout / (bno128 ? 128 : 64);
   a.nCt = Cin / (bc128 ? 128 : 64);
@@ -480,7 +492,8 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
   // per CU for the 64 / 48 / 32 KB LDS variants): a 2.3-round grid leaves the last round a
   // third full (measured: 1200 blocks ran at 28% MFMA issue vs 44% for k10,
   // profiles/pmc_conv_mi355x.txt)
-  const int slots = mt ? 512 : 256 * ((bno128 && bc128) ? 2 : (bno128 || bc128) ? 3 : 5);
+  const int slots = (mt ? 512 : 256 * ((bno128 && bc128) ? 2 : (bno128 || bc128) ? 3 : 5)) /
+                    (int)nb;
   int S = 1;
   if (tiles < slots) {
     // up to 1024 splits: a 1x1 conv's gradient is ONE 64 x 64 tile reduced over ~10^6 pixels
@@ -501,24 +514,25 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
   const bool direct = S == 1 && !out_bf16 && oc == Cout && oi == Cin;
   at::Tensor dW, part;
   if (direct) {
-    dW = at::empty({Cout, Cin, KH, KW},
+    dW = at::empty({nb * Cout, Cin, KH, KW},
                    x.options().dtype(at::kFloat).memory_format(at::MemoryFormat::ChannelsLast));
     a.out = dW.data_ptr<float>();
   } else {
-    part = at::empty({(int64_t)S * Cout * KK * Cin}, x.options().dtype(at::kFloat));
+    part = at::empty({(int64_t)S * nb * Cout * KK * Cin}, x.options().dtype(at::kFloat));
     a.out = part.data_ptr<float>();
   }
-  const int64_t grid = (int64_t)tiles * S;
-  IAMD_CHECK(grid < (1ll << 31), "conv2d_wgrad_mfma: grid too large");
+  const int64_t gx = (int64_t)tiles * S;
+  IAMD_CHECK(gx < (1ll << 31), "conv2d_wgrad_mfma: grid too large");
+  const dim3 grid((unsigned)gx, (unsigned)nb);
   const bool rows = Wo % kBP == 0;
   auto launch = [&](auto bv, auto cv) {
     constexpr int BNO = decltype(bv)::value;
     constexpr int BC = decltype(cv)::value;
     if (rows)
-      hipLaunchKernelGGL((conv_wgrad_mfma<BNO, BC, true>), dim3((unsigned)grid), dim3(kThreads),
+      hipLaunchKernelGGL((conv_wgrad_mfma<BNO, BC, true>), grid, dim3(kThreads),
                          0, stream(), a);
     else
-      hipLaunchKernelGGL((conv_wgrad_mfma<BNO, BC, false>), dim3((unsigned)grid), dim3(kThreads),
+      hipLaunchKernelGGL((conv_wgrad_mfma<BNO, BC, false>), grid, dim3(kThreads),
                          0, stream(), a);
   };
   using I64 = std::integral_constant<int, 64>;
@@ -527,7 +541,7 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
     constexpr int BNO = decltype(bv)::value;
     constexpr int BC = decltype(cv)::value;
     constexpr int NT = decltype(tv)::value;
-    hipLaunchKernelGGL((conv_wgrad_mfma_mt<BNO, BC, NT>), dim3((unsigned)grid), dim3(kThreads),
+    hipLaunchKernelGGL((conv_wgrad_mfma_mt<BNO, BC, NT>), grid, dim3(kThreads),
                        0, stream(), a);
   };
   if (mt) {
@@ -547,6 +561,9 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
   else launch(I64(), I64());
   IAMD_LAUNCH_CHECK();
   if (direct) return dW;
+  if (nb > 1)  // slabs [S][nb][Cout][KK][Cin]: one [nb * Cout] output, no crop
+    return wgrad_finalize(part, S, nb * Cout, Cin, nb * Cout, Cin, KH, KW,
+                          out_bf16 ? at::kBFloat16 : at::kFloat);
   return wgrad_finalize(part, S, Cout, Cin, oc, oi, KH, KW, out_bf16 ? at::kBFloat16 : at::kFloat);
 }
 

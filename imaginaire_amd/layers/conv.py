@@ -291,9 +291,15 @@ class HyperConv2d(nn.Module):
             padding = 0
         else:
             padding = self.padding
-        xg = x.reshape(1, b * x.size(1), x.size(2), x.size(3))
         if conv_weight.dim() == 4:
             conv_weight = conv_weight.unsqueeze(0).expand(b, *conv_weight.shape)
+        if self.stride == 1 and nhwc_conv.per_sample_eligible(x, conv_weight, self.stride,
+                                                               self.groups):
+            # one batched k10 launch (grid z = sample) instead of a grouped MIOpen conv
+            bias = conv_bias.reshape(b, -1) if conv_bias is not None else None
+            return nhwc_conv.conv2d_per_sample(nhwc_conv.nhwc(x), conv_weight, bias, padding,
+                                               self.dilation)
+        xg = x.reshape(1, b * x.size(1), x.size(2), x.size(3))
         if self.stride >= 1:
             w = conv_weight.reshape(b * conv_weight.size(1), *conv_weight.shape[2:])
             bias = conv_bias.reshape(-1) if conv_bias is not None else None

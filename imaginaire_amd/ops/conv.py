@@ -281,6 +281,83 @@ class _MfmaConv2d(torch.autograd.Function):
         return dx, dw, db, None, None, None, None
 
 
+class _MfmaConvPerSample(torch.autograd.Function):
+    """B independent convolutions with per-sample weights — the hyper convolutions of
+    few-shot vid2vid (reference layers/conv.py:575-590 loops over the batch) — as ONE batched
+    k10 launch (grid z = sample) forward, k10 on the per-sample flipped weights for the data
+    gradient and one batched k11 launch for the weight gradients. x [B, Cin, H, W], w [B, Cout,
+    Cin, KH, KW], bias [B, Cout]; stride 1, channels zero-padded to multiples of 64."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias, padding, dilation):
+        B, cout, cin, kh, kw = w.shape
+        cp, op = _round_up(cin, 64), _round_up(cout, 64)
+        xb = _pad_channels(x.to(torch.bfloat16), cp)
+        # sample-major channels-last weights [B][op][kh][kw][cp], zero-padded
+        wp = w.new_zeros((B, op, kh, kw, cp), dtype=torch.bfloat16)
+        wp[:, :cout, :, :, :cin] = w.permute(0, 1, 3, 4, 2)
+        wb = wp.view(B * op, kh, kw, cp).permute(0, 3, 1, 2)
+        bb = None
+        if bias is not None:
+            bb = bias.new_zeros((B, op), dtype=torch.float32)
+            bb[:, :cout] = bias
+            bb = bb.view(-1)
+        with _Logged('fwd', 'k10b', 2.0 * x.shape[2] * x.shape[3] * B * op * cp * kh * kw,
+                     _gemm_desc(xb, wb, (1, 1), padding) + ' nb%d' % B):
+            y = _ext.ext().conv2d_mfma(xb, wb, bb, 1, 1, padding[0], padding[1], dilation[0],
+                                       dilation[1], 1.0, B)
+        ctx.conf = (padding, dilation, cin, cout, x.dtype, w.dtype, x.shape[1],
+                    None if bias is None else bias.dtype)
+        ctx.save_for_backward(xb, wb)
+        return y if op == cout else y[:, :cout].contiguous(memory_format=_CL)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xb, wb = ctx.saved_tensors
+        padding, dilation, cin, cout, xdt, wdt, xc, bdt = ctx.conf
+        B, cp = xb.shape[0], xb.shape[1]
+        op = wb.shape[0] // B
+        kh, kw = wb.shape[2], wb.shape[3]
+        dy = _pad_channels(dy.to(torch.bfloat16), op)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            pt = (dilation[0] * (kh - 1) - padding[0], dilation[1] * (kw - 1) - padding[1])
+            wt = _ext.ext().conv_weight_flip_t(wb, 1, 0, 0, B)
+            dx = _ext.ext().conv2d_mfma(dy, wt, None, 1, 1, pt[0], pt[1], dilation[0],
+                                        dilation[1], 1.0, B)
+            dx = (dx[:, :xc] if dx.shape[1] != xc else dx).to(xdt)
+        if ctx.needs_input_grad[1]:
+            g = _ext.ext().conv2d_wgrad_mfma(dy, xb, kh, kw, 1, 1, padding[0], padding[1],
+                                             dilation[0], dilation[1], -1, -1, False, B)
+            # [B * op, cp, kh, kw] (memory [B][op][kh][kw][cp]) -> [B, cout, cin, kh, kw]
+            g = g.permute(0, 2, 3, 1).reshape(B, op, kh, kw, cp)[:, :cout, :, :, :cin]
+            dw = g.permute(0, 1, 4, 2, 3).to(wdt)
+        if ctx.needs_input_grad[2]:
+            db = dy.float().sum((2, 3))[:, :cout].to(bdt)
+        return dx, dw, db, None, None
+
+
+def per_sample_eligible(x, w, stride, groups):
+    """k10/k11 batched path for HyperConv2d: bf16 compute, stride 1, groups 1, 4-D x and
+    5-D per-sample weights, and enough pixels per sample to fill tiles."""
+    if not (x.is_cuda and x.dim() == 4 and w.dim() == 5 and groups == 1 and stride == 1 and
+            _mfma_enabled() and w.shape[0] == x.shape[0]):
+        return False
+    if _compute_dtype(x, w) != torch.bfloat16:
+        return False
+    # no padding-waste limit here: the alternative is MIOpen's grouped convolution, whose
+    # weight-gradient kernels ran at a few TF/s on the fs-vid2vid hyper layers (4.5 ms per call,
+    # profiles/recipe_fsvid2vid512_kernels_mi355x.txt), far below a 4x-padded MFMA tile
+    cin = w.shape[2]
+    return x.shape[2] * x.shape[3] >= 256 and \
+        x.numel() // x.shape[0] * _round_up(cin, 64) // max(cin, 1) * 2 < (1 << 30)
+
+
+def conv2d_per_sample(x, w, bias, padding, dilation=1):
+    """``y[b] = conv2d(x[b], w[b], bias[b])`` for every sample b in one batched MFMA launch."""
+    return _MfmaConvPerSample.apply(x, w, bias, _pair(padding), _pair(dilation))
+
+
 _WGRAD_CHOICE = {}
 
 

@@ -729,3 +729,36 @@ def test_pad_nhwc(mode, dtype, pad):
     yr.backward(g)
     tol = 3e-2 if dtype == torch.bfloat16 else 1e-5
     assert torch.allclose(x.grad.float(), xr.grad, atol=tol, rtol=tol)
+
+
+@pytest.mark.parametrize('case', [
+    # B, Cin, Cout, H, W, k, pad
+    (3, 32, 48, 20, 24, 3, 1),     # odd channel counts -> padded to 64
+    (2, 64, 128, 16, 32, 1, 0),
+    (3, 128, 64, 16, 16, 3, 1),
+])
+def test_conv2d_per_sample_batched(case):
+    """Per-sample-weight (hyper) convolution as one batched k10 / k11 launch vs a loop of fp32
+    convolutions (reference layers/conv.py:575-590)."""
+    from imaginaire_amd.ops import conv as C
+    B, cin, cout, H, W, k, p = case
+    torch.manual_seed(16)
+    x = torch.randn(B, cin, H, W, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last).requires_grad_(True)
+    w = (torch.randn(B, cout, cin, k, k, device='cuda') / (cin * k * k) ** 0.5).to(
+        torch.bfloat16).requires_grad_(True)
+    b = (torch.randn(B, cout, device='cuda') * 0.1).requires_grad_(True)
+    assert C.per_sample_eligible(x, w, 1, 1)
+    y = C.conv2d_per_sample(x, w, b, p)
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().float().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True)
+    yr = torch.stack([F.conv2d(xr[i:i + 1], wr[i], br[i], 1, p)[0] for i in range(B)])
+    assert y.shape == yr.shape
+    assert (y.float() - yr).abs().max().item() <= 1e-2 * max(1.0, yr.abs().max().item())
+    g = torch.randn_like(yr)
+    y.backward(g.to(y.dtype))
+    yr.backward(g)
+    for got, ref, name in ((x.grad, xr.grad, 'dx'), (w.grad, wr.grad, 'dw'), (b.grad, br.grad, 'db')):
+        e = (got.float() - ref).abs().max().item()
+        assert e <= 2e-2 * max(1.0, ref.abs().max().item()), (name, e)
