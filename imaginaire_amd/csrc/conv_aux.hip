@@ -76,35 +76,57 @@ flip_t_kernel(const __hip_bfloat16* __restrict__ w, __hip_bfloat16* __restrict__
 }
 
 // out[co][t][ci] = sum_s part[s][co][t][ci] for co < Cout, ci < Cin (padded slabs: Cop, Cip).
+// A block sums OPB = 256 / G outputs (4 channels each when VEC) with G thread groups splitting
+// the S slabs (s = g, g + G, ...), then adds the G partials in a fixed order (deterministic):
+// a one-tile weight gradient (1x1 conv, 64 x 64) is split over up to 1024 pixel ranges, and a
+// single thread per output walking all slabs was latency-bound at ~0.3 ms.
 template <typename T, bool VEC>
 __global__ void __launch_bounds__(kT)
 wgrad_finalize_kernel(const float* __restrict__ part, T* __restrict__ out, int S, int Cop, int Cip,
-                      int Cout, int Cin, int KK) {
+                      int Cout, int Cin, int KK, int G) {
+  __shared__ float4 red[kT];
+  const int opb = kT / G;
+  const int tid = threadIdx.x, o = tid % opb, g = tid / opb;
   const int per = VEC ? Cin / 4 : Cin;
   const int64_t n = (int64_t)Cout * KK * per;
   const int64_t slab = (int64_t)Cop * KK * Cip;
-  for (int64_t i = blockIdx.x * (int64_t)kT + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * kT) {
-    const int c = (int)(i % per);
-    const int64_t rt = i / per;  // co * KK + t
-    const int t = (int)(rt % KK);
-    const int co = (int)(rt / KK);
-    const int64_t src = ((int64_t)co * KK + t) * Cip + (VEC ? c * 4 : c);
-    if constexpr (VEC) {
-      float4 acc = *reinterpret_cast<const float4*>(part + src);
-      for (int s = 1; s < S; ++s) {
-        const float4 v = *reinterpret_cast<const float4*>(part + s * slab + src);
+  for (int64_t i0 = (int64_t)blockIdx.x * opb; i0 < n; i0 += (int64_t)gridDim.x * opb) {
+    const int64_t i = i0 + o;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int64_t rt = 0, src = 0;
+    int c = 0;
+    if (i < n) {
+      c = (int)(i % per);
+      rt = i / per;  // co * KK + t
+      const int t = (int)(rt % KK);
+      const int co = (int)(rt / KK);
+      src = ((int64_t)co * KK + t) * Cip + (VEC ? c * 4 : c);
+      for (int sl = g; sl < S; sl += G) {
+        if constexpr (VEC) {
+          const float4 v = *reinterpret_cast<const float4*>(part + sl * slab + src);
+          acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        } else {
+          acc.x += part[sl * slab + src];
+        }
+      }
+    }
+    red[tid] = acc;
+    __syncthreads();
+    if (g == 0 && i < n) {
+      for (int k = 1; k < G; ++k) {
+        const float4 v = red[k * opb + o];
         acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
       }
-      const float a[4] = {acc.x, acc.y, acc.z, acc.w};
-      T* o = out + rt * Cin + c * 4;
+      if constexpr (VEC) {
+        const float a[4] = {acc.x, acc.y, acc.z, acc.w};
+        T* dst = out + rt * Cin + c * 4;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) o[k] = from_f<T>(a[k]);
-    } else {
-      float acc = part[src];
-      for (int s = 1; s < S; ++s) acc += part[s * slab + src];
-      out[rt * Cin + c] = from_f<T>(acc);
+        for (int k = 0; k < 4; ++k) dst[k] = from_f<T>(a[k]);
+      } else {
+        out[rt * Cin + c] = from_f<T>(acc.x);
+      }
     }
+    __syncthreads();
   }
 }
 
@@ -293,17 +315,20 @@ at::Tensor wgrad_finalize(const at::Tensor& part, int64_t S, int64_t Cop, int64_
   const bool vec = Cin % 4 == 0 && Cip % 4 == 0;
   const int64_t n = Cout * KK * (vec ? Cin / 4 : Cin);
   if (n == 0) return out;
-  const int blocks = (int)std::min<int64_t>((n + kT - 1) / kT, 8192);
+  int G = 1;  // slab groups per output: more of them when there are many slabs, few outputs
+  while (G < 16 && G < S && (n * G * 2 <= (int64_t)256 * 4096 || G * 8 < S)) G *= 2;
+  const int opb = kT / G;
+  const int blocks = (int)std::min<int64_t>((n + opb - 1) / opb, 8192);
   auto launch = [&](auto tag) {
     using T = decltype(tag);
     if (vec)
       hipLaunchKernelGGL((wgrad_finalize_kernel<T, true>), dim3(blocks), dim3(kT), 0, stream(),
                          part.data_ptr<float>(), reinterpret_cast<T*>(out.data_ptr()), (int)S,
-                         (int)Cop, (int)Cip, (int)Cout, (int)Cin, KK);
+                         (int)Cop, (int)Cip, (int)Cout, (int)Cin, KK, G);
     else
       hipLaunchKernelGGL((wgrad_finalize_kernel<T, false>), dim3(blocks), dim3(kT), 0, stream(),
                          part.data_ptr<float>(), reinterpret_cast<T*>(out.data_ptr()), (int)S,
-                         (int)Cop, (int)Cip, (int)Cout, (int)Cin, KK);
+                         (int)Cop, (int)Cip, (int)Cout, (int)Cin, KK, G);
   };
   if (dtype == at::kBFloat16) launch(__hip_bfloat16());
   else if (dtype == at::kFloat) launch(float());

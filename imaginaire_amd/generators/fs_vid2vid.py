@@ -36,6 +36,7 @@ from imaginaire_amd.utils.data import (get_paired_input_image_channel_number,
 from imaginaire_amd.utils.distributed import master_only_print as print
 from imaginaire_amd.utils.init_weight import weights_init
 from imaginaire_amd.utils.misc import get_and_setattr, get_nested_attr
+from imaginaire_amd.ops.resize import interpolate, Upsample
 
 
 def _filters(num_filters, max_num_filters, n):
@@ -93,7 +94,7 @@ class Generator(nn.Module):
                 is_hyper_norm=self.use_hyper_spade and i < self.num_hyper_layers))
         self.conv_img = Conv2dBlock(num_filters, num_img_channels, conv_kernel_size,
                                     padding=padding, nonlinearity='leakyrelu', order='AC')
-        self.upsample = partial(F.interpolate, scale_factor=2)
+        self.upsample = partial(interpolate, scale_factor=2)
 
         self.warp_ref = getattr(flow_cfg, 'warp_ref', True)
         if self.warp_ref:
@@ -567,7 +568,7 @@ class FlowGenerator(nn.Module):
                for _ in range(num_blocks)]
         up = []
         for i in reversed(range(num_downsamples)):
-            up += [nn.Upsample(scale_factor=2), block(nf[i + 1], nf[i])]
+            up += [Upsample(scale_factor=2), block(nf[i + 1], nf[i])]
         self.down_flow = nn.Sequential(*down)
         self.res_flow = nn.Sequential(*res)
         self.up_flow = nn.Sequential(*up)
@@ -611,7 +612,7 @@ class LabelEmbedder(nn.Module):
                 ch[i], ch[i + 1], stride=2,
                 is_hyper_conv=(i < num_hyper_layers) and not self.has_decoder))
         if self.has_decoder:
-            self.upsample = nn.Upsample(scale_factor=2)
+            self.upsample = Upsample(scale_factor=2)
             for i in reversed(range(num_downsamples)):
                 ch_i = ch[i + 1] * (2 if self.unet and i != num_downsamples - 1 else 1)
                 setattr(self, 'up_%d' % i, block(ch_i, ch[i],

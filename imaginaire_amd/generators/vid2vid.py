@@ -26,6 +26,7 @@ from imaginaire_amd.model_utils.fs_vid2vid import extract_valid_pose_labels, res
 from imaginaire_amd.utils.data import (get_paired_input_image_channel_number,
                                        get_paired_input_label_channel_number)
 from imaginaire_amd.utils.init_weight import weights_init
+from imaginaire_amd.ops.resize import interpolate, Upsample
 
 
 class BaseNetwork(nn.Module):
@@ -105,13 +106,13 @@ class Generator(BaseNetwork):
         else:
             self.fc = LinearBlock(self.z_dim, top * self.sh * self.sw)
         self.downsample = nn.AvgPool2d(kernel_size=3, stride=2, padding=1)
-        self.upsample = partial(F.interpolate, scale_factor=2)
+        self.upsample = partial(interpolate, scale_factor=2)
         self.init_temporal_network()
 
     # ------------------------------------------------------------------ forward
     def _first_frame_code(self, label, z, bs, cond_maps_now):
         if self.use_segmap_as_input:
-            x = self.fc(F.interpolate(label, size=(self.sh, self.sw)))
+            x = self.fc(interpolate(label, size=(self.sh, self.sw)))
         else:
             if z is None:
                 z = torch.zeros(bs, self.z_dim, dtype=label.dtype, device=label.device)
@@ -275,7 +276,7 @@ class FlowGenerator(BaseNetwork):
                     for _ in range(self.num_res_blocks)]
         up_flow = []
         for i in reversed(range(num_downsamples)):
-            up_flow += [nn.Upsample(scale_factor=2),
+            up_flow += [Upsample(scale_factor=2),
                         block(self.get_num_filters(i + 1), self.get_num_filters(i))]
         self.down_lbl = nn.Sequential(*down_lbl)
         self.down_img = nn.Sequential(*down_img)

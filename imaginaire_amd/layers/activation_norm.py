@@ -422,7 +422,7 @@ class HyperSpatiallyAdaptiveNorm(nn.Module):
                 continue
             if type(cond_inputs[i]) == list:
                 cond_input, mask = cond_inputs[i]
-                mask = F.interpolate(mask, size=x.size()[2:], mode='bilinear',
+                mask = interpolate(mask, size=x.size()[2:], mode='bilinear',
                                      align_corners=False)
             else:
                 cond_input = cond_inputs[i]

@@ -19,6 +19,7 @@ from imaginaire_amd.ops import conv as nhwc_conv
 from imaginaire_amd.utils.distributed import master_only_print as print
 from imaginaire_amd.ops.loss import weighted_l1
 from imaginaire_amd.utils.misc import apply_imagenet_normalization
+from imaginaire_amd.ops.resize import interpolate
 
 
 class PerceptualLoss(nn.Module):
@@ -72,8 +73,8 @@ class PerceptualLoss(nn.Module):
         inp, target = apply_imagenet_normalization(inp), apply_imagenet_normalization(target)
         inp, target = inp[:, :3], target[:, :3]
         if self.resize:
-            inp = F.interpolate(inp, mode=self.resize_mode, size=(224, 224), align_corners=False)
-            target = F.interpolate(target, mode=self.resize_mode, size=(224, 224),
+            inp = interpolate(inp, mode=self.resize_mode, size=(224, 224), align_corners=False)
+            target = interpolate(target, mode=self.resize_mode, size=(224, 224),
                                    align_corners=False)
         dtype = next(self.model.parameters()).dtype
         loss = 0
@@ -95,9 +96,9 @@ class PerceptualLoss(nn.Module):
                     target_feature = F.instance_norm(target_feature)
                 loss = loss + weight * self.criterion(input_feature, target_feature).float()
             if scale != self.num_scales - 1:
-                inp = F.interpolate(inp, mode=self.resize_mode, scale_factor=0.5,
+                inp = interpolate(inp, mode=self.resize_mode, scale_factor=0.5,
                                     align_corners=False, recompute_scale_factor=True)
-                target = F.interpolate(target, mode=self.resize_mode, scale_factor=0.5,
+                target = interpolate(target, mode=self.resize_mode, scale_factor=0.5,
                                        align_corners=False, recompute_scale_factor=True)
         return loss.float()
 

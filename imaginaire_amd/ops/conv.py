@@ -137,6 +137,35 @@ def _pad_channels(t, c):
     return out
 
 
+def stack_nhwc(rows, dtype=None, align=64):
+    """``cat([cat(row, 1) for row in rows], 0)`` written ONCE into a channel-padded NHWC
+    buffer (channels rounded up to ``align``, zero tail marked for the convs): the
+    discriminator inputs label|image for real and fake, without the two channel concats, the
+    batch concat, the fp32 -> bf16 cast and the conv's own zero-padding copy. ``dtype``
+    defaults to the autocast dtype (or the first tensor's)."""
+    first = rows[0][0]
+    if dtype is None:
+        dtype = torch.get_autocast_dtype('cuda') if (first.is_cuda and
+                                                     torch.is_autocast_enabled('cuda')) \
+            else first.dtype
+    c = sum(t.shape[1] for t in rows[0])
+    cp = _round_up(c, align)
+    n = [row[0].shape[0] for row in rows]
+    out = torch.empty((sum(n), cp) + tuple(first.shape[2:]), dtype=dtype, device=first.device,
+                      memory_format=_CL)
+    o = 0
+    for row, k in zip(rows, n):
+        ch = 0
+        for t in row:
+            out[o:o + k, ch:ch + t.shape[1]] = t
+            ch += t.shape[1]
+        o += k
+    if cp > c:
+        out[:, c:].zero_()
+        mark_zero_tail(out, c)
+    return out
+
+
 def mark_zero_tail(t, valid_channels):
     """Declare channels ``[valid_channels:]`` of the NHWC tensor ``t`` to be zeros (a
     channel-padded buffer such as the 192-channel label|image discriminator input). A conv

@@ -119,6 +119,12 @@ def interpolate(x, size=None, scale_factor=None, mode='nearest', align_corners=N
                 recompute_scale_factor=None):
     # bilinear on NHWC activations: the k12 kernel in the activation dtype (autocast would
     # run an fp32 resize whose backward is an atomic scatter)
+    if recompute_scale_factor and scale_factor is not None and size is None and \
+            _bilinear_native_ok(x) and mode in ('bilinear', 'nearest'):
+        # recomputed scale = in / out of the floored size: the same as passing the size
+        sfh, sfw = _pair(scale_factor)
+        size = (int(math.floor(x.shape[2] * sfh)), int(math.floor(x.shape[3] * sfw)))
+        scale_factor, recompute_scale_factor = None, None
     if mode == 'bilinear' and not recompute_scale_factor and _bilinear_native_ok(x):
         return _bilinear(x, size, scale_factor, align_corners)
     if mode == 'nearest' and not recompute_scale_factor and _bilinear_native_ok(x):

@@ -34,6 +34,9 @@ def main():
                    help='video families: frames per training sequence')
     p.add_argument('--pool', type=int, default=2)
     p.add_argument('--cpu', action='store_true', help='plumbing check on the CPU')
+    p.add_argument('--op-sites', action='store_true',
+                   help='after the timed steps, attribute the aten glue of one more iteration '
+                        'to Python call sites (scripts/probe/op_sites.py) on stderr')
     p.add_argument('--conv-log', action='store_true',
                    help='after the timed steps, time every conv kernel call of one more '
                         'iteration and print time / TF/s per (kind, shape, kernel) to stderr')
@@ -137,6 +140,10 @@ def main():
         data = step(args.warmup + it)
     sync()
     dt = (time.perf_counter() - t0) / args.steps
+    if args.op_sites and device.type == 'cuda':
+        sys.path.insert(0, os.path.join(HERE, 'probe'))
+        from op_sites import record_sites
+        record_sites(lambda: step(args.warmup + args.steps + 1), out=sys.stderr)
     if args.conv_log and device.type == 'cuda':
         from imaginaire_amd.ops import conv as conv_ops
         conv_ops.enable_conv_log(True)

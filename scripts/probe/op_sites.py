@@ -20,13 +20,16 @@ import torch  # noqa: E402
 from torch.utils._python_dispatch import TorchDispatchMode  # noqa: E402
 
 
+DEFAULT_OPS = ('copy_,_to_copy,cat,fill_,add_,add,mul,div,flip,upsample_nearest2d,'
+               'upsample_bilinear2d,avg_pool2d,clone,sub,mul_,zero_,constant_pad_nd,contiguous,'
+               'reflection_pad2d,index,grid_sampler_2d,sum,mean')
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument('--config', default=os.path.join(HERE, 'configs', 'bench',
                                                     'spade_256x512_synthetic.yaml'))
-    p.add_argument('--ops', default='copy_,_to_copy,cat,fill_,add_,add,mul,div,flip,'
-                                    'upsample_nearest2d,upsample_bilinear2d,avg_pool2d,'
-                                    'clone,sub,mul_,zero_,constant_pad_nd,contiguous')
+    p.add_argument('--ops', default=DEFAULT_OPS)
     p.add_argument('--top', type=int, default=60)
     args = p.parse_args()
     from imaginaire_amd.config import Config
@@ -47,7 +50,13 @@ def main():
     for i in range(2):
         step(i)
     torch.cuda.synchronize()
-    wanted = set(args.ops.split(','))
+    record_sites(lambda: step(2), args.ops, args.top)
+
+
+def record_sites(step_fn, ops=DEFAULT_OPS, top=60, out=sys.stdout):
+    """Run ``step_fn`` once under a dispatch-mode recorder of the listed aten ops; print the
+    call sites sorted by output bytes (forward and the autograd engine's backward thread)."""
+    wanted = set(ops.split(','))
     stats = collections.defaultdict(lambda: [0, 0])
     lock = threading.Lock()
 
@@ -59,10 +68,10 @@ def main():
 
     class Mode(TorchDispatchMode):
         def __torch_dispatch__(self, func, types, args=(), kwargs=None):
-            out = func(*args, **(kwargs or {}))
+            out_ = func(*args, **(kwargs or {}))
             name = func.__name__.split('.')[0]
             if name in wanted:
-                t = out if torch.is_tensor(out) else (args[0] if args and torch.is_tensor(
+                t = out_ if torch.is_tensor(out_) else (args[0] if args and torch.is_tensor(
                     args[0]) else None)
                 nbytes = t.numel() * t.element_size() if t is not None else 0
                 shape = tuple(t.shape) if t is not None else ()
@@ -71,18 +80,20 @@ def main():
                     s = stats[(name, shape, dt, site())]
                     s[0] += 1
                     s[1] += nbytes
-            return out
+            return out_
 
     # the backward engine runs on its own thread: enable the mode there too
     torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch(False)
     with Mode():
-        step(2)
+        step_fn()
     torch.cuda.synchronize()
     rows = sorted(stats.items(), key=lambda kv: -kv[1][1])
     tot = sum(v[1] for _, v in rows)
-    print('recorded %d op calls, %.2f GB output' % (sum(v[0] for _, v in rows), tot / 1e9))
-    for (name, shape, dt, st), (n, b) in rows[:args.top]:
-        print('%8.1f MB %4d  %-20s %-9s %-26s %s' % (b / 1e6, n, name, dt, str(shape)[:26], st))
+    print('recorded %d op calls, %.2f GB output' % (sum(v[0] for _, v in rows), tot / 1e9),
+          file=out)
+    for (name, shape, dt, st), (n, b) in rows[:top]:
+        print('%8.1f MB %4d  %-20s %-9s %-26s %s' % (b / 1e6, n, name, dt, str(shape)[:26], st),
+              file=out)
 
 
 if __name__ == '__main__':
