@@ -504,12 +504,18 @@ def _save_checkpoint(cfg, net_G, net_D, opt_G, opt_D, sch_G, sch_D, current_epoc
         current_epoch, current_iteration)
     save_path = os.path.join(cfg.logdir, latest_checkpoint_path)
     os.makedirs(cfg.logdir, exist_ok=True)
+    # written to a temporary name and renamed, pointer file last: a rank killed mid-save
+    # (watchdog, lost node) never leaves latest_checkpoint.txt naming a torn file, so the
+    # restarted job auto-resumes from the previous complete checkpoint
     torch.save({'net_G': net_G.state_dict(), 'net_D': net_D.state_dict(),
                 'opt_G': opt_G.state_dict(), 'opt_D': opt_D.state_dict(),
                 'sch_G': sch_G.state_dict(), 'sch_D': sch_D.state_dict(),
                 'current_epoch': current_epoch, 'current_iteration': current_iteration},
-               save_path)
-    with open(os.path.join(cfg.logdir, 'latest_checkpoint.txt'), 'wt') as f:
+               save_path + '.tmp')
+    os.replace(save_path + '.tmp', save_path)
+    pointer = os.path.join(cfg.logdir, 'latest_checkpoint.txt')
+    with open(pointer + '.tmp', 'wt') as f:
         f.write('latest_checkpoint: %s' % latest_checkpoint_path)
+    os.replace(pointer + '.tmp', pointer)
     print('Save checkpoint to {}'.format(save_path))
     return save_path

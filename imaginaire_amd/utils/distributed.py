@@ -32,6 +32,11 @@ def init_dist(local_rank=None, backend=None, **kwargs):
     os.environ.setdefault('MASTER_PORT', '29500')
     if backend == 'nccl' and use_gpu:
         kwargs.setdefault('device_id', torch.device('cuda', local_rank))
+        # a collective that exceeds the timeout aborts the communicator and raises instead
+        # of blocking every rank forever (utils/health.py)
+        os.environ.setdefault('TORCH_NCCL_ASYNC_ERROR_HANDLING', '3')
+    from imaginaire_amd.utils.health import dist_timeout
+    kwargs.setdefault('timeout', dist_timeout())
     dist.init_process_group(backend=backend, init_method='env://', **kwargs)
     return local_rank if use_gpu else -1
 

@@ -20,6 +20,7 @@ from imaginaire_amd.utils.cudnn import init_cudnn  # noqa: E402
 from imaginaire_amd.utils.dataset import get_train_and_val_dataloader  # noqa: E402
 from imaginaire_amd.utils.distributed import init_dist, get_world_size  # noqa: E402
 from imaginaire_amd.utils.distributed import master_only_print as print  # noqa: E402
+from imaginaire_amd.utils.health import FaultInjector, StragglerMonitor, Watchdog  # noqa: E402
 from imaginaire_amd.utils.logging import init_logging, make_logging_dir  # noqa: E402
 from imaginaire_amd.utils.trainer import (get_model_optimizer_and_scheduler, get_trainer,  # noqa
                                           set_random_seed)
@@ -38,6 +39,10 @@ def parse_args(argv=None):
     parser.add_argument('--backend', default=None, help='nccl (RCCL) / gloo; default auto')
     parser.add_argument('--no_graph', '--no-graph', action='store_true',
                         help='run every iteration eagerly (no hipGraph replay)')
+    parser.add_argument('--watchdog_timeout', '--watchdog-timeout', type=float,
+                        default=float(os.environ.get('IMAGINAIRE_AMD_WATCHDOG_S', 900)),
+                        help='seconds without a finished iteration before the rank dumps its '
+                             'stacks to <logdir>/hang_rank<R>.txt and exits (0: off)')
     return parser.parse_args(argv)
 
 
@@ -65,21 +70,33 @@ def main(argv=None):
     # trainer supports it (single process, see imaginaire_amd/utils/cuda_graph.py)
     from imaginaire_amd.utils.cuda_graph import make_trainer_step
     train_step, _ = make_trainer_step(trainer, enabled=not args.no_graph)
-    for epoch in range(current_epoch, cfg.max_epoch):
-        print('Epoch {} ...'.format(epoch))
-        if hasattr(train_data_loader.sampler, 'set_epoch'):
-            train_data_loader.sampler.set_epoch(current_epoch)
-        trainer.start_of_epoch(current_epoch)
-        for it, data in enumerate(train_data_loader):
-            data = trainer.start_of_iteration(data, current_iteration)
-            train_step(data)
-            current_iteration += 1
-            trainer.end_of_iteration(data, current_epoch, current_iteration)
-            if current_iteration >= cfg.max_iter:
-                print('Done with training!!!')
-                return
-        current_epoch += 1
-        trainer.end_of_epoch(data, current_epoch, current_iteration)
+    # failure detection (imaginaire_amd/utils/health.py): per-rank hang watchdog, optional
+    # fault injection, straggler report at logging boundaries
+    faults = FaultInjector()
+    stragglers = StragglerMonitor()
+    with Watchdog(args.watchdog_timeout, cfg.logdir) as watchdog:
+        watchdog.beat(current_iteration, 'start')
+        for epoch in range(current_epoch, cfg.max_epoch):
+            print('Epoch {} ...'.format(epoch))
+            if hasattr(train_data_loader.sampler, 'set_epoch'):
+                train_data_loader.sampler.set_epoch(current_epoch)
+            trainer.start_of_epoch(current_epoch)
+            for it, data in enumerate(train_data_loader):
+                data = trainer.start_of_iteration(data, current_iteration)
+                if faults:
+                    data = faults.apply(current_iteration, data)
+                train_step(data)
+                current_iteration += 1
+                trainer.end_of_iteration(data, current_epoch, current_iteration)
+                watchdog.beat(current_iteration)
+                stragglers.tick()
+                if get_world_size() > 1 and current_iteration % cfg.logging_iter == 0:
+                    stragglers.report()
+                if current_iteration >= cfg.max_iter:
+                    print('Done with training!!!')
+                    return
+            current_epoch += 1
+            trainer.end_of_epoch(data, current_epoch, current_iteration)
     print('Done with training!!!')
 
 
