@@ -86,6 +86,11 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
                              int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh,
                              int64_t dw, int64_t out_cout, int64_t out_cin, bool out_bf16,
                              int64_t nb);
+// conv_tapsplit.hip
+at::Tensor conv_tap_sum(const at::Tensor& z, const c10::optional<at::Tensor>& bias, int64_t Cout,
+                        int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t dh, int64_t dw);
+at::Tensor conv_tap_gather(const at::Tensor& dy, int64_t Cz, int64_t KH, int64_t KW, int64_t ph,
+                           int64_t pw, int64_t dh, int64_t dw, int64_t H, int64_t W);
 // conv_aux.hip
 at::Tensor conv_weight_flip_t(const at::Tensor& w, int64_t s, int64_t qy, int64_t qx,
                               int64_t nb);
@@ -119,6 +124,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dy"), py::arg("x"), py::arg("KH"), py::arg("KW"), py::arg("sh"), py::arg("sw"),
         py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("out_cout") = -1,
         py::arg("out_cin") = -1, py::arg("out_bf16") = false, py::arg("nb") = 1);
+  m.def("conv_tap_sum", &iamd::conv_tap_sum, "tap-split conv: sum of per-tap partials (+bias)");
+  m.def("conv_tap_gather", &iamd::conv_tap_gather, "tap-split conv backward: dy -> per-tap dZ");
   m.def("pad_nhwc_fwd", &iamd::pad_nhwc_fwd, "NHWC reflect / replicate padding");
   m.def("pad_nhwc_bwd", &iamd::pad_nhwc_bwd, "NHWC reflect / replicate padding backward (gather)");
   m.def("conv_weight_flip_t", &iamd::conv_weight_flip_t,

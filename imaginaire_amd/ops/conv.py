@@ -387,6 +387,80 @@ def conv2d_per_sample(x, w, bias, padding, dilation=1):
     return _MfmaConvPerSample.apply(x, w, bias, _pair(padding), _pair(dilation))
 
 
+class _TapSplitConv2d(torch.autograd.Function):
+    """Narrow-output (Cout <= 8) stride-1 convolutions — the RGB image heads — re-associated
+    as a 1x1 MFMA GEMM into per-tap partial outputs Z[p, t*Cout + c] (k10, N = KH*KW*Cout
+    padded to 64) followed by a tap-sum gather (csrc/conv_tapsplit.hip). Backward: per-tap
+    gather of dy into dZ, then dx = k10 1x1 conv of dZ with the transposed Z weight and
+    dW = k11 1x1 weight gradient of (dZ, x). Every input element is read once by a useful-width
+    MFMA tile instead of streaming the KH*KW*Cin im2col operand for 3 outputs per pixel."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias, padding, dilation):
+        cout, cin, kh, kw = w.shape
+        cp, cz = _round_up(cin, 64), _round_up(cout * kh * kw, 64)
+        xb = _pad_channels(x.to(torch.bfloat16), cp)
+        # Wz[t*cout + c, ci] = w[c, ci, t]
+        wz = torch.zeros((cz, cp), dtype=torch.bfloat16, device=w.device)
+        wz[:cout * kh * kw, :cin] = w.to(torch.bfloat16).permute(2, 3, 0, 1).reshape(-1, cin)
+        wz = wz.view(cz, cp, 1, 1)
+        ho, wo = _out_hw(x.shape[2], x.shape[3], (kh, kw), (1, 1), padding, dilation)
+        with _Logged('fwd', 'k10t', 2.0 * x.shape[0] * x.shape[2] * x.shape[3] * cz * cp,
+                     _gemm_desc(xb, w, (1, 1), padding) + ' tapsplit'):
+            z = _ext.ext().conv2d_mfma(xb, wz, None, 1, 1, 0, 0, 1, 1, 1.0, 1)
+            y = _ext.ext().conv_tap_sum(z, bias, cout, kh, kw, padding[0], padding[1],
+                                        dilation[0], dilation[1])
+        ctx.conf = (padding, dilation, cin, cout, kh, kw, x.dtype, w.dtype,
+                    None if bias is None else bias.dtype, x.shape[1])
+        ctx.save_for_backward(xb, wz)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xb, wz = ctx.saved_tensors
+        padding, dilation, cin, cout, kh, kw, xdt, wdt, bdt, xc = ctx.conf
+        cz, cp = wz.shape[0], wz.shape[1]
+        dz = _ext.ext().conv_tap_gather(dy.to(torch.bfloat16), cz, kh, kw, padding[0], padding[1],
+                                        dilation[0], dilation[1], xb.shape[2], xb.shape[3])
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            wzt = wz.view(cz, cp).t().contiguous().view(cp, cz, 1, 1)
+            dx = _ext.ext().conv2d_mfma(dz, wzt, None, 1, 1, 0, 0, 1, 1, 1.0, 1)
+            dx = (dx[:, :xc] if dx.shape[1] != xc else dx).to(xdt)
+        if ctx.needs_input_grad[1]:
+            g = _ext.ext().conv2d_wgrad_mfma(dz, xb, 1, 1, 1, 1, 0, 0, 1, 1, cout * kh * kw, cin,
+                                             False, 1)
+            # [t*cout + c, ci] -> [c, ci, kh, kw]
+            dw = g.reshape(kh, kw, cout, cin).permute(2, 3, 0, 1).to(wdt)
+        if ctx.needs_input_grad[2]:
+            db = dy.float().sum((0, 2, 3)).to(bdt)
+        return dx, dw, db, None, None
+
+
+_TAPSPLIT = os.environ.get('IMAGINAIRE_AMD_TAPSPLIT', '1') == '1'
+
+
+def tapsplit_eligible(x, w, stride, padding, dilation, groups):
+    """The tap-split path (``_TapSplitConv2d``) for narrow RGB heads: bf16 compute, stride 1,
+    groups 1, Cout <= 8 with a spatial filter, a wide input and enough pixels to fill the chip."""
+    if not (_TAPSPLIT and x.is_cuda and x.dim() == 4 and w.dim() == 4 and groups == 1 and
+            stride == (1, 1) and _mfma_enabled()):
+        return False
+    cout, cin, kh, kw = w.shape
+    if not (cout <= 8 and kh * kw > 1 and cin >= 32 and kh * kw * cout <= 512):
+        return False
+    if _compute_dtype(x, w) != torch.bfloat16:
+        return False
+    ho, wo = _out_hw(x.shape[2], x.shape[3], (kh, kw), stride, padding, dilation)
+    if (ho, wo) != (x.shape[2] + 2 * padding[0] - dilation[0] * (kh - 1),
+                    x.shape[3] + 2 * padding[1] - dilation[1] * (kw - 1)) or ho <= 0 or wo <= 0:
+        return False
+    npix = x.shape[0] * x.shape[2] * x.shape[3]
+    cp, cz = _round_up(cin, 64), _round_up(cout * kh * kw, 64)
+    # k10 / k11 32-bit buffer offsets on x and on the partials Z / dZ
+    return npix >= 128 * 64 and npix * cp * 2 < (1 << 30) and npix * cz * 2 < (1 << 30)
+
+
 _WGRAD_CHOICE = {}
 
 
@@ -447,6 +521,8 @@ def conv2d_act(x, weight, bias=None, stride=1, padding=0, dilation=1, slope=1.0)
     one k10 launch when eligible, otherwise MIOpen conv + k2 bias-act epilogue."""
     stride, padding, dilation = _pair(stride), _pair(padding), _pair(dilation)
     weight = _match_channels(x, weight)
+    if slope == 1.0 and tapsplit_eligible(x, weight, stride, padding, dilation, 1):
+        return _TapSplitConv2d.apply(x, weight, bias, padding, dilation)
     if mfma_eligible(x, weight, stride, padding, dilation, 1):
         return _MfmaConv2d.apply(x, weight, bias, stride, padding, dilation, slope)
     from imaginaire_amd.ops.bias_act import bias_act
@@ -497,6 +573,8 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1,
         padding = 0
     if x.is_cuda and x.dim() == 4:
         st, pd, dl = _pair(stride), _pair(padding), _pair(dilation)
+        if tapsplit_eligible(x, weight, st, pd, dl, groups):
+            return _TapSplitConv2d.apply(x, weight, bias, pd, dl)
         if mfma_eligible(x, weight, st, pd, dl, groups):
             return _MfmaConv2d.apply(x, weight, bias, st, pd, dl, 1.0)
         cin = weight.shape[1]

@@ -762,3 +762,46 @@ def test_conv2d_per_sample_batched(case):
     for got, ref, name in ((x.grad, xr.grad, 'dx'), (w.grad, wr.grad, 'dw'), (b.grad, br.grad, 'db')):
         e = (got.float() - ref).abs().max().item()
         assert e <= 2e-2 * max(1.0, ref.abs().max().item()), (name, e)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case', [
+    # B, cin, cout, H, W, k, p, d, bias, autocast
+    (2, 256, 3, 64, 96, 5, 2, 1, True, False),    # SPADE conv_img (256 -> 3, 5x5)
+    (1, 64, 3, 96, 100, 7, 3, 1, True, True),     # pix2pixHD / vid2vid 7x7 head, fp32 params
+    (2, 96, 1, 65, 79, 3, 2, 2, False, False),    # dilation, odd sizes, Cin padded to 128
+    (1, 128, 8, 96, 98, 3, 0, 1, True, False),    # valid conv (no padding), Cout 8
+])
+def test_conv_tapsplit_fwd_bwd(case):
+    """Tap-split narrow-output conv (1x1 k10 into per-tap partials + tap-sum gather; backward
+    tap gather + k10 / k11 1x1) against an fp32 F.conv2d."""
+    from imaginaire_amd.ops import conv as C
+    B, cin, cout, H, W, k, p, d, bias, amp = case
+    torch.manual_seed(5)
+    dt = torch.float32 if amp else torch.bfloat16
+    x = torch.randn(B, cin, H, W, device='cuda').to(dt).contiguous(
+        memory_format=torch.channels_last).requires_grad_(True)
+    w = (torch.randn(cout, cin, k, k, device='cuda') / (cin * k * k) ** 0.5 +
+         torch.arange(cout, device='cuda').view(-1, 1, 1, 1) * 1e-2).to(dt).requires_grad_(True)
+    b = (torch.randn(cout, device='cuda') * 0.1).requires_grad_(True) if bias else None
+    with torch.autocast('cuda', dtype=torch.bfloat16, enabled=amp):
+        assert C.tapsplit_eligible(x, w, (1, 1), (p, p), (d, d), 1)
+        y = C.conv2d(x, w, b, 1, p, d)
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().float().requires_grad_(True)
+    br = b.detach().clone().float().requires_grad_(True) if bias else None
+    yr = F.conv2d(xr, wr, br, 1, p, d)
+    assert y.shape == yr.shape and y.dtype == torch.bfloat16
+    err = (y.float() - yr).abs().max().item()
+    assert err <= 2e-2 * max(1.0, yr.abs().max().item()), err
+    go = torch.randn_like(yr)
+    y.backward(go.to(y.dtype))
+    yr.backward(go)
+    pairs = [(x.grad, xr.grad, 'dx'), (w.grad, wr.grad, 'dw')]
+    if bias:
+        pairs.append((b.grad, br.grad, 'db'))
+    for got, ref, name in pairs:
+        assert got.shape == ref.shape, name
+        assert got.dtype == (torch.float32 if name == 'db' else dt), name
+        e = (got.float() - ref).abs().max().item()
+        assert e <= 2e-2 * max(1.0, ref.abs().max().item()), (name, e)
