@@ -31,10 +31,12 @@
 #include <utility>
 #include <vector>
 
+#ifndef IAMD_LMDB_NO_PYTHON
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
 namespace py = pybind11;
+#endif
 
 namespace iamd {
 namespace lmdb {
@@ -110,6 +112,8 @@ class Reader {
     ::madvise(const_cast<char*>(base_), size_, MADV_RANDOM);
     const MetaRec* m0 = meta_at(0, 0);
     psize_ = m0->dbs[0].pad ? m0->dbs[0].pad : 4096;
+    if (psize_ < 512 || psize_ > (1u << 16) || (psize_ & (psize_ - 1)))
+      throw std::runtime_error("lmdb: bad page size in " + path);
     const MetaRec* m1 = meta_at(1, psize_);
     const MetaRec* m = m0;
     if (m1 && m1->magic == kMagic && (m0->magic != kMagic || m1->txnid > m0->txnid)) m = m1;
@@ -138,6 +142,7 @@ class Reader {
       const PageHdr* h = reinterpret_cast<const PageHdr*>(p);
       const int n = num_keys(h);
       if (h->flags & P_BRANCH) {
+        if (n < 1) throw std::runtime_error("lmdb: empty branch page");
         // last node whose key <= search key (node 0 = -inf)
         int lo = 1, hi = n - 1, idx = 0;
         while (lo <= hi) {
@@ -184,15 +189,28 @@ class Reader {
     return reinterpret_cast<const MetaRec*>(base_ + off);
   }
   const char* page(uint64_t pg) const {
-    size_t off = (size_t)pg * psize_;
-    if (off + psize_ > size_) throw std::runtime_error("lmdb: page out of range");
-    return base_ + off;
+    if (pg >= size_ / psize_) throw std::runtime_error("lmdb: page out of range");
+    return base_ + (size_t)pg * psize_;
   }
-  static int num_keys(const PageHdr* h) { return (h->lower - kPageHdr) >> 1; }
-  static const NodeHdr* node(const char* p, int i) {
+  // Every field read from the file is bounds-checked against the page before it is used:
+  // a truncated or corrupted data.mdb raises instead of reading outside the mapping
+  // (tests/native/lmdb_sanitize.cpp fuzzes this under ASan + UBSan).
+  int num_keys(const PageHdr* h) const {
+    if (h->lower < kPageHdr || h->lower > psize_ || (h->lower - kPageHdr) % 2)
+      throw std::runtime_error("lmdb: corrupt page header");
+    return (h->lower - kPageHdr) >> 1;
+  }
+  const NodeHdr* node(const char* p, int i) const {
     uint16_t off;
     std::memcpy(&off, p + kPageHdr + 2 * i, 2);
-    return reinterpret_cast<const NodeHdr*>(p + off);
+    // LMDB keeps nodes 2-byte aligned; an odd offset is corruption (and would make every
+    // NodeHdr field access misaligned)
+    if (off < kPageHdr || (off & 1) || (size_t)off + kNodeHdr > psize_)
+      throw std::runtime_error("lmdb: corrupt node offset");
+    const NodeHdr* nd = reinterpret_cast<const NodeHdr*>(p + off);
+    if ((size_t)off + kNodeHdr + nd->ksize > psize_)
+      throw std::runtime_error("lmdb: corrupt key size");
+    return nd;
   }
   static const char* node_key(const NodeHdr* nd) {
     return reinterpret_cast<const char*>(nd) + kNodeHdr;
@@ -202,14 +220,17 @@ class Reader {
     const char* d = node_key(nd) + nd->ksize;
     if (nd->flags & (F_SUBDATA | F_DUPDATA))
       throw std::runtime_error("lmdb: sub-databases are not supported");
+    // node() checked the header and key against the page; the value must fit as well
+    const size_t in_page = (size_t)(d - base_) % psize_;
     if (nd->flags & F_BIGDATA) {
+      if (in_page + 8 > psize_) throw std::runtime_error("lmdb: corrupt overflow link");
       uint64_t opg;
       std::memcpy(&opg, d, 8);
-      const char* op = page(opg);
-      if ((size_t)opg * psize_ + kPageHdr + dsize > size_)
+      if (opg >= size_ / psize_ || dsize > size_ - (size_t)opg * psize_ - kPageHdr)
         throw std::runtime_error("lmdb: overflow out of range");
-      return {op + kPageHdr, dsize};
+      return {page(opg) + kPageHdr, dsize};
     }
+    if (in_page + dsize > psize_) throw std::runtime_error("lmdb: corrupt value size");
     return {d, dsize};
   }
   void walk(uint64_t pg, std::vector<std::string>& out, int depth) const {
@@ -223,7 +244,7 @@ class Reader {
         walk(uint64_t(nd->lo) | (uint64_t(nd->hi) << 16) | (uint64_t(nd->flags) << 32), out,
              depth + 1);
       } else {
-        out.emplace_back(node_key(nd), nd->ksize);
+        out.emplace_back(node_key(nd), static_cast<size_t>(nd->ksize));
       }
     }
   }
@@ -433,6 +454,7 @@ void write_lmdb(const std::string& root, std::vector<std::pair<std::string, std:
 
 }  // namespace lmdb
 
+#ifndef IAMD_LMDB_NO_PYTHON
 void register_lmdb(py::module_& m) {
   using lmdb::Reader;
   py::class_<Reader, std::shared_ptr<Reader>>(m, "LmdbReader")
@@ -473,5 +495,7 @@ void register_lmdb(py::module_& m) {
         py::arg("root"), py::arg("items"), py::arg("page_size") = 4096,
         "write a fresh LMDB environment (<root>/data.mdb) from (key, value) bytes pairs");
 }
+
+#endif  // IAMD_LMDB_NO_PYTHON
 
 }  // namespace iamd
