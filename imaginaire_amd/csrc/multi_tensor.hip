@@ -133,9 +133,17 @@ uint64_t mix(uint64_t h, uint64_t v) {
 Table& get_table(const std::vector<std::vector<at::Tensor>>& lists, const at::Device& dev) {
   const size_t T = lists[0].size();
   uint64_t h = 1469598103934665603ULL ^ (uint64_t)lists.size();
+  // the key covers everything an entry records: pointers, sizes and the memory layout (a
+  // freed tensor's address reused by one of another shape must not hit a stale entry)
   for (size_t i = 0; i < T; ++i) {
-    for (auto& l : lists) h = mix(h, reinterpret_cast<uint64_t>(l[i].data_ptr()));
-    h = mix(h, (uint64_t)lists[0][i].numel());
+    for (auto& l : lists) {
+      h = mix(h, reinterpret_cast<uint64_t>(l[i].data_ptr()));
+      h = mix(h, (uint64_t)l[i].numel());
+    }
+    const at::Tensor& t0 = lists[0][i];
+    h = mix(h, t0.dim() > 0 ? (uint64_t)t0.size(0) : 0);
+    h = mix(h, t0.dim() == 4 ? (uint64_t)(t0.size(1) * 31 + t0.size(2) * 7 + t0.size(3)) : 1);
+    h = mix(h, (uint64_t)t0.is_contiguous());
   }
   std::lock_guard<std::mutex> lk(g_mu);
   auto it = g_cache.find(h);
@@ -263,11 +271,11 @@ adam_kernel(const TensorEntry* __restrict__ ents, const int* __restrict__ blocks
   }
 }
 
-// σ_i = Σ_{r,c} u[r] W[r,c] v[c]  (W viewed as [rows, numel/rows]); atomic per chunk.
+// σ_i = Σ_{r,c} u[r] W[r,c] v[c]  (W viewed as [rows, numel/rows]); one partial per chunk.
 // entry: p0 = W (fp32), p1 = u, p2 = v; rows carried in the sigma-rows array.
 __global__ void __launch_bounds__(kThreads)
 sn_sigma_kernel(const TensorEntry* __restrict__ ents, const int* __restrict__ blocks,
-                float* __restrict__ sigma) {
+                float* __restrict__ part) {
   __shared__ float sh[kThreads / 64];
   const int b = blockIdx.x;
   const int t = blocks[2 * b], chunk = blocks[2 * b + 1];
@@ -296,7 +304,28 @@ sn_sigma_kernel(const TensorEntry* __restrict__ ents, const int* __restrict__ bl
   if (threadIdx.x == 0) {
     float s = 0.f;
     for (int k = 0; k < kThreads / 64; ++k) s += sh[k];
-    atomicAdd(sigma + t, s);
+    part[b] = s;  // per-workgroup partial; reduce_block_partials sums them in a fixed order
+  }
+}
+
+// out[t] = Σ_{b : blocks[b].tensor == t} part[b], one workgroup per tensor (T = 1 with
+// all_blocks: every partial). Fixed per-thread strides + a fixed tree: bitwise reproducible,
+// unlike one float atomic per workgroup (whose arrival order varies run to run).
+__global__ void __launch_bounds__(kThreads)
+reduce_block_partials(const float* __restrict__ part, const int* __restrict__ blocks, int nblocks,
+                      bool all_blocks, float* __restrict__ out) {
+  __shared__ float sh[kThreads / 64];
+  const int t = blockIdx.x;
+  float acc = 0.f;
+  for (int b = threadIdx.x; b < nblocks; b += kThreads)
+    if (all_blocks || blocks[2 * b] == t) acc += part[b];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int k = 0; k < kThreads / 64; ++k) s += sh[k];
+    out[t] = s;
   }
 }
 
@@ -356,7 +385,7 @@ scale_kernel(const TensorEntry* __restrict__ ents, const int* __restrict__ block
 template <typename T>
 __global__ void __launch_bounds__(kThreads)
 sqnorm_kernel(const TensorEntry* __restrict__ ents, const int* __restrict__ blocks,
-              float* __restrict__ out) {
+              float* __restrict__ part) {
   __shared__ float sh[kThreads / 64];
   const int b = blockIdx.x;
   const int t = blocks[2 * b], chunk = blocks[2 * b + 1];
@@ -375,7 +404,7 @@ sqnorm_kernel(const TensorEntry* __restrict__ ents, const int* __restrict__ bloc
   if (threadIdx.x == 0) {
     float s = 0.f;
     for (int k = 0; k < kThreads / 64; ++k) s += sh[k];
-    atomicAdd(out, s);
+    part[b] = s;
   }
 }
 
@@ -461,12 +490,16 @@ at::Tensor mt_sn_sigma(const std::vector<at::Tensor>& weights, const std::vector
     }
   }
   Table& tb = get_table({weights, us, vs, vms}, weights[0].device());
-  auto sigma = at::zeros({(int64_t)weights.size()}, weights[0].options());
+  auto sigma = at::empty({(int64_t)weights.size()}, weights[0].options());
+  auto part = at::empty({(int64_t)tb.nblocks}, weights[0].options());
   hipLaunchKernelGGL(sn_vperm, dim3((unsigned)weights.size()), dim3(kThreads), 0, stream(),
                      reinterpret_cast<const TensorEntry*>(tb.entries.data_ptr()));
   hipLaunchKernelGGL(sn_sigma_kernel, dim3(tb.nblocks), dim3(kThreads), 0, stream(),
                      reinterpret_cast<const TensorEntry*>(tb.entries.data_ptr()),
-                     tb.blocks.data_ptr<int>(), sigma.data_ptr<float>());
+                     tb.blocks.data_ptr<int>(), part.data_ptr<float>());
+  hipLaunchKernelGGL(reduce_block_partials, dim3((unsigned)weights.size()), dim3(kThreads), 0,
+                     stream(), part.data_ptr<float>(), tb.blocks.data_ptr<int>(), tb.nblocks,
+                     false, sigma.data_ptr<float>());
   IAMD_LAUNCH_CHECK();
   return sigma;
 }
@@ -518,12 +551,16 @@ at::Tensor mt_sqnorm(const std::vector<at::Tensor>& xs) {
   const auto dt = xs[0].scalar_type();
   check_same_dtype(xs, dt, "mt_sqnorm");
   Table& tb = get_table({xs}, xs[0].device());
-  auto out = at::zeros({1}, xs[0].options().dtype(at::kFloat));
+  auto out = at::empty({1}, xs[0].options().dtype(at::kFloat));
+  auto part = at::empty({(int64_t)tb.nblocks}, xs[0].options().dtype(at::kFloat));
   IAMD_DISPATCH_FLOAT_TYPES(dt, "mt_sqnorm", [&] {
     hipLaunchKernelGGL((sqnorm_kernel<scalar_t>), dim3(tb.nblocks), dim3(kThreads), 0, stream(),
                        reinterpret_cast<const TensorEntry*>(tb.entries.data_ptr()),
-                       tb.blocks.data_ptr<int>(), out.data_ptr<float>());
+                       tb.blocks.data_ptr<int>(), part.data_ptr<float>());
   });
+  hipLaunchKernelGGL(reduce_block_partials, dim3(1), dim3(kThreads), 0, stream(),
+                     part.data_ptr<float>(), tb.blocks.data_ptr<int>(), tb.nblocks, true,
+                     out.data_ptr<float>());
   IAMD_LAUNCH_CHECK();
   return out;
 }

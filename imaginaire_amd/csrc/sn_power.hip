@@ -6,7 +6,9 @@
 // autocast the GEMVs go through bf16 hipBLASLt with a host-side heuristic
 // query each call. Here ONE set of 4 launches covers all L layers, in fp32:
 //
-//   K1 colsum : t_l  = W_l^T u_l                 (column-parallel, coalesced)
+//   K1 colsum : t_l  = W_l^T u_l                 (column-parallel, coalesced; one fp32 partial
+//               slab per 64-row split, summed in split order by K1b tsum — no float
+//               atomics, so the iteration is bitwise reproducible run to run)
 //   K2 tnorm  : |t_l|^2                           (one block per layer)
 //   K3 rows   : s_l  = W_l (t_l / max(|t_l|,eps)) (one wave per row)
 //   K4 final  : u_l <- s_l / max(|s_l|,eps), v_l <- t_l / max(|t_l|,eps),
@@ -35,6 +37,8 @@ struct SnEntry {
   float* v;
   float* t;  // workspace [w]
   float* s;  // workspace [h]
+  float* tp; // workspace [nsplit][w]: K1 partials per row split
+  int64_t nsplit;
   int64_t h, w;
   int64_t cl_cin, cl_khw;  // channels-last mapping (0 = none)
 };
@@ -75,7 +79,19 @@ __global__ void __launch_bounds__(kT) sn_colsum(const SnEntry* __restrict__ ents
   const int64_t r1 = min(e.h, r0 + kRowsPerSplit);
   float acc = 0.f;
   for (int64_t r = r0; r < r1; ++r) acc = fmaf(e.W[r * e.w + c], e.u[r], acc);
-  atomicAdd(e.t + c, acc);  // memory order
+  e.tp[bm[2] * e.w + c] = acc;  // memory order, this row split's slab
+}
+
+// blocks: {layer, col_tile}: t[c] = sum over row splits of the K1 slabs, in split order
+__global__ void __launch_bounds__(kT) sn_tsum(const SnEntry* __restrict__ ents,
+                                               const int* __restrict__ blocks) {
+  const int* bm = blocks + 2 * blockIdx.x;
+  const SnEntry e = ents[bm[0]];
+  const int64_t c = (int64_t)bm[1] * kColTile + threadIdx.x;
+  if (c >= e.w) return;
+  float acc = 0.f;
+  for (int64_t k = 0; k < e.nsplit; ++k) acc += e.tp[k * e.w + c];
+  e.t[c] = acc;
 }
 
 // one block per layer: sums of squares of t -> scal[l*4 + 0]
@@ -151,9 +167,10 @@ __global__ void __launch_bounds__(kT) sn_final(const SnEntry* __restrict__ ents,
 struct SnPlan {
   at::Tensor ents;         // device SnEntry[L]
   at::Tensor col_blocks;   // device int3
+  at::Tensor sum_blocks;   // device int2
   at::Tensor row_blocks;   // device int2
-  at::Tensor t_ws, s_ws;   // fp32 workspaces (flat)
-  int n_col_blocks, n_row_blocks, L;
+  at::Tensor t_ws, s_ws, tp_ws;   // fp32 workspaces (flat)
+  int n_col_blocks, n_sum_blocks, n_row_blocks, L;
 };
 
 std::mutex g_sn_mu;
@@ -166,23 +183,26 @@ SnPlan& get_plan(const std::vector<at::Tensor>& W, const std::vector<at::Tensor>
     hsh ^= reinterpret_cast<uint64_t>(W[i].data_ptr()) + 0x9e3779b97f4a7c15ULL + (hsh << 6);
     hsh ^= reinterpret_cast<uint64_t>(U[i].data_ptr()) + (hsh >> 2);
     hsh ^= reinterpret_cast<uint64_t>(V[i].data_ptr()) * 31 + (uint64_t)W[i].numel();
+    hsh ^= (uint64_t)W[i].size(0) * 0x100000001b3ULL + (uint64_t)W[i].is_contiguous() + (hsh << 3);
   }
   std::lock_guard<std::mutex> lk(g_sn_mu);
   auto it = g_sn_cache.find(hsh);
   if (it != g_sn_cache.end()) return it->second;
   const int L = (int)W.size();
-  int64_t tot_w = 0, tot_h = 0;
+  int64_t tot_w = 0, tot_h = 0, tot_p = 0;
   for (int i = 0; i < L; ++i) {
     tot_h += W[i].size(0);
     tot_w += W[i].numel() / W[i].size(0);
+    tot_p += (W[i].size(0) + kRowsPerSplit - 1) / kRowsPerSplit * (W[i].numel() / W[i].size(0));
   }
   SnPlan p;
   auto fopt = W[0].options().dtype(at::kFloat);
   p.t_ws = at::zeros({tot_w}, fopt);
   p.s_ws = at::zeros({tot_h}, fopt);
+  p.tp_ws = at::empty({tot_p}, fopt);
   std::vector<SnEntry> ents(L);
-  std::vector<int32_t> cb, rb;
-  int64_t ow = 0, oh = 0;
+  std::vector<int32_t> cb, sb, rb;
+  int64_t ow = 0, oh = 0, op = 0;
   for (int i = 0; i < L; ++i) {
     const at::Tensor& w = W[i];
     IAMD_CHECK(w.scalar_type() == at::kFloat && w.is_non_overlapping_and_dense(),
@@ -202,16 +222,22 @@ SnPlan& get_plan(const std::vector<at::Tensor>& W, const std::vector<at::Tensor>
     e.cl_khw = cl ? w.size(2) * w.size(3) : 0;
     e.t = p.t_ws.data_ptr<float>() + ow;
     e.s = p.s_ws.data_ptr<float>() + oh;
-    ow += e.w;
-    oh += e.h;
     const int ntile = (int)((e.w + kColTile - 1) / kColTile);
     const int nsplit = (int)((e.h + kRowsPerSplit - 1) / kRowsPerSplit);
-    for (int a = 0; a < ntile; ++a)
+    e.tp = p.tp_ws.data_ptr<float>() + op;
+    e.nsplit = nsplit;
+    ow += e.w;
+    oh += e.h;
+    op += (int64_t)nsplit * e.w;
+    for (int a = 0; a < ntile; ++a) {
       for (int b = 0; b < nsplit; ++b) {
         cb.push_back(i);
         cb.push_back(a);
         cb.push_back(b);
       }
+      sb.push_back(i);
+      sb.push_back(a);
+    }
     for (int64_t r = 0; r < e.h; r += kRowsPerBlock) {
       rb.push_back(i);
       rb.push_back((int32_t)r);
@@ -221,6 +247,8 @@ SnPlan& get_plan(const std::vector<at::Tensor>& W, const std::vector<at::Tensor>
   auto stage = [&](const void* src, size_t bytes) { return stage_to_device(src, bytes, dev); };
   p.ents = stage(ents.data(), ents.size() * sizeof(SnEntry));
   p.col_blocks = stage(cb.data(), cb.size() * sizeof(int32_t)).view(at::kInt);
+  p.sum_blocks = stage(sb.data(), sb.size() * sizeof(int32_t)).view(at::kInt);
+  p.n_sum_blocks = (int)(sb.size() / 2);
   p.row_blocks = stage(rb.data(), rb.size() * sizeof(int32_t)).view(at::kInt);
   p.n_col_blocks = (int)(cb.size() / 3);
   p.n_row_blocks = (int)(rb.size() / 2);
@@ -243,9 +271,10 @@ at::Tensor mt_sn_power(const std::vector<at::Tensor>& weights, const std::vector
   const auto* ents = reinterpret_cast<const SnEntry*>(p.ents.data_ptr());
   hipStream_t st = stream();
   if (update) {
-    IAMD_HIP_CHECK(hipMemsetAsync(p.t_ws.data_ptr(), 0, p.t_ws.numel() * sizeof(float), st));
     hipLaunchKernelGGL(sn_colsum, dim3(p.n_col_blocks), dim3(kT), 0, st, ents,
                        p.col_blocks.data_ptr<int>());
+    hipLaunchKernelGGL(sn_tsum, dim3(p.n_sum_blocks), dim3(kT), 0, st, ents,
+                       p.sum_blocks.data_ptr<int>());
     hipLaunchKernelGGL(sn_tnorm, dim3(p.L), dim3(kT), 0, st, ents, scal.data_ptr<float>());
   }
   hipLaunchKernelGGL(sn_rows, dim3(p.n_row_blocks), dim3(64 * kRowsPerBlock), 0, st, ents,

@@ -219,7 +219,9 @@ def mfma_eligible(x, w, stride, padding, dilation, groups):
             x.shape[0] * op * ho * wo * 2 >= (1 << 30):
         return False
     blocks = -(-x.shape[0] * ho * wo // 128) * max(1, op // (128 if op % 128 == 0 else 64))
-    return blocks >= _MFMA_MIN_BLOCKS
+    # deterministic mode: tiny grids run k10 too (its split-K sums slabs in a fixed order);
+    # MIOpen's immediate-mode solvers for them may split K with atomics
+    return blocks >= _MFMA_MIN_BLOCKS or torch.are_deterministic_algorithms_enabled()
 
 
 def _flip_t(w):

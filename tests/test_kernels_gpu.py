@@ -805,3 +805,17 @@ def test_conv_tapsplit_fwd_bwd(case):
         assert got.dtype == (torch.float32 if name == 'db' else dt), name
         e = (got.float() - ref).abs().max().item()
         assert e <= 2e-2 * max(1.0, ref.abs().max().item()), (name, e)
+
+
+@pytest.mark.gpu
+def test_multi_tensor_sqnorm_fixed_order():
+    """mt_sqnorm: one partial per workgroup summed in a fixed tree (no float atomics): matches
+    the fp64 sum of squares and is bitwise identical across calls."""
+    from imaginaire_amd.ops import _ext
+    torch.manual_seed(0)
+    xs = [torch.randn(n, device='cuda') for n in (3, 70000, 1 << 20, 513)]
+    a = _ext.ext().mt_sqnorm(xs)
+    b = _ext.ext().mt_sqnorm(xs)
+    ref = sum(float((x.double() ** 2).sum()) for x in xs)
+    assert torch.equal(a, b)
+    assert abs(float(a) - ref) <= 1e-4 * ref
