@@ -215,6 +215,30 @@ pad_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int B, int C, int H
   }
 }
 
+// Phase scatter of the strided-conv data gradient: dx[b, s*q + ry, s*q2 + rx, c] =
+// src[b, i0 + q, j0 + q2, c] for q < Qy, q2 < Qx (both NHWC, C % 8 == 0). The s*s phase
+// convolutions (k10) each fill one parity sub-grid of dx; 16-byte loads and stores along C.
+__global__ void __launch_bounds__(kT)
+phase_scatter_kernel(const __hip_bfloat16* __restrict__ src, __hip_bfloat16* __restrict__ dst,
+                     int B, int C, int Hs, int Ws, int H, int W, int s, int ry, int rx, int i0,
+                     int j0, int Qy, int Qx) {
+  const int cv = C / 8;
+  const int64_t total = (int64_t)B * Qy * Qx * cv;
+  for (int64_t t = (int64_t)blockIdx.x * kT + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * kT) {
+    const int c8 = (int)(t % cv);
+    int64_t p = t / cv;
+    const int q2 = (int)(p % Qx);
+    p /= Qx;
+    const int q = (int)(p % Qy);
+    const int b = (int)(p / Qy);
+    const uint4 v = *reinterpret_cast<const uint4*>(
+        src + (((int64_t)b * Hs + i0 + q) * Ws + j0 + q2) * C + c8 * 8);
+    *reinterpret_cast<uint4*>(dst + (((int64_t)b * H + s * q + ry) * W + s * q2 + rx) * C +
+                              c8 * 8) = v;
+  }
+}
+
 int pad_grid(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + kT - 1) / kT, 65536)); }
 
 }  // namespace
@@ -335,6 +359,30 @@ at::Tensor wgrad_finalize(const at::Tensor& part, int64_t S, int64_t Cop, int64_
   else IAMD_CHECK(false, "wgrad_finalize: bf16 or fp32 output expected");
   IAMD_LAUNCH_CHECK();
   return out;
+}
+
+// src [B, C, Hs, Ws] -> the (ry, rx) parity sub-grid of dst [B, C, H, W] (both channels-last bf16)
+void conv_phase_scatter(const at::Tensor& src, at::Tensor& dst, int64_t s, int64_t ry, int64_t rx,
+                        int64_t i0, int64_t j0, int64_t Qy, int64_t Qx) {
+  IAMD_CHECK(src.is_cuda() && dst.is_cuda() && src.scalar_type() == at::kBFloat16 &&
+                 dst.scalar_type() == at::kBFloat16 && src.dim() == 4 && dst.dim() == 4 &&
+                 src.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                 dst.is_contiguous(at::MemoryFormat::ChannelsLast),
+             "conv_phase_scatter: packed channels-last bf16 tensors expected");
+  const int B = (int)src.size(0), C = (int)src.size(1), Hs = (int)src.size(2), Ws = (int)src.size(3);
+  const int H = (int)dst.size(2), W = (int)dst.size(3);
+  IAMD_CHECK(dst.size(0) == B && dst.size(1) == C && C % 8 == 0, "conv_phase_scatter: shapes");
+  IAMD_CHECK(Qy >= 0 && Qx >= 0 && i0 >= 0 && j0 >= 0 && i0 + Qy <= Hs && j0 + Qx <= Ws &&
+                 ry >= 0 && rx >= 0 && ry < s && rx < s && s * (Qy - 1) + ry < H + (Qy == 0) * s &&
+                 s * (Qx - 1) + rx < W + (Qx == 0) * s,
+             "conv_phase_scatter: phase window out of range");
+  const int64_t total = (int64_t)B * Qy * Qx * (C / 8);
+  if (total == 0) return;
+  hipLaunchKernelGGL(phase_scatter_kernel, dim3(pad_grid(total)), dim3(kT), 0, stream(),
+                     reinterpret_cast<const __hip_bfloat16*>(src.data_ptr()),
+                     reinterpret_cast<__hip_bfloat16*>(dst.data_ptr()), B, C, Hs, Ws, H, W, (int)s,
+                     (int)ry, (int)rx, (int)i0, (int)j0, (int)Qy, (int)Qx);
+  IAMD_LAUNCH_CHECK();
 }
 
 }  // namespace iamd

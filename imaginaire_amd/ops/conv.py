@@ -241,6 +241,47 @@ def _pad_rows(t, n):
     return out.contiguous(memory_format=_CL) if out.dim() == 4 else out
 
 
+# stride-s data gradients as s*s phase convolutions on k10 (0: MIOpen backward-data)
+_STRIDED_DGRAD = os.environ.get('IMAGINAIRE_AMD_STRIDED_DGRAD', '1') == '1'
+_STRIDED_DGRAD_MIN_PIX = int(os.environ.get('IMAGINAIRE_AMD_STRIDED_DGRAD_MIN_PIX', 131072))
+
+
+def _strided_dgrad(dy, wb, H, W, s, padding):
+    """Data gradient of a stride-``s`` conv (weight ``wb`` [Cout, Cin, KH, KW], channels-last
+    bf16) as s*s stride-1 phase convolutions on k10. Input row i = s*q + r receives
+    dy[q + c0 - j] * w[kh0 + s*j] for kh0 = (r + p) mod s, c0 = (r + p - kh0) / s: a J-tap
+    correlation of dy with the flipped phase sub-kernel (``conv_weight_flip_t(w, s, kh0, kw0)``),
+    whose output rows [m0, m0 + Q) are scattered into the parity sub-grid of dx
+    (``conv_phase_scatter``). Same FLOPs as the dense dgrad, no zero-insertion."""
+    X = _ext.ext()
+    cout, cin, kh, kw = wb.shape
+    ho, wo = dy.shape[2], dy.shape[3]
+    ph, pw = padding
+    dx = None
+    phases = []
+    for ry in range(s):
+        for rx in range(s):
+            ky0, kx0 = (ry + ph) % s, (rx + pw) % s
+            jy, jx = -(-(kh - ky0) // s), -(-(kw - kx0) // s)
+            qy, qx = (H - ry + s - 1) // s, (W - rx + s - 1) // s
+            phases.append((ry, rx, ky0, kx0, jy, jx, qy, qx))
+    zero_fill = any(p[4] <= 0 or p[5] <= 0 for p in phases)
+    dx = torch.empty((dy.shape[0], cin, H, W), dtype=torch.bfloat16, device=dy.device,
+                     memory_format=_CL)
+    if zero_fill:  # some parity sub-grid receives no filter taps
+        dx.zero_()
+    for ry, rx, ky0, kx0, jy, jx, qy, qx in phases:
+        if jy <= 0 or jx <= 0 or qy <= 0 or qx <= 0:
+            continue
+        cy, cx = (ry + ph - ky0) // s, (rx + pw - kx0) // s
+        py = max(0, jy - 1 - cy, qy + cy - ho)
+        px = max(0, jx - 1 - cx, qx + cx - wo)
+        wt = X.conv_weight_flip_t(wb, s, ky0, kx0, 1)
+        out = X.conv2d_mfma(dy, wt, None, 1, 1, py, px, 1, 1, 1.0, 1)
+        X.conv_phase_scatter(out, dx, s, ry, rx, cy - (jy - 1) + py, cx - (jx - 1) + px, qy, qx)
+    return dx
+
+
 class _MfmaConv2d(torch.autograd.Function):
     """k10 forward / stride-1 dgrad, k11 wgrad, k2 activation + bias backward. Channel
     counts are zero-padded to multiples of 64 (input) / 64 (output) around the kernels."""
@@ -294,6 +335,13 @@ class _MfmaConv2d(torch.autograd.Function):
                 with _Logged('dgrad', 'k10', fl, _gemm_desc(dy, wt, (1, 1), pt)):
                     dx = _ext.ext().conv2d_mfma(dy, wt, None, 1, 1, pt[0], pt[1],
                                                 dilation[0], dilation[1], 1.0)
+            elif _STRIDED_DGRAD and stride[0] == stride[1] and 2 <= stride[0] <= 4 and \
+                    dilation == (1, 1) and dblocks >= _MFMA_MIN_DGRAD_BLOCKS * stride[0] ** 2 and \
+                    xb.shape[0] * xb.shape[2] * xb.shape[3] >= _STRIDED_DGRAD_MIN_PIX:
+                # large maps only: 1.3-1.6x MIOpen on the full-resolution PatchGAN layers, on par
+                # or slower below ~128K dx pixels (profiles/strided_dgrad_probe_mi355x.txt)
+                with _Logged('dgrad', 'k10s', fl, _gemm_desc(dy, wb, stride, padding)):
+                    dx = _strided_dgrad(dy, wb, xb.shape[2], xb.shape[3], stride[0], padding)
             else:
                 with _Logged('dgrad', 'miopen', fl, _gemm_desc(dy, wb, stride, padding)):
                     dx = torch.ops.aten.convolution_backward(

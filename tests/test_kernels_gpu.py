@@ -319,7 +319,7 @@ _CONV_CASES = [
     (2, 3, 64, 16, 24, 3, 1, 1, 1),         # RGB in: Cin padded 3 -> 64
     (2, 64, 3, 16, 24, 3, 1, 1, 1),         # RGB out: Cout padded 3 -> 64
     (1, 128, 100, 12, 12, 3, 1, 1, 1),      # Cout padded 100 -> 128
-    # more stride-2 shapes (forward on k10; data gradient on MIOpen)
+    # more stride-2 shapes (forward on k10; data gradient as k10 phase convolutions)
     (2, 64, 128, 15, 17, 3, 2, 1, 1),       # 3x3 s2, odd sizes: 1x1 / 1x2 / 2x1 / 2x2 phases
     (1, 128, 64, 9, 14, 1, 2, 0, 1),        # 1x1 s2: three phases receive no taps (zeros)
     (1, 64, 128, 11, 13, 5, 2, 2, 1),       # 5x5 s2
@@ -335,6 +335,7 @@ def test_conv2d_mfma_fwd_bwd(case, slope, bias):
     os.environ['IMAGINAIRE_AMD_MFMA_MIN_BLOCKS'] = '0'
     C._MFMA_MIN_BLOCKS = 0
     C._MFMA_MIN_DGRAD_BLOCKS = 0
+    C._STRIDED_DGRAD_MIN_PIX = 0  # strided data gradients on the k10 phase path
     C._MFMA_WGRAD = 'auto' if slope == 0.0 else '1'
     B, cin, cout, H, W, k, s, p, d = case
     torch.manual_seed(1)
