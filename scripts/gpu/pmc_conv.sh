@@ -7,7 +7,7 @@ cd /tmp && export TMPDIR=/tmp
 SHAPE="4 128 1024 128 256 5"
 P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES"
 P2="SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_INSTS_SALU SQ_INSTS_VMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA SQ_INST_CYCLES_VMEM SQ_WAIT_INST_ANY"
-for mode in fwd wgrad; do
+for mode in ${MODES:-fwd dgrad wgrad}; do
   for pass in 1 2; do
     eval "CTRS=\$P$pass"
     rm -rf /tmp/pmc_$mode$pass

@@ -1,6 +1,9 @@
 """Run one k10 / k11 conv shape N times (target for rocprofv3 --pmc counter passes).
 
-    python scripts/probe/conv_kernel_driver.py {fwd|wgrad} B Cin Cout H W k [iters]
+    python scripts/probe/conv_kernel_driver.py {fwd|wgrad|dgrad} B Cin Cout H W k [iters]
+
+dgrad runs the stride-1 data gradient as k10 sees it: dy [B, Cout, H, W] convolved with the
+flipped, transposed weight [Cin, Cout, k, k] (the narrow-N, wide-K GEMM of the SPADE convs).
 """
 import os
 import sys
@@ -20,9 +23,12 @@ w = (torch.randn(cout, cin, k, k, device='cuda', dtype=torch.bfloat16) * 0.02).c
     memory_format=CL)
 g = torch.randn(B, cout, H, W, device='cuda', dtype=torch.bfloat16).contiguous(memory_format=CL)
 ext = _ext.ext()
+wt = ext.conv_weight_flip_t(w, 1, 0, 0, 1) if mode == 'dgrad' else None
 for _ in range(iters):
     if mode == 'fwd':
         ext.conv2d_mfma(x, w, None, 1, 1, pad, pad, 1, 1, 1.0)
+    elif mode == 'dgrad':
+        ext.conv2d_mfma(g, wt, None, 1, 1, k - 1 - pad, k - 1 - pad, 1, 1, 1.0)
     else:
         ext.conv2d_wgrad_mfma(g, x, k, k, 1, 1, pad, pad, 1, 1)
 torch.cuda.synchronize()
