@@ -50,6 +50,14 @@ at::Tensor mt_l1_loss(const std::vector<at::Tensor>& a, const std::vector<at::Te
 std::vector<at::Tensor> mt_l1_loss_backward(const std::vector<at::Tensor>& a,
                                             const std::vector<at::Tensor>& b,
                                             const std::vector<double>& w, const at::Tensor& gout);
+at::Tensor mt_gan_loss(const std::vector<at::Tensor>& xs, const std::vector<int64_t>& kinds,
+                       const std::vector<double>& pa, const std::vector<double>& pb,
+                       const std::vector<double>& w);
+std::vector<at::Tensor> mt_gan_loss_backward(const std::vector<at::Tensor>& xs,
+                                             const std::vector<int64_t>& kinds,
+                                             const std::vector<double>& pa,
+                                             const std::vector<double>& pb,
+                                             const std::vector<double>& w, const at::Tensor& gout);
 at::Tensor resize_bilinear_fwd(const at::Tensor& x, int64_t Ho, int64_t Wo, double scale_h,
                                double scale_w, bool align_corners,
                                const c10::optional<at::Tensor>& add);
@@ -161,6 +169,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mt_sqnorm", &iamd::mt_sqnorm, "multi-tensor squared L2 norm");
   m.def("mt_l1_loss", &iamd::mt_l1_loss, "multi-tensor weighted L1 loss (k13)");
   m.def("mt_l1_loss_backward", &iamd::mt_l1_loss_backward, "k13 backward");
+  m.def("mt_gan_loss", &iamd::mt_gan_loss, "multi-tensor GAN loss over D outputs (k13b)");
+  m.def("mt_gan_loss_backward", &iamd::mt_gan_loss_backward, "k13b backward");
   m.def("resize_bilinear_fwd", &iamd::resize_bilinear_fwd,
         "NHWC bilinear resize (+ residual) (k12)");
   m.def("resize_bilinear_bwd", &iamd::resize_bilinear_bwd, "k12 backward (gather)");

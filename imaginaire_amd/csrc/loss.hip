@@ -12,6 +12,15 @@
 //   * backward: ONE launch writes every dL/da_t = w_t / n_t * sign(a_t - b_t) * dL in the
 //     feature dtype.
 // Up to kMaxT pairs per launch travel in the kernel arguments (no device table).
+//
+// k13b: multi-tensor GAN loss  L = sum_t w_t * mean(phi_t(x_t))  over every discriminator
+// output of a pass (reference losses/gan.py:12-132: per-output min/mean/neg kernels, averaged
+// over the multi-scale list), one forward + one fixed-order reduce launch and one backward
+// launch for all outputs:
+//   kind 0  phi = relu(a + b x)               hinge, D update (a = 1, b = -1 real / +1 fake)
+//   kind 1  phi = b x                         hinge G update / wasserstein (b = -1 / +1)
+//   kind 2  phi = bce_with_logits(x, y = a)   non_saturated
+//   kind 3  phi = 0.5 (x - a)^2               least_square
 #include "common.h"
 
 namespace iamd {
@@ -124,6 +133,127 @@ __global__ void __launch_bounds__(kThreads) l1_grad(const L1Args<T> p, const flo
 }
 
 template <typename T>
+struct GanArgs {
+  const T* x[kMaxT];
+  T* g[kMaxT];
+  int64_t n[kMaxT];
+  float scale[kMaxT];  // w_t / n_t
+  float pa[kMaxT], pb[kMaxT];
+  int kind[kMaxT];
+  int start[kMaxT + 1];
+  int nt;
+};
+
+__device__ __forceinline__ float gan_phi(int kind, float a, float b, float x) {
+  switch (kind) {
+    case 0: return fmaxf(a + b * x, 0.f);
+    case 1: return b * x;
+    case 2: return fmaxf(x, 0.f) - x * a + log1pf(expf(-fabsf(x)));
+    default: { const float d = x - a; return 0.5f * d * d; }
+  }
+}
+
+__device__ __forceinline__ float gan_dphi(int kind, float a, float b, float x) {
+  switch (kind) {
+    case 0: return (a + b * x) > 0.f ? b : 0.f;
+    case 1: return b;
+    case 2: return 1.f / (1.f + expf(-x)) - a;
+    default: return x - a;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ int find_gan_tensor(const GanArgs<T>& p, int bid) {
+  int t = 0;
+#pragma unroll
+  for (int k = 1; k < kMaxT; ++k)
+    if (k < p.nt && bid >= p.start[k]) t = k;
+  return t;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kThreads) gan_partials(const GanArgs<T> p, float* __restrict__ part) {
+  __shared__ float sh[kThreads / 64];
+  const int bid = blockIdx.x;
+  const int t = find_gan_tensor(p, bid);
+  const int64_t c0 = (int64_t)(bid - p.start[t]) * kChunk;
+  const int64_t c1 = min(p.n[t], c0 + kChunk);
+  const T* __restrict__ x = p.x[t];
+  const int kind = p.kind[t];
+  const float a = p.pa[t], b = p.pb[t];
+  float acc = 0.f;
+  for (int64_t j = c0 + threadIdx.x; j < c1; j += kThreads) acc += gan_phi(kind, a, b, to_f<T>(x[j]));
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < kThreads / 64; ++k) s += sh[k];
+    part[bid] = s * p.scale[t];
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kThreads) gan_grad(const GanArgs<T> p, const float* __restrict__ gout) {
+  const int bid = blockIdx.x;
+  const int t = find_gan_tensor(p, bid);
+  const int64_t c0 = (int64_t)(bid - p.start[t]) * kChunk;
+  const int64_t c1 = min(p.n[t], c0 + kChunk);
+  const T* __restrict__ x = p.x[t];
+  T* __restrict__ g = p.g[t];
+  const int kind = p.kind[t];
+  const float a = p.pa[t], b = p.pb[t], s = p.scale[t] * gout[0];
+  for (int64_t j = c0 + threadIdx.x; j < c1; j += kThreads)
+    g[j] = from_f<T>(s * gan_dphi(kind, a, b, to_f<T>(x[j])));
+}
+
+template <typename T>
+GanArgs<T> make_gan_args(const std::vector<at::Tensor>& xs, const std::vector<int64_t>& kinds,
+                         const std::vector<double>& pa, const std::vector<double>& pb,
+                         const std::vector<double>& w, int& nblocks) {
+  GanArgs<T> p;
+  p.nt = (int)xs.size();
+  int blocks = 0;
+  for (int t = 0; t < kMaxT; ++t) {
+    p.start[t] = blocks;
+    p.g[t] = nullptr;
+    if (t < p.nt) {
+      p.x[t] = reinterpret_cast<const T*>(xs[t].data_ptr());
+      p.n[t] = xs[t].numel();
+      p.scale[t] = (float)(w[t] / (double)std::max<int64_t>(1, xs[t].numel()));
+      p.kind[t] = (int)kinds[t];
+      p.pa[t] = (float)pa[t];
+      p.pb[t] = (float)pb[t];
+      blocks += (int)((p.n[t] + kChunk - 1) / kChunk);
+    } else {
+      p.x[t] = nullptr;
+      p.n[t] = 0;
+      p.scale[t] = p.pa[t] = p.pb[t] = 0.f;
+      p.kind[t] = 1;
+    }
+  }
+  p.start[kMaxT] = blocks;
+  nblocks = blocks;
+  return p;
+}
+
+void check_gan(const std::vector<at::Tensor>& xs, const std::vector<int64_t>& kinds,
+               const std::vector<double>& pa, const std::vector<double>& pb,
+               const std::vector<double>& w) {
+  IAMD_CHECK(!xs.empty() && (int)xs.size() <= kMaxT, "mt_gan_loss: 1..", kMaxT, " tensors");
+  IAMD_CHECK(kinds.size() == xs.size() && pa.size() == xs.size() && pb.size() == xs.size() &&
+                 w.size() == xs.size(), "mt_gan_loss: list sizes differ");
+  const auto dt = xs[0].scalar_type();
+  IAMD_CHECK(dt == at::kBFloat16 || dt == at::kFloat, "mt_gan_loss: bf16 or fp32 tensors");
+  for (size_t t = 0; t < xs.size(); ++t) {
+    IAMD_CHECK(xs[t].is_cuda() && xs[t].scalar_type() == dt && xs[t].is_non_overlapping_and_dense(),
+               "mt_gan_loss: dense CUDA tensors of one dtype expected");
+    IAMD_CHECK(kinds[t] >= 0 && kinds[t] <= 3, "mt_gan_loss: kind must be 0..3");
+  }
+}
+
+template <typename T>
 L1Args<T> make_args(const std::vector<at::Tensor>& a, const std::vector<at::Tensor>& b,
                     const std::vector<double>& w, int& nblocks) {
   L1Args<T> p;
@@ -206,6 +336,51 @@ std::vector<at::Tensor> mt_l1_loss_backward(const std::vector<at::Tensor>& a,
                          g32.data_ptr<float>());
   };
   if (a[0].scalar_type() == at::kBFloat16) launch(__hip_bfloat16()); else launch(float());
+  IAMD_LAUNCH_CHECK();
+  return grads;
+}
+
+at::Tensor mt_gan_loss(const std::vector<at::Tensor>& xs, const std::vector<int64_t>& kinds,
+                       const std::vector<double>& pa, const std::vector<double>& pb,
+                       const std::vector<double>& w) {
+  check_gan(xs, kinds, pa, pb, w);
+  auto out = at::empty({}, xs[0].options().dtype(at::kFloat));
+  int nb = 0;
+  auto launch = [&](auto tag) {
+    using T = decltype(tag);
+    auto p = make_gan_args<T>(xs, kinds, pa, pb, w, nb);
+    auto part = at::empty({std::max(nb, 1)}, xs[0].options().dtype(at::kFloat));
+    if (nb > 0)
+      hipLaunchKernelGGL((gan_partials<T>), dim3(nb), dim3(kThreads), 0, stream(), p,
+                         part.data_ptr<float>());
+    hipLaunchKernelGGL(sum_fixed, dim3(1), dim3(1024), 0, stream(), part.data_ptr<float>(), nb,
+                       out.data_ptr<float>());
+  };
+  if (xs[0].scalar_type() == at::kBFloat16) launch(__hip_bfloat16()); else launch(float());
+  IAMD_LAUNCH_CHECK();
+  return out;
+}
+
+std::vector<at::Tensor> mt_gan_loss_backward(const std::vector<at::Tensor>& xs,
+                                             const std::vector<int64_t>& kinds,
+                                             const std::vector<double>& pa,
+                                             const std::vector<double>& pb,
+                                             const std::vector<double>& w, const at::Tensor& gout) {
+  check_gan(xs, kinds, pa, pb, w);
+  IAMD_CHECK(gout.is_cuda() && gout.numel() == 1, "mt_gan_loss_backward: scalar grad expected");
+  auto g32 = gout.to(at::kFloat).contiguous();
+  std::vector<at::Tensor> grads;
+  for (auto& t : xs) grads.push_back(at::empty_like(t));
+  int nb = 0;
+  auto launch = [&](auto tag) {
+    using T = decltype(tag);
+    auto p = make_gan_args<T>(xs, kinds, pa, pb, w, nb);
+    for (size_t t = 0; t < xs.size(); ++t) p.g[t] = reinterpret_cast<T*>(grads[t].data_ptr());
+    if (nb > 0)
+      hipLaunchKernelGGL((gan_grad<T>), dim3(nb), dim3(kThreads), 0, stream(), p,
+                         g32.data_ptr<float>());
+  };
+  if (xs[0].scalar_type() == at::kBFloat16) launch(__hip_bfloat16()); else launch(float());
   IAMD_LAUNCH_CHECK();
   return grads;
 }

@@ -1,4 +1,4 @@
-"""Multi-tensor weighted L1 (k13, ``csrc/loss.hip``).
+"""Multi-tensor weighted L1 (k13) and GAN loss (k13b), ``csrc/loss.hip``.
 
 ``weighted_l1(as_, bs, weights) = sum_t weights[t] * mean(|as_[t] - bs[t]|)`` as one forward
 and one backward launch over every pair (fp32 accumulation, bf16 features read in place,
@@ -61,3 +61,55 @@ def weighted_l1(as_, bs, weights):
     if total is None:
         raise ValueError('weighted_l1: empty input')
     return total
+
+
+class _MultiGan(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, spec, *xs):
+        ctx.spec = spec
+        ctx.save_for_backward(*xs)
+        return _ext.ext().mt_gan_loss(list(xs), *spec)
+
+    @staticmethod
+    def backward(ctx, g):
+        xs = ctx.saved_tensors
+        need = ctx.needs_input_grad[1:]
+        grads = _ext.ext().mt_gan_loss_backward(list(xs), *ctx.spec, g) if any(need) else \
+            [None] * len(xs)
+        return (None,) + tuple(gr if n else None for gr, n in zip(grads, need))
+
+
+# phi kinds of csrc/loss.hip k13b
+GAN_RELU, GAN_LINEAR, GAN_BCE, GAN_LSQ = 0, 1, 2, 3
+
+
+def _gan_phi_ref(kind, a, b, x):
+    x = x.float()
+    if kind == GAN_RELU:
+        return F.relu(a + b * x).mean()
+    if kind == GAN_LINEAR:
+        return (b * x).mean()
+    if kind == GAN_BCE:
+        return F.binary_cross_entropy_with_logits(x, torch.full_like(x, a))
+    return 0.5 * F.mse_loss(x, torch.full_like(x, a))
+
+
+def gan_loss_multi(xs, kind, a=0.0, b=1.0, weight=1.0):
+    """``weight * sum_t mean(phi(xs[t]))`` for one phi over every discriminator output, as one
+    k13b forward + one backward launch (fp32 accumulation, fixed-order reduction). ``phi`` is
+    relu(a + b x) (hinge D), b x (hinge G / wasserstein), BCE-with-logits against target a
+    (non_saturated) or 0.5 (x - a)^2 (least squares). CPU / non-native inputs: same math in
+    PyTorch ops."""
+    xs = list(xs)
+    native = len(xs) <= _MAX_PAIRS and all(
+        x.is_cuda and _ext.use_native(x) and x.dtype in (torch.bfloat16, torch.float32) and
+        x.dtype == xs[0].dtype and _ext.is_dense(x) for x in xs)
+    if not native:
+        total = None
+        for x in xs:
+            v = _gan_phi_ref(kind, a, b, x)
+            total = v if total is None else total + v
+        return weight * total
+    n = len(xs)
+    spec = ([kind] * n, [float(a)] * n, [float(b)] * n, [float(weight)] * n)
+    return _MultiGan.apply(spec, *xs)

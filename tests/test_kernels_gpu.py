@@ -820,3 +820,31 @@ def test_multi_tensor_sqnorm_fixed_order():
     ref = sum(float((x.double() ** 2).sum()) for x in xs)
     assert torch.equal(a, b)
     assert abs(float(a) - ref) <= 1e-4 * ref
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize('mode,t_real,dis_update', [
+    ('hinge', True, True), ('hinge', False, True), ('hinge', True, False),
+    ('non_saturated', True, True), ('non_saturated', False, True),
+    ('least_square', False, True), ('wasserstein', False, True)])
+def test_multi_tensor_gan_loss(dtype, mode, t_real, dis_update):
+    """k13b: one launch over every D output (SPADE D: 3 FPSE + 2 PatchGAN scales, channels-last
+    NHWC with C = 1) == the per-output fp32 PyTorch losses averaged over the list."""
+    from imaginaire_amd.losses.gan import GANLoss
+    torch.manual_seed(2)
+    shapes = [(4, 1, 8, 16), (4, 1, 16, 32), (4, 1, 32, 64), (4, 1, 33, 65), (4, 1, 17, 33)]
+    xs = [torch.randn(s, device='cuda').to(dtype).contiguous(memory_format=torch.channels_last)
+          .requires_grad_(True) for s in shapes]
+    crit = GANLoss(mode)
+    got = crit(xs, t_real, dis_update)
+    refs = [x.detach().float().requires_grad_(True) for x in xs]
+    ref = sum(crit.loss(r, t_real, dis_update) for r in refs) / len(refs)
+    assert got.dtype == torch.float32
+    assert abs(float(got) - float(ref)) <= 1e-5 * max(1.0, abs(float(ref))), (float(got), float(ref))
+    got.backward()
+    ref.backward()
+    for x, r in zip(xs, refs):
+        assert x.grad.dtype == dtype and x.grad.shape == x.shape
+        torch.testing.assert_close(x.grad.float(), r.grad, atol=2e-3 * float(r.grad.abs().max()) + 1e-9,
+                                   rtol=1e-2)
