@@ -57,7 +57,9 @@ def has_spectral_norm(module):
 
 
 class WeightDemodulation(nn.Module):
-    """StyleGAN2 modulated / demodulated convolution (weight_norm.py:14-63)."""
+    """StyleGAN2 modulated / demodulated convolution (weight_norm.py:14-63). On the GPU the
+    per-sample modulated weights feed the batched per-sample k10 convolution (the hyper-conv
+    path of few-shot vid2vid, ``ops/conv.py: conv2d_per_sample``)."""
 
     def __init__(self, conv, cond_dims, eps=1e-8, adaptive_bias=False, demod=True):
         super().__init__()
@@ -78,14 +80,23 @@ class WeightDemodulation(nn.Module):
         if self.demod:
             d = torch.rsqrt((weight ** 2).sum(dim=(2, 3, 4), keepdim=True) + self.eps)
             weight = weight * d
-        x = x.reshape(1, -1, h, w)
-        _, _, *ws = weight.shape
-        weight = weight.reshape(b * self.conv.out_channels, *ws)
-        bias = self.conv.bias.repeat(b) if self.conv.bias is not None else None
-        from imaginaire_amd.ops.conv import conv2d as _conv2d
-        x = _conv2d(x, weight, bias, self.conv.stride, self.conv.padding, self.conv.dilation,
-                    groups=b)
-        x = x.reshape(-1, self.conv.out_channels, x.shape[2], x.shape[3])
+        from imaginaire_amd.ops import conv as conv_ops
+        stride = self.conv.stride[0] if self.conv.stride[0] == self.conv.stride[1] else None
+        if isinstance(self.conv.padding, tuple) and stride == 1 and \
+                conv_ops.per_sample_eligible(x, weight, stride, 1):
+            # per-sample (modulated) weights as ONE batched k10 launch, grid z = sample (and
+            # batched k10 / k11 backward), instead of a b-group MIOpen convolution
+            bias = self.conv.bias[None].expand(b, -1) if self.conv.bias is not None else None
+            x = conv_ops.conv2d_per_sample(x, weight, bias, self.conv.padding,
+                                           self.conv.dilation)
+        else:
+            x = x.reshape(1, -1, h, w)
+            _, _, *ws = weight.shape
+            weight = weight.reshape(b * self.conv.out_channels, *ws)
+            bias = self.conv.bias.repeat(b) if self.conv.bias is not None else None
+            x = conv_ops.conv2d(x, weight, bias, self.conv.stride, self.conv.padding,
+                                self.conv.dilation, groups=b)
+            x = x.reshape(-1, self.conv.out_channels, x.shape[2], x.shape[3])
         if self.adaptive_bias:
             x = x + self.fc_beta(y)[:, :, None, None]
         return x

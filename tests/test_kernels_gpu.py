@@ -848,3 +848,42 @@ def test_multi_tensor_gan_loss(dtype, mode, t_real, dis_update):
         assert x.grad.dtype == dtype and x.grad.shape == x.shape
         torch.testing.assert_close(x.grad.float(), r.grad, atol=2e-3 * float(r.grad.abs().max()) + 1e-9,
                                    rtol=1e-2)
+
+
+@pytest.mark.gpu
+def test_weight_demod_conv_per_sample_path():
+    """StyleGAN2 modulated/demodulated conv (weight_demod) on the batched per-sample k10 path
+    == the grouped fp32 convolution of the reference formulation, forward and backward."""
+    from imaginaire_amd.config import AttrDict
+    from imaginaire_amd.layers import Conv2dBlock
+    from imaginaire_amd.ops import conv as C
+    torch.manual_seed(4)
+    blk = Conv2dBlock(64, 128, 3, padding=1, weight_norm_type='weight_demod',
+                      weight_norm_params=AttrDict(cond_dims=32)).cuda()
+    x = torch.randn(3, 64, 24, 40, device='cuda').contiguous(memory_format=torch.channels_last)
+    y = torch.randn(3, 32, device='cuda')
+    wd = blk.layers.conv
+    w5 = wd.conv.weight[None] * (wd.fc_gamma(y)[:, None, :, None, None] + 1)
+    assert C.per_sample_eligible(x.bfloat16(), w5.bfloat16(), 1, 1)
+    xr = x.clone().requires_grad_(True)
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        out = blk(xr, y)
+    params = [p for p in blk.parameters()]
+    g = torch.randn_like(out.float())
+    grads = torch.autograd.grad(out.float(), [xr] + params, g)
+
+    def ref_forward(xx):
+        b, c, h, w = xx.shape
+        gamma = wd.fc_gamma(y)[:, None, :, None, None]
+        wt = wd.conv.weight[None] * (gamma + 1)
+        wt = wt * torch.rsqrt((wt ** 2).sum(dim=(2, 3, 4), keepdim=True) + wd.eps)
+        o = F.conv2d(xx.reshape(1, -1, h, w), wt.reshape(b * 128, 64, 3, 3),
+                     wd.conv.bias.repeat(b), 1, 1, 1, groups=b)
+        return o.reshape(b, 128, h, w)
+    xf = x.clone().requires_grad_(True)
+    with torch.autocast('cuda', enabled=False):
+        ref = ref_forward(xf)
+    rgrads = torch.autograd.grad(ref, [xf] + params, g)
+    torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=3e-2)
+    for a, r in zip(grads, rgrads):
+        torch.testing.assert_close(a.float(), r, atol=5e-2 * float(r.abs().max()) + 1e-6, rtol=5e-2)
