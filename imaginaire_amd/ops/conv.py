@@ -507,8 +507,11 @@ def tapsplit_eligible(x, w, stride, padding, dilation, groups):
         return False
     npix = x.shape[0] * x.shape[2] * x.shape[3]
     cp, cz = _round_up(cin, 64), _round_up(cout * kh * kw, 64)
-    # k10 / k11 32-bit buffer offsets on x and on the partials Z / dZ
-    return npix >= 128 * 64 and npix * cp * 2 < (1 << 30) and npix * cz * 2 < (1 << 30)
+    # the partials Z must not outweigh the input (MUNIT's 64 -> 3 7x7 head: 147 partial
+    # channels per pixel ran slower than the direct 64-wide k10 tile,
+    # profiles/recipe_munit256_conv_log_mi355x.txt); k10 / k11 32-bit buffer offsets
+    return cz <= cp and npix >= 128 * 64 and npix * cp * 2 < (1 << 30) and \
+        npix * cz * 2 < (1 << 30)
 
 
 _WGRAD_CHOICE = {}

@@ -193,3 +193,60 @@ def test_ddp_spade_world2_grads_match_single_process(comm):
     gr = ref[2]
     rel = float((g0 - gr).norm() / gr.norm())
     assert rel < (2e-2 if comm else 2e-3), rel
+
+
+def _rccl_world1_worker(rank, world, port, q):
+    import sys
+    import faulthandler
+    import torch.distributed as dist
+    faulthandler.dump_traceback_later(150, exit=True, file=sys.__stderr__)
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK='0', WORLD_SIZE='1',
+                      LOCAL_RANK='0')
+    torch.cuda.set_device(0)
+    dist.init_process_group('nccl', rank=0, world_size=1, device_id=torch.device('cuda', 0))
+    from imaginaire_amd.parallel import DistributedDataParallel
+    out = {}
+    for comm in (None, torch.bfloat16):
+        torch.manual_seed(0)
+        net = torch.nn.Sequential(torch.nn.Conv2d(8, 16, 3, padding=1), torch.nn.ReLU(),
+                                  torch.nn.Conv2d(16, 4, 3, padding=1)).cuda()
+        unused = torch.nn.Linear(3, 3).cuda()
+        holder = torch.nn.ModuleDict({'net': net, 'unused': unused})
+        ref = [p.detach().clone() for p in net.parameters()]
+        ddp = DistributedDataParallel(holder, bucket_cap_mb=0.002, first_bucket_mb=0.001,
+                                      comm_dtype=comm, _force_distributed=True)
+        x = torch.randn(2, 8, 12, 12, device='cuda')
+        grads = []
+        for it in range(2):  # the second backward must not see the first one's gradients
+            ddp.begin()
+            ddp.module['net'](x * (it + 1)).pow(2).mean().backward()
+            ddp.finish()
+            grads.append([p.grad.detach().clone() for p in net.parameters()])
+        # plain single-process gradients of the same two backwards
+        plain = torch.nn.Sequential(torch.nn.Conv2d(8, 16, 3, padding=1), torch.nn.ReLU(),
+                                    torch.nn.Conv2d(16, 4, 3, padding=1)).cuda()
+        with torch.no_grad():
+            for p, r in zip(plain.parameters(), ref):
+                p.copy_(r)
+        ok = True
+        for it in range(2):
+            plain.zero_grad(set_to_none=True)
+            plain(x * (it + 1)).pow(2).mean().backward()
+            tol = 1e-5 if comm is None else 1e-2
+            for g, p in zip(grads[it], plain.parameters()):
+                ok &= bool(torch.allclose(g, p.grad, atol=tol, rtol=tol))
+        ok &= all(p.grad is None for p in unused.parameters())
+        ok &= len(ddp.buckets) > 1
+        out['bf16' if comm else 'fp32'] = (ok, ddp._avg)
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+def test_ddp_rccl_world1_buckets_avg_and_unused():
+    """The bucketed DDP on a real RCCL communicator (world size 1, forced through the
+    distributed path): ReduceOp.AVG is detected, hook-filled buckets reproduce the plain
+    gradients over two backwards (fp32 and bf16 wire), unused parameters keep grad None."""
+    (_, out), = _spawn(_rccl_world1_worker, 1)
+    for k, (ok, avg) in out.items():
+        assert ok, k
+        assert avg, 'RCCL should average in the collective (ReduceOp.AVG)'

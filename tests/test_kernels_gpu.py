@@ -769,7 +769,7 @@ def test_conv2d_per_sample_batched(case):
 @pytest.mark.parametrize('case', [
     # B, cin, cout, H, W, k, p, d, bias, autocast
     (2, 256, 3, 64, 96, 5, 2, 1, True, False),    # SPADE conv_img (256 -> 3, 5x5)
-    (1, 64, 3, 96, 100, 7, 3, 1, True, True),     # pix2pixHD / vid2vid 7x7 head, fp32 params
+    (1, 256, 3, 96, 100, 7, 3, 1, True, True),    # pix2pixHD / vid2vid 7x7 head, fp32 params
     (2, 96, 1, 65, 79, 3, 2, 2, False, False),    # dilation, odd sizes, Cin padded to 128
     (1, 128, 8, 96, 98, 3, 0, 1, True, False),    # valid conv (no padding), Cout 8
 ])
