@@ -9,7 +9,8 @@ from types import SimpleNamespace
 
 import torch
 from torch import nn
-from torch.nn import Upsample as NearestUpsample
+# nn.Upsample runs in fp32 under autocast; this one is the bf16 NHWC k12 resize
+from imaginaire_amd.ops.resize import Upsample as NearestUpsample
 
 from imaginaire_amd.generators.unit import ContentEncoder, _kw, _name
 from imaginaire_amd.layers import Conv2dBlock, LinearBlock, Res2dBlock

@@ -2,7 +2,8 @@
 import warnings
 
 from torch import nn
-from torch.nn import Upsample as NearestUpsample
+# nn.Upsample runs in fp32 under autocast; this one is the bf16 NHWC k12 resize
+from imaginaire_amd.ops.resize import Upsample as NearestUpsample
 
 from imaginaire_amd.layers import Conv2dBlock, Res2dBlock
 
