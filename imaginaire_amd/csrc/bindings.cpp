@@ -100,6 +100,7 @@ at::Tensor conv_tap_sum(const at::Tensor& z, const c10::optional<at::Tensor>& bi
 at::Tensor conv_tap_gather(const at::Tensor& dy, int64_t Cz, int64_t KH, int64_t KW, int64_t ph,
                            int64_t pw, int64_t dh, int64_t dw, int64_t H, int64_t W);
 // conv_aux.hip
+at::Tensor pad_channels_cast(const at::Tensor& x, int64_t Cp, at::ScalarType dtype);
 void conv_phase_scatter(const at::Tensor& src, at::Tensor& dst, int64_t s, int64_t ry, int64_t rx,
                         int64_t i0, int64_t j0, int64_t Qy, int64_t Qx);
 at::Tensor conv_weight_flip_t(const at::Tensor& w, int64_t s, int64_t qy, int64_t qx,
@@ -138,6 +139,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_tap_gather", &iamd::conv_tap_gather, "tap-split conv backward: dy -> per-tap dZ");
   m.def("conv_phase_scatter", &iamd::conv_phase_scatter,
         "strided-conv dgrad: one phase conv output into its parity sub-grid of dx");
+  m.def("pad_channels_cast", &iamd::pad_channels_cast,
+        "zero-padded channel copy + dtype cast into a channels-last tensor");
   m.def("pad_nhwc_fwd", &iamd::pad_nhwc_fwd, "NHWC reflect / replicate padding");
   m.def("pad_nhwc_bwd", &iamd::pad_nhwc_bwd, "NHWC reflect / replicate padding backward (gather)");
   m.def("conv_weight_flip_t", &iamd::conv_weight_flip_t,

@@ -239,6 +239,35 @@ phase_scatter_kernel(const __hip_bfloat16* __restrict__ src, __hip_bfloat16* __r
   }
 }
 
+// Zero-padded channel copy with dtype cast: y[b, h, w, c] = c < C ? x[b, c, h, w] : 0 for
+// c < Cp, y channels-last in TO, x in TI with arbitrary strides (NHWC activations, NCHW image
+// batches). One thread per 8 output channels of a pixel: one 16-byte (bf16) / two (fp32)
+// stores, instead of a strided zero-fill of the tail plus a strided copy plus a cast pass.
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(kT)
+pad_cast_kernel(const TI* __restrict__ x, TO* __restrict__ y, int B, int C, int H, int W, int Cp,
+                int64_t sb, int64_t sc, int64_t sh, int64_t sw) {
+  const int cv = Cp / 8;
+  const int64_t total = (int64_t)B * H * W * cv;
+  for (int64_t t = (int64_t)blockIdx.x * kT + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * kT) {
+    const int c8 = (int)(t % cv);
+    int64_t p = t / cv;
+    const int w = (int)(p % W);
+    p /= W;
+    const int h = (int)(p % H);
+    const int b = (int)(p / H);
+    const TI* xp = x + b * sb + h * sh + w * sw;
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = c8 * 8 + k;
+      v[k] = c < C ? to_f<TI>(xp[c * sc]) : 0.f;
+    }
+    store_vec<TO, 8>(y + t * 8, v);
+  }
+}
+
 int pad_grid(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + kT - 1) / kT, 65536)); }
 
 }  // namespace
@@ -383,6 +412,34 @@ void conv_phase_scatter(const at::Tensor& src, at::Tensor& dst, int64_t s, int64
                      reinterpret_cast<__hip_bfloat16*>(dst.data_ptr()), B, C, Hs, Ws, H, W, (int)s,
                      (int)ry, (int)rx, (int)i0, (int)j0, (int)Qy, (int)Qx);
   IAMD_LAUNCH_CHECK();
+}
+
+// x [B, C, H, W] (bf16 / fp32, any strides) -> channels-last [B, Cp, H, W] in `dtype`, channels
+// C..Cp-1 zero (Cp % 8 == 0, Cp >= C)
+at::Tensor pad_channels_cast(const at::Tensor& x, int64_t Cp, at::ScalarType dtype) {
+  IAMD_CHECK(x.is_cuda() && x.dim() == 4, "pad_channels_cast: 4-D CUDA tensor expected");
+  IAMD_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat,
+             "pad_channels_cast: bf16 / fp32 input");
+  IAMD_CHECK(dtype == at::kBFloat16 || dtype == at::kFloat, "pad_channels_cast: bf16 / fp32 out");
+  const int B = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  IAMD_CHECK(Cp % 8 == 0 && Cp >= C, "pad_channels_cast: Cp must be a multiple of 8 >= C");
+  auto y = at::empty({B, Cp, H, W}, x.options().dtype(dtype).memory_format(at::MemoryFormat::ChannelsLast));
+  const int64_t total = (int64_t)B * H * W * (Cp / 8);
+  if (total == 0) return y;
+  auto launch = [&](auto ti, auto to) {
+    using TI = decltype(ti);
+    using TO = decltype(to);
+    hipLaunchKernelGGL((pad_cast_kernel<TI, TO>), dim3(pad_grid(total)), dim3(kT), 0, stream(),
+                       reinterpret_cast<const TI*>(x.data_ptr()), reinterpret_cast<TO*>(y.data_ptr()),
+                       B, C, H, W, (int)Cp, x.stride(0), x.stride(1), x.stride(2), x.stride(3));
+  };
+  const bool ib = x.scalar_type() == at::kBFloat16, ob = dtype == at::kBFloat16;
+  if (ib && ob) launch(__hip_bfloat16(), __hip_bfloat16());
+  else if (ib) launch(__hip_bfloat16(), float());
+  else if (ob) launch(float(), __hip_bfloat16());
+  else launch(float(), float());
+  IAMD_LAUNCH_CHECK();
+  return y;
 }
 
 }  // namespace iamd

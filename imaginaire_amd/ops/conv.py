@@ -126,11 +126,20 @@ def _out_pad(cout):
     return _round_up(cout, 64)
 
 
-def _pad_channels(t, c):
-    """Zero-pad dim 1 of a 4-D tensor to ``c`` channels (packed channels-last result)."""
+def _pad_channels(t, c, dtype=None):
+    """Zero-pad dim 1 of a 4-D tensor to ``c`` channels (packed channels-last result), cast to
+    ``dtype`` (default: t's). Outside autograd on the GPU this is ONE pass of the
+    ``pad_channels_cast`` kernel (16-byte stores of whole padded pixels, any input layout);
+    differentiable inputs keep the autograd-visible slice copy."""
+    dtype = dtype or t.dtype
     if t.shape[1] == c:
-        return nhwc(t)
-    out = torch.empty((t.shape[0], c, t.shape[2], t.shape[3]), dtype=t.dtype, device=t.device,
+        return nhwc(t.to(dtype))
+    if t.is_cuda and t.dim() == 4 and c % 8 == 0 and _ext.use_native(t) and \
+            t.dtype in (torch.bfloat16, torch.float32) and \
+            dtype in (torch.bfloat16, torch.float32) and \
+            not (t.requires_grad and torch.is_grad_enabled()):
+        return _ext.ext().pad_channels_cast(t, c, dtype)
+    out = torch.empty((t.shape[0], c, t.shape[2], t.shape[3]), dtype=dtype, device=t.device,
                       memory_format=_CL)
     out[:, t.shape[1]:].zero_()
     out[:, :t.shape[1]] = t
@@ -290,8 +299,8 @@ class _MfmaConv2d(torch.autograd.Function):
     def forward(ctx, x, w, bias, stride, padding, dilation, slope):
         cout, cin = w.shape[0], w.shape[1]
         cp, op = _round_up(cin, 64), _out_pad(cout)
-        xb = _pad_channels(x.to(torch.bfloat16), cp)
-        wb = _pad_rows(_pad_channels(w.to(torch.bfloat16), cp), op)
+        xb = _pad_channels(x, cp, torch.bfloat16)
+        wb = _pad_rows(_pad_channels(w, cp, torch.bfloat16), op)
         ho, wo = _out_hw(x.shape[2], x.shape[3], w.shape[2:], stride, padding, dilation)
         with _Logged('fwd', 'k10', 2.0 * x.shape[0] * ho * wo * op * cp * w.shape[2] * w.shape[3],
                      _gemm_desc(xb, wb, stride, padding)):
@@ -314,7 +323,7 @@ class _MfmaConv2d(torch.autograd.Function):
         xb, wb, y = ctx.saved_tensors
         stride, padding, dilation, slope, cin, cout, xdt, wdt, bdt, xc = ctx.conf
         need_x, need_w, need_b = ctx.needs_input_grad[:3]
-        dy = _pad_channels(dy.to(torch.bfloat16), wb.shape[0])
+        dy = _pad_channels(dy, wb.shape[0], torch.bfloat16)
         db = None
         if slope != 1.0 or need_b:
             # identity activation: the k2 kernel reads only dy (y stands in for the layout)
@@ -371,7 +380,7 @@ class _MfmaConvPerSample(torch.autograd.Function):
     def forward(ctx, x, w, bias, padding, dilation):
         B, cout, cin, kh, kw = w.shape
         cp, op = _round_up(cin, 64), _round_up(cout, 64)
-        xb = _pad_channels(x.to(torch.bfloat16), cp)
+        xb = _pad_channels(x, cp, torch.bfloat16)
         # sample-major channels-last weights [B][op][kh][kw][cp], zero-padded
         wp = w.new_zeros((B, op, kh, kw, cp), dtype=torch.bfloat16)
         wp[:, :cout, :, :, :cin] = w.permute(0, 1, 3, 4, 2)
@@ -397,7 +406,7 @@ class _MfmaConvPerSample(torch.autograd.Function):
         B, cp = xb.shape[0], xb.shape[1]
         op = wb.shape[0] // B
         kh, kw = wb.shape[2], wb.shape[3]
-        dy = _pad_channels(dy.to(torch.bfloat16), op)
+        dy = _pad_channels(dy, op, torch.bfloat16)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             pt = (dilation[0] * (kh - 1) - padding[0], dilation[1] * (kw - 1) - padding[1])
@@ -449,7 +458,7 @@ class _TapSplitConv2d(torch.autograd.Function):
     def forward(ctx, x, w, bias, padding, dilation):
         cout, cin, kh, kw = w.shape
         cp, cz = _round_up(cin, 64), _round_up(cout * kh * kw, 64)
-        xb = _pad_channels(x.to(torch.bfloat16), cp)
+        xb = _pad_channels(x, cp, torch.bfloat16)
         # Wz[t*cout + c, ci] = w[c, ci, t]
         wz = torch.zeros((cz, cp), dtype=torch.bfloat16, device=w.device)
         wz[:cout * kh * kw, :cin] = w.to(torch.bfloat16).permute(2, 3, 0, 1).reshape(-1, cin)

@@ -887,3 +887,22 @@ def test_weight_demod_conv_per_sample_path():
     torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=3e-2)
     for a, r in zip(grads, rgrads):
         torch.testing.assert_close(a.float(), r, atol=5e-2 * float(r.abs().max()) + 1e-6, rtol=5e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('src_dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('dst_dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('layout', ['nchw', 'nhwc'])
+def test_pad_channels_cast(src_dtype, dst_dtype, layout):
+    """One-pass zero-padded channel copy + cast into channels-last (RGB 3 -> 64, label maps
+    185 -> 192) == the slice-copy reference, from NCHW and NHWC sources."""
+    from imaginaire_amd.ops import _ext
+    for c, cp in ((3, 64), (185, 192), (8, 16)):
+        x = torch.randn(2, c, 9, 13, device='cuda').to(src_dtype)
+        if layout == 'nhwc':
+            x = x.contiguous(memory_format=torch.channels_last)
+        y = _ext.ext().pad_channels_cast(x, cp, dst_dtype)
+        assert y.dtype == dst_dtype and y.shape == (2, cp, 9, 13)
+        assert y.is_contiguous(memory_format=torch.channels_last)
+        assert torch.equal(y[:, :c].float(), x.to(dst_dtype).float())
+        assert not y[:, c:].any()
