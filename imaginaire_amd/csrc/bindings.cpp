@@ -82,7 +82,8 @@ at::Tensor channelnorm_backward(const at::Tensor& x, const at::Tensor& out,
 // flow_warp.hip (k9 warp, k7 resample2d)
 at::Tensor flow_warp_fwd(const at::Tensor& img, const at::Tensor& flow);
 std::vector<at::Tensor> flow_warp_bwd(const at::Tensor& img, const at::Tensor& flow,
-                                      const at::Tensor& dout);
+                                      const at::Tensor& dout,
+                                      bool need_dimg);
 at::Tensor resample2d_forward(const at::Tensor& in1, const at::Tensor& flow, int64_t ks);
 std::vector<at::Tensor> resample2d_backward(const at::Tensor& in1, const at::Tensor& flow,
                                             const at::Tensor& dout, int64_t ks);
@@ -180,7 +181,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("resize_nearest_fwd", &iamd::resize_nearest_fwd, "NHWC nearest resize (k12)");
   m.def("resize_nearest_bwd", &iamd::resize_nearest_bwd, "k12 nearest backward (gather)");
   m.def("flow_warp_fwd", &iamd::flow_warp_fwd, "bilinear flow warp, border (k9)");
-  m.def("flow_warp_bwd", &iamd::flow_warp_bwd, "k9 backward");
+  m.def("flow_warp_bwd", &iamd::flow_warp_bwd, "k9 backward", py::arg("img"), py::arg("flow"),
+        py::arg("dout"), py::arg("need_dimg") = true);
   m.def("resample2d_forward", &iamd::resample2d_forward, "FlowNet2 Resample2d (k7)");
   m.def("resample2d_backward", &iamd::resample2d_backward, "k7 backward");
   m.def("correlation_forward", &iamd::correlation_forward, "FlowNet correlation (k6)");

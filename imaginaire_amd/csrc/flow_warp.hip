@@ -7,7 +7,9 @@
 // w.r.t. the flow where clamped). One thread per output pixel loops over
 // channels so the 4 tap weights / addresses are computed once and reused.
 // Backward: d(image) by fp32 atomics (4 taps per pixel, contention-free across
-// waves), d(flow) = Σ_c dout · ∂sample/∂(x,y) with no atomics.
+// waves), d(flow) = Σ_c dout · ∂sample/∂(x,y) with no atomics. When the image needs no
+// gradient (the detached previous frame of vid2vid) the scatter is skipped entirely, and
+// ops/flow_warp.py replaces it by a sort-based deterministic scatter in deterministic mode.
 //
 // k7 reproduces third_party/resample2d/src/resample2d_kernel.cu:15-203
 // semantics (edge-clamped taps, kernel_size² window average), written for
@@ -85,7 +87,7 @@ warp_bwd(const T* __restrict__ img, const T* __restrict__ flow, const T* __restr
     const float w10 = (1.f - t.wx) * t.wy, w11 = t.wx * t.wy;
     const T* ib = img + b * isb;
     const T* db = dout + b * dsb + y * dsy + x * dsx;
-    float* gb = dimg + (int64_t)b * C * H * W;
+    float* gb = dimg != nullptr ? dimg + (int64_t)b * C * H * W : nullptr;
     const int64_t HW = (int64_t)H * W;
     float gx = 0.f, gy = 0.f;
     for (int c = 0; c < C; ++c) {
@@ -97,11 +99,13 @@ warp_bwd(const T* __restrict__ img, const T* __restrict__ flow, const T* __restr
       const float v11 = to_f<T>(ic[t.y1 * isy + t.x1 * isx]);
       gx += g * ((v01 - v00) * (1.f - t.wy) + (v11 - v10) * t.wy);
       gy += g * ((v10 - v00) * (1.f - t.wx) + (v11 - v01) * t.wx);
-      float* gc = gb + c * HW;
-      atomicAdd(gc + t.y0 * W + t.x0, g * w00);
-      atomicAdd(gc + t.y0 * W + t.x1, g * w01);
-      atomicAdd(gc + t.y1 * W + t.x0, g * w10);
-      atomicAdd(gc + t.y1 * W + t.x1, g * w11);
+      if (dimg != nullptr) {
+        float* gc = gb + c * HW;
+        atomicAdd(gc + t.y0 * W + t.x0, g * w00);
+        atomicAdd(gc + t.y0 * W + t.x1, g * w01);
+        atomicAdd(gc + t.y1 * W + t.x0, g * w10);
+        atomicAdd(gc + t.y1 * W + t.x1, g * w11);
+      }
     }
     float* dfp = dflow + (int64_t)b * 2 * HW + (int64_t)y * W + x;
     dfp[0] = t.cx ? 0.f : gx;
@@ -214,18 +218,19 @@ at::Tensor flow_warp_fwd(const at::Tensor& img, const at::Tensor& flow) {
 }
 
 std::vector<at::Tensor> flow_warp_bwd(const at::Tensor& img, const at::Tensor& flow,
-                                      const at::Tensor& dout) {
+                                      const at::Tensor& dout, bool need_dimg) {
   at::Tensor fl = flow.scalar_type() == img.scalar_type() ? flow : flow.to(img.scalar_type());
   at::Tensor g = dout.scalar_type() == img.scalar_type() ? dout : dout.to(img.scalar_type());
   const int B = img.size(0), C = img.size(1), H = img.size(2), W = img.size(3);
   auto fopt = img.options().dtype(at::kFloat);
-  auto dimg = at::zeros({B, C, H, W}, fopt);
+  auto dimg = need_dimg ? at::zeros({B, C, H, W}, fopt) : at::Tensor();
   auto dflow = at::empty({B, 2, H, W}, fopt);
   IAMD_DISPATCH_FLOAT_TYPES(img.scalar_type(), "flow_warp_bwd", [&] {
     hipLaunchKernelGGL((warp_bwd<scalar_t>), dim3(grid_for((int64_t)B * H * W)), dim3(kThreads),
                        0, stream(), reinterpret_cast<const scalar_t*>(img.data_ptr()),
                        reinterpret_cast<const scalar_t*>(fl.data_ptr()),
-                       reinterpret_cast<const scalar_t*>(g.data_ptr()), dimg.data_ptr<float>(),
+                       reinterpret_cast<const scalar_t*>(g.data_ptr()),
+                       need_dimg ? dimg.data_ptr<float>() : nullptr,
                        dflow.data_ptr<float>(), B, C, H, W, img.stride(0), img.stride(1),
                        img.stride(2), img.stride(3), fl.stride(0), fl.stride(1), fl.stride(2),
                        fl.stride(3), g.stride(0), g.stride(1), g.stride(2), g.stride(3));

@@ -19,12 +19,46 @@ class _FlowWarpFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         image, flow = ctx.saved_tensors
-        dimg, dflow = _ext.ext().flow_warp_bwd(image, flow, dout.contiguous())
-        dimg = dimg.to(image.dtype) if ctx.needs_input_grad[0] else None
+        need_img = ctx.needs_input_grad[0]
+        deterministic = need_img and torch.are_deterministic_algorithms_enabled()
+        # the image scatter runs in the kernel (float atomics) unless the image needs no
+        # gradient (vid2vid's detached previous frame) or the run must be reproducible
+        dimg, dflow = _ext.ext().flow_warp_bwd(image, flow, dout.contiguous(),
+                                               need_img and not deterministic)
+        if deterministic:
+            dimg = _scatter_image_grad_deterministic(image, flow, dout)
+        dimg = dimg.to(image.dtype) if need_img else None
         if dimg is not None and image.is_contiguous(memory_format=torch.channels_last) and \
                 not image.is_contiguous():
             dimg = dimg.contiguous(memory_format=torch.channels_last)
         return dimg, (dflow.to(flow.dtype) if ctx.needs_input_grad[1] else None)
+
+
+def _scatter_image_grad_deterministic(image, flow, dout):
+    """d(image) of the border-clamped bilinear warp as ONE accumulate-``index_put_`` of the
+    4 x B*H*W tap contributions: with deterministic algorithms enabled PyTorch sorts the
+    indices and sums in a fixed order, so the result is bitwise reproducible."""
+    b, c, h, w = image.shape
+    f = flow.float()
+    ys, xs = torch.meshgrid(torch.arange(h, device=image.device, dtype=torch.float32),
+                            torch.arange(w, device=image.device, dtype=torch.float32),
+                            indexing='ij')
+    sx = (xs[None] + f[:, 0]).clamp(0, w - 1)
+    sy = (ys[None] + f[:, 1]).clamp(0, h - 1)
+    x0, y0 = sx.floor(), sy.floor()
+    wx, wy = sx - x0, sy - y0
+    x0, y0 = x0.long(), y0.long()
+    x1, y1 = (x0 + 1).clamp(max=w - 1), (y0 + 1).clamp(max=h - 1)
+    base = (torch.arange(b, device=image.device) * (h * w)).view(b, 1, 1)
+    g = dout.float().permute(0, 2, 3, 1).reshape(-1, c)  # [B*H*W, C]
+    idx, vals = [], []
+    for yy, xx, wt in ((y0, x0, (1 - wx) * (1 - wy)), (y0, x1, wx * (1 - wy)),
+                       (y1, x0, (1 - wx) * wy), (y1, x1, wx * wy)):
+        idx.append((base + yy * w + xx).reshape(-1))
+        vals.append(g * wt.reshape(-1, 1))
+    out = torch.zeros(b * h * w, c, device=image.device, dtype=torch.float32)
+    out.index_put_((torch.cat(idx),), torch.cat(vals), accumulate=True)
+    return out.view(b, h, w, c).permute(0, 3, 1, 2)
 
 
 def flow_warp_reference(image, flow):

@@ -906,3 +906,33 @@ def test_pad_channels_cast(src_dtype, dst_dtype, layout):
         assert y.is_contiguous(memory_format=torch.channels_last)
         assert torch.equal(y[:, :c].float(), x.to(dst_dtype).float())
         assert not y[:, c:].any()
+
+
+@pytest.mark.gpu
+def test_flow_warp_backward_modes():
+    """k9 backward: the flow-only path (detached image: no scatter) gives the same flow
+    gradient, and deterministic mode's sort-based image scatter matches the atomic kernel and
+    is bitwise reproducible."""
+    from imaginaire_amd.ops.flow_warp import flow_warp
+    torch.manual_seed(6)
+    img = torch.randn(2, 3, 40, 56, device='cuda')
+    flow = (torch.randn(2, 2, 40, 56, device='cuda') * 6).requires_grad_(True)
+    g = torch.randn(2, 3, 40, 56, device='cuda')
+    ia = img.clone().requires_grad_(True)
+    fa = flow.detach().clone().requires_grad_(True)
+    flow_warp(ia, fa).backward(g)
+    fb = flow.detach().clone().requires_grad_(True)
+    flow_warp(img, fb).backward(g)  # image needs no grad: flow gradient only
+    assert torch.equal(fa.grad, fb.grad)
+    grads = []
+    prev = torch.are_deterministic_algorithms_enabled()
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    try:
+        for _ in range(2):
+            ic = img.clone().requires_grad_(True)
+            flow_warp(ic, flow.detach()).backward(g)
+            grads.append(ic.grad.clone())
+    finally:
+        torch.use_deterministic_algorithms(prev)
+    assert torch.equal(grads[0], grads[1])
+    torch.testing.assert_close(grads[0], ia.grad, atol=1e-4, rtol=1e-4)
