@@ -100,6 +100,11 @@ at::Tensor conv_tap_sum(const at::Tensor& z, const c10::optional<at::Tensor>& bi
                         int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t dh, int64_t dw);
 at::Tensor conv_tap_gather(const at::Tensor& dy, int64_t Cz, int64_t KH, int64_t KW, int64_t ph,
                            int64_t pw, int64_t dh, int64_t dw, int64_t H, int64_t W);
+// pool.hip
+at::Tensor avg_pool_nhwc_fwd(const at::Tensor& x, int64_t kh, int64_t kw, int64_t sh, int64_t sw,
+                             int64_t ph, int64_t pw, bool include_pad);
+at::Tensor avg_pool_nhwc_bwd(const at::Tensor& dy, int64_t H, int64_t W, int64_t kh, int64_t kw,
+                             int64_t sh, int64_t sw, int64_t ph, int64_t pw, bool include_pad);
 // conv_aux.hip
 at::Tensor pad_channels_cast(const at::Tensor& x, int64_t Cp, at::ScalarType dtype);
 void conv_phase_scatter(const at::Tensor& src, at::Tensor& dst, int64_t s, int64_t ry, int64_t rx,
@@ -142,6 +147,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "strided-conv dgrad: one phase conv output into its parity sub-grid of dx");
   m.def("pad_channels_cast", &iamd::pad_channels_cast,
         "zero-padded channel copy + dtype cast into a channels-last tensor");
+  m.def("avg_pool_nhwc_fwd", &iamd::avg_pool_nhwc_fwd, "NHWC average pooling (k14)");
+  m.def("avg_pool_nhwc_bwd", &iamd::avg_pool_nhwc_bwd, "k14 backward (gather)");
   m.def("pad_nhwc_fwd", &iamd::pad_nhwc_fwd, "NHWC reflect / replicate padding");
   m.def("pad_nhwc_bwd", &iamd::pad_nhwc_bwd, "NHWC reflect / replicate padding backward (gather)");
   m.def("conv_weight_flip_t", &iamd::conv_weight_flip_t,

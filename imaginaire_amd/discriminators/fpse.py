@@ -7,6 +7,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from imaginaire_amd.layers import Conv2dBlock
+from imaginaire_amd.ops.pool import avg_pool2d
 from imaginaire_amd.ops.resize import Upsample, upsample_add
 
 
@@ -77,12 +78,12 @@ class FPSEDiscriminator(nn.Module):
         # block: pool the label map first so the 1x1 conv (and its weight gradient) runs at
         # half resolution and the full-resolution 2F-channel embedding is never materialised
         if self._embedding_is_linear():
-            segembs = self.embedding(F.avg_pool2d(segmaps, kernel_size=2, stride=2))
+            segembs = self.embedding(avg_pool2d(segmaps, kernel_size=2, stride=2))
         else:
-            segembs = F.avg_pool2d(self.embedding(segmaps), kernel_size=2, stride=2)
-        segembs2 = F.avg_pool2d(segembs, kernel_size=2, stride=2)
-        segembs3 = F.avg_pool2d(segembs2, kernel_size=2, stride=2)
-        segembs4 = F.avg_pool2d(segembs3, kernel_size=2, stride=2)
+            segembs = avg_pool2d(self.embedding(segmaps), kernel_size=2, stride=2)
+        segembs2 = avg_pool2d(segembs, kernel_size=2, stride=2)
+        segembs3 = avg_pool2d(segembs2, kernel_size=2, stride=2)
+        segembs4 = avg_pool2d(segembs3, kernel_size=2, stride=2)
         if seg_repeat > 1:
             segembs2, segembs3, segembs4 = (e.repeat(seg_repeat, 1, 1, 1)
                                             for e in (segembs2, segembs3, segembs4))

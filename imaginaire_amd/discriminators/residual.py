@@ -5,6 +5,7 @@ import torch
 import torch.nn as nn
 
 from imaginaire_amd.layers import Conv2dBlock, Res2dBlock
+from imaginaire_amd.ops.pool import AvgPool2d
 
 
 class ResDiscriminator(nn.Module):
@@ -25,7 +26,7 @@ class ResDiscriminator(nn.Module):
             num_filters_prev = num_filters
             num_filters = min(num_filters * 2, max_num_filters)
             model.append(Res2dBlock(num_filters_prev, num_filters, order=order, **conv_params))
-            model.append(nn.AvgPool2d(2, stride=2))
+            model.append(AvgPool2d(2, stride=2))
         if aggregation == 'pool':
             model += [torch.nn.AdaptiveAvgPool2d(1)]
         elif aggregation == 'conv':

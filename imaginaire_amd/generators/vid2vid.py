@@ -21,6 +21,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from imaginaire_amd.generators.fs_vid2vid import LabelEmbedder
+from imaginaire_amd.ops.pool import AvgPool2d
 from imaginaire_amd.layers import Conv2dBlock, LinearBlock, Res2dBlock
 from imaginaire_amd.model_utils.fs_vid2vid import extract_valid_pose_labels, resample
 from imaginaire_amd.utils.data import (get_paired_input_image_channel_number,
@@ -105,7 +106,7 @@ class Generator(BaseNetwork):
             self.fc = Conv2dBlock(num_input_channels, top, kernel_size=3, padding=1)
         else:
             self.fc = LinearBlock(self.z_dim, top * self.sh * self.sw)
-        self.downsample = nn.AvgPool2d(kernel_size=3, stride=2, padding=1)
+        self.downsample = AvgPool2d(kernel_size=3, stride=2, padding=1)
         self.upsample = partial(interpolate, scale_factor=2)
         self.init_temporal_network()
 

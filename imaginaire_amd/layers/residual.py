@@ -8,6 +8,7 @@ The blocks' norm/activation pairs run as fused HIP kernels via the conv blocks.
 import functools
 
 from torch import nn
+from imaginaire_amd.ops.pool import AvgPool2d
 from imaginaire_amd.ops.resize import Upsample as NearestUpsample
 from torch.utils.checkpoint import checkpoint
 
@@ -209,7 +210,7 @@ class DownRes2dBlock(_BaseDownResBlock):
                  activation_norm_params=None, skip_activation_norm=True,
                  skip_nonlinearity=False, nonlinearity='leakyrelu', inplace_nonlinearity=False,
                  apply_noise=False, hidden_channels_equal_out_channels=False, order='CNACNA',
-                 pooling=nn.AvgPool2d, down_factor=2, learn_shortcut=False):
+                 pooling=AvgPool2d, down_factor=2, learn_shortcut=False):
         super().__init__(in_channels, out_channels, kernel_size, padding, dilation, groups, bias,
                          padding_mode, weight_norm_type, weight_norm_params,
                          activation_norm_type, activation_norm_params, skip_activation_norm,

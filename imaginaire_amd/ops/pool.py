@@ -1,0 +1,73 @@
+"""NHWC average pooling (k14, ``csrc/pool.hip``) with a gather backward.
+
+``avg_pool2d`` / ``AvgPool2d`` are drop-ins for ``F.avg_pool2d`` / ``nn.AvgPool2d`` (no
+parameters, identical state dicts). Packed channels-last bf16 / fp32 activations with a
+channel count divisible by 8 run the HIP kernels; anything else (CPU, NCHW, ``ceil_mode``,
+``divisor_override``) falls back to PyTorch.
+"""
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from imaginaire_amd.ops import _ext
+
+
+def _pair(v):
+    return (int(v), int(v)) if not isinstance(v, (tuple, list)) else (int(v[0]), int(v[1]))
+
+
+class _AvgPoolNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p, include_pad):
+        ctx.conf = (x.shape[2], x.shape[3], k, s, p, include_pad)
+        return _ext.ext().avg_pool_nhwc_fwd(x, k[0], k[1], s[0], s[1], p[0], p[1], include_pad)
+
+    @staticmethod
+    def backward(ctx, dy):
+        h, w, k, s, p, include_pad = ctx.conf
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = _ext.ext().avg_pool_nhwc_bwd(dy, h, w, k[0], k[1], s[0], s[1], p[0], p[1],
+                                          include_pad)
+        return dx, None, None, None, None
+
+
+def avg_pool2d(x, kernel_size, stride=None, padding=0, ceil_mode=False, count_include_pad=True,
+               divisor_override=None):
+    k = _pair(kernel_size)
+    s = _pair(stride if stride is not None else kernel_size)
+    p = _pair(padding)
+    if x.is_cuda and x.dim() == 4 and not ceil_mode and divisor_override is None and \
+            x.dtype in (torch.bfloat16, torch.float32) and x.shape[1] % 8 == 0 and \
+            x.is_contiguous(memory_format=torch.channels_last) and _ext.use_native(x) and \
+            2 * p[0] <= k[0] and 2 * p[1] <= k[1] and \
+            x.shape[2] + 2 * p[0] >= k[0] and x.shape[3] + 2 * p[1] >= k[1]:
+        y = _AvgPoolNHWC.apply(x, k, s, p, bool(count_include_pad))
+    else:
+        y = F.avg_pool2d(x, kernel_size, stride, padding, ceil_mode, count_include_pad,
+                         divisor_override)
+    valid = getattr(x, '_iamd_valid_channels', None)
+    if valid is not None:  # pooling acts per channel: a zero channel tail stays zero
+        y._iamd_valid_channels = valid
+    return y
+
+
+class AvgPool2d(nn.Module):
+    """Drop-in for ``nn.AvgPool2d`` running k14 on NHWC activations."""
+
+    def __init__(self, kernel_size, stride=None, padding=0, ceil_mode=False,
+                 count_include_pad=True, divisor_override=None):
+        super().__init__()
+        self.kernel_size = kernel_size
+        self.stride = stride if stride is not None else kernel_size
+        self.padding = padding
+        self.ceil_mode = ceil_mode
+        self.count_include_pad = count_include_pad
+        self.divisor_override = divisor_override
+
+    def forward(self, x):
+        return avg_pool2d(x, self.kernel_size, self.stride, self.padding, self.ceil_mode,
+                          self.count_include_pad, self.divisor_override)
+
+    def extra_repr(self):
+        return 'kernel_size={}, stride={}, padding={}'.format(self.kernel_size, self.stride,
+                                                              self.padding)

@@ -936,3 +936,30 @@ def test_flow_warp_backward_modes():
         torch.use_deterministic_algorithms(prev)
     assert torch.equal(grads[0], grads[1])
     torch.testing.assert_close(grads[0], ia.grad, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('cfg', [
+    (2, 2, 0, True), (3, 2, 1, True), (3, 2, 1, False), (3, 1, 1, False), (4, 3, 2, True)])
+def test_avg_pool_nhwc(dtype, cfg):
+    """k14 NHWC average pool (ResDiscriminator 2x2, pix2pixHD/vid2vid 3x3/s2/p1 with and
+    without count_include_pad, odd sizes) forward and gather backward == fp32 F.avg_pool2d on
+    an NCHW copy. (PyTorch-ROCm's own channels-last avg_pool2d backward is wrong for
+    overlapping / padded windows on this stack — 0.82 max error at 3x3/s2/p1 against the CPU
+    and NCHW results, scripts/probe/pool_debug.py — so the reference runs NCHW.)"""
+    from imaginaire_amd.ops.pool import avg_pool2d
+    k, s, p, inc = cfg
+    torch.manual_seed(8)
+    x = torch.randn(2, 24, 19, 26, device='cuda').to(dtype).contiguous(
+        memory_format=torch.channels_last).requires_grad_(True)
+    y = avg_pool2d(x, k, s, p, count_include_pad=inc)
+    xr = x.detach().float().contiguous().requires_grad_(True)
+    yr = F.avg_pool2d(xr, k, s, p, count_include_pad=inc)
+    assert y.shape == yr.shape and y.dtype == dtype
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    g = torch.randn_like(yr)
+    y.backward(g.to(dtype).contiguous(memory_format=torch.channels_last))
+    yr.backward(g)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=tol, rtol=tol)
