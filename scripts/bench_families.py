@@ -64,13 +64,16 @@ def main():
         parts = key.split('.')
         for k in parts[:-1]:
             node = getattr(node, k)
-        try:
-            val = int(val)
-        except ValueError:
+        if val in ('True', 'False'):
+            val = val == 'True'
+        else:
             try:
-                val = float(val)
+                val = int(val)
             except ValueError:
-                pass
+                try:
+                    val = float(val)
+                except ValueError:
+                    pass
         setattr(node, parts[-1], val)
     # the synthetic dataset is constructed directly below; cfg.data.type keeps naming the
     # reference dataset so the batch contract (few-shot keys, video axis) follows it
