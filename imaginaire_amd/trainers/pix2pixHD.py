@@ -29,7 +29,16 @@ class Trainer(SPADETrainer):
                 weights=cfg.trainer.perceptual_loss.weights), loss_weight.perceptual)
 
     def _start_of_iteration(self, data, current_iteration):
-        return self.pre_process(data)
+        data = self.pre_process(data)
+        if self.amp_dtype is not None:
+            # every consumer of the label map and the real image in the training step is a
+            # bf16 conv (G, D, VGG): cast once here instead of at each conv, and halve the
+            # bytes of the reflect pads, D-input concatenations and resizes (the instance map
+            # stays fp32 for the feature encoder's instance pooling)
+            for key in ('label', 'images'):
+                if torch.is_tensor(data.get(key)) and data[key].is_floating_point():
+                    data[key] = data[key].to(self.amp_dtype)
+        return data
 
     def gen_forward(self, data):
         net_G_output = self.net_G(data)
