@@ -133,7 +133,16 @@ class Trainer(BaseTrainer):
             print('------ Now start training %d frames -------' % self.sequence_length)
 
     def _start_of_iteration(self, data, current_iteration):
-        return self.pre_process(data)
+        data = self.pre_process(data)
+        if self.amp_dtype is not None and not self.is_inference:
+            # every network input of the training step (label maps, frames, few-shot
+            # references) feeds bf16 convs: cast once per sequence instead of per conv and
+            # per frame (halves the per-frame concatenations, pads and warps)
+            for key in ('label', 'images', 'few_shot_label', 'few_shot_images'):
+                v = data.get(key)
+                if torch.is_tensor(v) and v.is_floating_point():
+                    data[key] = v.to(self.amp_dtype)
+        return data
 
     def pre_process(self, data):
         data_cfg = self.cfg.data
