@@ -165,22 +165,23 @@ __device__ __forceinline__ int pad_list(int i, int p0, int p1, int n, int mode,
   return cnt;
 }
 
+// grid (ceil(Wo*C/8 / kT), B*Ho): one block row per output image row, 32-bit in-row indices
+// (the flat int64 index with three 64-bit div/mods per 16-byte copy made these kernels
+// ALU-bound at ~1/10 of HBM bandwidth)
 template <typename T>
 __global__ void __launch_bounds__(kT)
 pad_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int B, int C, int H, int W, int Ho,
                int Wo, int pt, int pl, int mode) {
   const int cv = C / 8;
-  const int64_t n = (int64_t)B * Ho * Wo * cv;
-  for (int64_t t = blockIdx.x * (int64_t)kT + threadIdx.x; t < n; t += (int64_t)gridDim.x * kT) {
-    const int c8 = (int)(t % cv);
-    int64_t p = t / cv;
-    const int ox = (int)(p % Wo);
-    p /= Wo;
-    const int oy = (int)(p % Ho);
-    const int b = (int)(p / Ho);
-    const int64_t src = (((int64_t)b * H + pad_src(oy, pt, H, mode)) * W +
-                         pad_src(ox, pl, W, mode)) * C + c8 * 8;
-    *reinterpret_cast<Pack<T, 8>*>(y + t * 8) = *reinterpret_cast<const Pack<T, 8>*>(x + src);
+  const int e = blockIdx.x * kT + threadIdx.x;
+  if (e >= Wo * cv) return;
+  const int ox = e / cv, c8 = e - ox * cv;
+  const int sx = pad_src(ox, pl, W, mode);
+  for (int row = blockIdx.y; row < B * Ho; row += gridDim.y) {  // row = b * Ho + oy
+    const int b = row / Ho, oy = row - b * Ho;
+    const int64_t src = (((int64_t)b * H + pad_src(oy, pt, H, mode)) * W + sx) * C + c8 * 8;
+    *reinterpret_cast<Pack<T, 8>*>(y + ((int64_t)row * Wo + ox) * C + c8 * 8) =
+        *reinterpret_cast<const Pack<T, 8>*>(x + src);
   }
 }
 
@@ -188,18 +189,18 @@ template <typename T>
 __global__ void __launch_bounds__(kT)
 pad_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int B, int C, int H, int W, int Ho,
                int Wo, int pt, int pb, int pl, int pr, int mode) {
+  // grid (ceil(W*C/8 / kT), B*H): one block row per input image row (see pad_fwd_kernel)
   const int cv = C / 8;
-  const int64_t n = (int64_t)B * H * W * cv;
-  for (int64_t t = blockIdx.x * (int64_t)kT + threadIdx.x; t < n; t += (int64_t)gridDim.x * kT) {
-    const int c8 = (int)(t % cv);
-    int64_t p = t / cv;
-    const int ix = (int)(p % W);
-    p /= W;
-    const int iy = (int)(p % H);
-    const int b = (int)(p / H);
-    int ys[kPadMax], xs[kPadMax];
+  const int e = blockIdx.x * kT + threadIdx.x;
+  if (e >= W * cv) return;
+  const int ix = e / cv, c8 = e - ix * cv;
+  int xs[kPadMax];
+  const int nx = pad_list(ix, pl, pr, W, mode, xs);
+  for (int row = blockIdx.y; row < B * H; row += gridDim.y) {  // row = b * H + iy
+    const int b = row / H, iy = row - b * H;
+    const int64_t t = (int64_t)row * W * cv + e;
+    int ys[kPadMax];
     const int ny = pad_list(iy, pt, pb, H, mode, ys);
-    const int nx = pad_list(ix, pl, pr, W, mode, xs);
     float acc[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[k] = 0.f;
@@ -268,6 +269,12 @@ pad_cast_kernel(const TI* __restrict__ x, TO* __restrict__ y, int B, int C, int 
   }
 }
 
+// (in-row blocks, rows): rows beyond the grid's y limit are walked by a grid-stride loop
+dim3 pad_rows_grid(int64_t per_row, int64_t rows) {
+  IAMD_CHECK(per_row < (1ll << 30) && rows < (1ll << 31), "pad_nhwc: tensor too large");
+  return dim3((unsigned)((per_row + kT - 1) / kT), (unsigned)std::min<int64_t>(rows, 65535));
+}
+
 int pad_grid(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + kT - 1) / kT, 65536)); }
 
 }  // namespace
@@ -288,12 +295,12 @@ at::Tensor pad_nhwc_fwd(const at::Tensor& x, int64_t pl, int64_t pr, int64_t pt,
   const int64_t n = (int64_t)B * Ho * Wo * (C / 8);
   if (n == 0) return y;
   if (x.scalar_type() == at::kBFloat16)
-    hipLaunchKernelGGL(pad_fwd_kernel<__hip_bfloat16>, dim3(pad_grid(n)), dim3(kT), 0, stream(),
+    hipLaunchKernelGGL(pad_fwd_kernel<__hip_bfloat16>, pad_rows_grid(Wo * (C / 8), B * Ho), dim3(kT), 0, stream(),
                        reinterpret_cast<const __hip_bfloat16*>(x.data_ptr()),
                        reinterpret_cast<__hip_bfloat16*>(y.data_ptr()), B, C, H, W, Ho, Wo,
                        (int)pt, (int)pl, (int)mode);
   else
-    hipLaunchKernelGGL(pad_fwd_kernel<float>, dim3(pad_grid(n)), dim3(kT), 0, stream(),
+    hipLaunchKernelGGL(pad_fwd_kernel<float>, pad_rows_grid(Wo * (C / 8), B * Ho), dim3(kT), 0, stream(),
                        x.data_ptr<float>(), y.data_ptr<float>(), B, C, H, W, Ho, Wo, (int)pt,
                        (int)pl, (int)mode);
   IAMD_LAUNCH_CHECK();
@@ -312,13 +319,13 @@ at::Tensor pad_nhwc_bwd(const at::Tensor& dy, int64_t H, int64_t W, int64_t pl, 
   const int64_t n = (int64_t)B * H * W * (C / 8);
   if (n == 0) return dx;
   if (dy.scalar_type() == at::kBFloat16)
-    hipLaunchKernelGGL(pad_bwd_kernel<__hip_bfloat16>, dim3(pad_grid(n)), dim3(kT), 0, stream(),
+    hipLaunchKernelGGL(pad_bwd_kernel<__hip_bfloat16>, pad_rows_grid(W * (C / 8), B * H), dim3(kT), 0, stream(),
                        reinterpret_cast<const __hip_bfloat16*>(dy.data_ptr()),
                        reinterpret_cast<__hip_bfloat16*>(dx.data_ptr()), B, C, (int)H, (int)W,
                        (int)dy.size(2), (int)dy.size(3), (int)pt, (int)pb, (int)pl, (int)pr,
                        (int)mode);
   else
-    hipLaunchKernelGGL(pad_bwd_kernel<float>, dim3(pad_grid(n)), dim3(kT), 0, stream(),
+    hipLaunchKernelGGL(pad_bwd_kernel<float>, pad_rows_grid(W * (C / 8), B * H), dim3(kT), 0, stream(),
                        dy.data_ptr<float>(), dx.data_ptr<float>(), B, C, (int)H, (int)W,
                        (int)dy.size(2), (int)dy.size(3), (int)pt, (int)pb, (int)pl, (int)pr,
                        (int)mode);
