@@ -8,7 +8,9 @@ exercise). Set ``IMAGINAIRE_AMD_EAGER=1`` to force the reference path on GPU
 (used only by the self-baseline benchmark and numerics tests).
 """
 import importlib
+import contextlib
 import os
+import threading
 
 import torch
 
@@ -69,8 +71,30 @@ def available():
     return load() is not None
 
 
+_SCOPE = threading.local()
+
+
 def force_eager():
-    return os.environ.get('IMAGINAIRE_AMD_EAGER', '0') == '1'
+    return os.environ.get('IMAGINAIRE_AMD_EAGER', '0') == '1' or \
+        getattr(_SCOPE, 'depth', 0) > 0
+
+
+@contextlib.contextmanager
+def eager_scope(enabled=True):
+    """Route every op dispatched inside the block to its plain PyTorch path.
+
+    The HIP kernels' autograd Functions are first-order only (their backwards call raw
+    kernels), so a forward whose gradient is itself differentiated -- the gradient
+    penalty's ``autograd.grad(..., create_graph=True)`` -- must run on PyTorch ops, or the
+    penalty's dependence on the weights is silently dropped."""
+    if not enabled:
+        yield
+        return
+    _SCOPE.depth = getattr(_SCOPE, 'depth', 0) + 1
+    try:
+        yield
+    finally:
+        _SCOPE.depth -= 1
 
 
 def use_native(t):

@@ -10,6 +10,7 @@ import torch
 from imaginaire_amd.evaluation import compute_fid
 from imaginaire_amd.losses import GANLoss, GaussianKLLoss, PerceptualLoss
 from imaginaire_amd.losses.gp import GradientPenaltyLoss
+from imaginaire_amd.ops import _ext
 from imaginaire_amd.trainers.base import BaseTrainer
 from imaginaire_amd.utils.distributed import master_only_print as print
 from imaginaire_amd.utils.meters import Meter
@@ -119,8 +120,11 @@ class Trainer(BaseTrainer):
             gp = self.criteria['gp']
             images_a_gp = gp.get_dis_inputs(data['images_a'], out['images_ba'])
             images_b_gp = gp.get_dis_inputs(data['images_b'], out['images_ab'])
-            dout_gp = self.net_D(data, dict(images_ab=images_b_gp, images_ba=images_a_gp),
-                                 real=False)
+            # the penalty differentiates D's input gradient: D runs on twice-differentiable
+            # PyTorch ops here (the HIP kernels' autograd Functions are first-order only)
+            with _ext.eager_scope():
+                dout_gp = self.net_D(data, dict(images_ab=images_b_gp, images_ba=images_a_gp),
+                                     real=False)
             self.dis_losses['gp_a'] = gp(images_a_gp, dout_gp['out_ba'])
             self.dis_losses['gp_b'] = gp(images_b_gp, dout_gp['out_ab'])
             self.dis_losses['gp'] = self.dis_losses['gp_a'] + self.dis_losses['gp_b']

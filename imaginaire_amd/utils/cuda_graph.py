@@ -175,7 +175,7 @@ class GraphedStep(object):
         return None
 
 
-def make_trainer_step(trainer, warmup=None, enabled=True):
+def make_trainer_step(trainer, warmup=None, enabled=True, force=False):
     """The steady-state iteration of an image trainer: ``dis_step`` D updates then
     ``gen_step`` G updates (reference train.py:72-84), as a GraphedStep when supported
     (``trainer.graph_capturable`` and :func:`graph_supported`). Returns (callable, graph or
@@ -190,7 +190,9 @@ def make_trainer_step(trainer, warmup=None, enabled=True):
         for _ in range(cfg.trainer.gen_step):
             trainer.gen_update(data)
 
-    if not (enabled and getattr(trainer, 'graph_capturable', False) and
+    # force: try any trainer (the capture falls back to eager on failure); used by
+    # scripts/bench_families.py --graph to evaluate families not yet marked capturable
+    if not (enabled and (force or getattr(trainer, 'graph_capturable', False)) and
             graph_supported(trainer)):
         return step, None
 

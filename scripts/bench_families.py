@@ -37,6 +37,8 @@ def main():
     p.add_argument('--op-sites', action='store_true',
                    help='after the timed steps, attribute the aten glue of one more iteration '
                         'to Python call sites (scripts/probe/op_sites.py) on stderr')
+    p.add_argument('--graph', action='store_true',
+                   help='replay the steady-state iteration from a captured hipGraph (any family)')
     p.add_argument('--conv-log', action='store_true',
                    help='after the timed steps, time every conv kernel call of one more '
                         'iteration and print time / TF/s per (kind, shape, kernel) to stderr')
@@ -120,13 +122,24 @@ def main():
             return [fresh(v) for v in x]
         return x
 
+    graphed = None
+    if args.graph:
+        from imaginaire_amd.utils.cuda_graph import make_trainer_step
+        cfg.speed_benchmark = False
+        trainer.speed_benchmark = False
+        train_step, graphed = make_trainer_step(trainer, warmup=max(1, args.warmup - 1),
+                                                force=True)
+    else:
+        def train_step(data):
+            for _ in range(cfg.trainer.dis_step):
+                trainer.dis_update(data)
+            for _ in range(cfg.trainer.gen_step):
+                trainer.gen_update(data)
+
     def step(it):
         data = fresh(pool[it % len(pool)])
         data = trainer.start_of_iteration(data, it)
-        for _ in range(cfg.trainer.dis_step):
-            trainer.dis_update(data)
-        for _ in range(cfg.trainer.gen_step):
-            trainer.gen_update(data)
+        train_step(data)
         return data
 
     def sync():
@@ -178,7 +191,10 @@ def main():
         'device': torch.cuda.get_device_name(0) if device.type == 'cuda' else 'cpu',
         'data': 'synthetic, random-init weights',
         'peak_mem_gb': round(torch.cuda.max_memory_allocated() / 2 ** 30, 2)
-        if device.type == 'cuda' else None}), flush=True)
+        if device.type == 'cuda' else None,
+        'hipgraph': bool(graphed is not None and graphed.graph is not None),
+        'losses': {k: round(float(v), 5) for k, v in trainer.gen_losses.items()
+                   if torch.is_tensor(v) and v.numel() == 1}}), flush=True)
 
 
 if __name__ == '__main__':
