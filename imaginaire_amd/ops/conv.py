@@ -218,7 +218,10 @@ def mfma_eligible(x, w, stride, padding, dilation, groups):
     # zero-padded channels cost MFMA work: allow ≤ 1/3 waste, except for the thin RGB-facing
     # convs (3-channel image in / out) where MIOpen's kernels run at ~1 TF/s and a 64-channel
     # padded MFMA tile is still an order of magnitude faster (profiles/spade_step_k10_k11)
-    if cp * op * 3 > cin * cout * 4 and min(cin, cout) > 16:
+    # up to 2x padding waste still runs k10 for the 32-channel full-resolution layers of the
+    # video models (MIOpen's NHWC bf16 solvers reach only 35-150 TF/s on [2, 32, 512, 1024]
+    # 1x1 / 3x3 convs, profiles/recipe_vid2vid512x1024_conv_log_mi355x.txt)
+    if cp * op * 3 > cin * cout * 4 and min(cin, cout) > 16 and cp * op > 2 * cin * cout:
         return False
     ho, wo = _out_hw(x.shape[2], x.shape[3], w.shape[2:], stride, padding, dilation)
     if ho <= 0 or wo <= 0:
@@ -230,7 +233,9 @@ def mfma_eligible(x, w, stride, padding, dilation, groups):
     blocks = -(-x.shape[0] * ho * wo // 128) * max(1, op // (128 if op % 128 == 0 else 64))
     # deterministic mode: tiny grids run k10 too (its split-K sums slabs in a fixed order);
     # MIOpen's immediate-mode solvers for them may split K with atomics
-    return blocks >= _MFMA_MIN_BLOCKS or torch.are_deterministic_algorithms_enabled()
+    # narrow outputs (flow / mask heads, FlowNet2's predict_flow on 1/64-scale maps): MIOpen
+    # takes ~0.65 ms for a [2, 1056, 16, 32] -> 2-channel 3x3 conv; k10 splits K over the grid
+    return blocks >= _MFMA_MIN_BLOCKS or cout <= 8 or torch.are_deterministic_algorithms_enabled()
 
 
 def _flip_t(w):
@@ -255,7 +260,7 @@ _STRIDED_DGRAD = os.environ.get('IMAGINAIRE_AMD_STRIDED_DGRAD', '1') == '1'
 _STRIDED_DGRAD_MIN_PIX = int(os.environ.get('IMAGINAIRE_AMD_STRIDED_DGRAD_MIN_PIX', 131072))
 
 
-def _strided_dgrad(dy, wb, H, W, s, padding):
+def _strided_dgrad(dy, wb, H, W, s, padding, wts=None):
     """Data gradient of a stride-``s`` conv (weight ``wb`` [Cout, Cin, KH, KW], channels-last
     bf16) as s*s stride-1 phase convolutions on k10. Input row i = s*q + r receives
     dy[q + c0 - j] * w[kh0 + s*j] for kh0 = (r + p) mod s, c0 = (r + p - kh0) / s: a J-tap
@@ -285,7 +290,7 @@ def _strided_dgrad(dy, wb, H, W, s, padding):
         cy, cx = (ry + ph - ky0) // s, (rx + pw - kx0) // s
         py = max(0, jy - 1 - cy, qy + cy - ho)
         px = max(0, jx - 1 - cx, qx + cx - wo)
-        wt = X.conv_weight_flip_t(wb, s, ky0, kx0, 1)
+        wt = wts[(ry, rx)] if wts is not None else X.conv_weight_flip_t(wb, s, ky0, kx0, 1)
         out = X.conv2d_mfma(dy, wt, None, 1, 1, py, px, 1, 1, 1.0, 1)
         X.conv_phase_scatter(out, dx, s, ry, rx, cy - (jy - 1) + py, cx - (jx - 1) + px, qy, qx)
     return dx
@@ -646,11 +651,110 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1,
             weight = _pad_channels(weight, cp)
         x = nhwc(x)
         weight = nhwc(weight)
+        if _CONV_LOG is not None and weight.dim() == 4:
+            ho, wo = _out_hw(x.shape[2], x.shape[3], weight.shape[2:], st, pd, dl)
+            with _Logged('fwd', 'miopen', 2.0 * x.shape[0] * ho * wo * weight.numel(),
+                         _gemm_desc(x, weight, st, pd)):
+                return F.conv2d(x, weight, bias, stride, padding, dilation, groups)
     return F.conv2d(x, weight, bias, stride, padding, dilation, groups)
+
+
+_DECONV_MIN_PIX = int(os.environ.get('IMAGINAIRE_AMD_DECONV_MIN_PIX', 4096))
+_DECONV_CHOICE = {}
+_DECONV_WEIGHTS = {}
+_DECONV_FORCE = os.environ.get('IMAGINAIRE_AMD_DECONV')  # 'k10s' / 'miopen': skip the tuning
+
+
+def deconv_eligible(x, weight, stride, padding, output_padding, groups, dilation):
+    """The phase-convolution path of :func:`conv_transpose2d`: inference (no autograd graph),
+    bf16, square stride 2-4, no dilation / output padding / groups, >= 16 channels each side
+    and an output map that is not tiny."""
+    if not (x.is_cuda and x.dim() == 4 and weight.dim() == 4 and groups == 1 and
+            _STRIDED_DGRAD and _mfma_enabled() and _ext.use_native(x)):
+        return False
+    if torch.is_grad_enabled() and (x.requires_grad or weight.requires_grad):
+        return False
+    s, op, dl = stride, output_padding, dilation
+    if not (s[0] == s[1] and 2 <= s[0] <= 4 and op == (0, 0) and dl == (1, 1)):
+        return False
+    if _compute_dtype(x, weight) != torch.bfloat16:
+        return False
+    cin, cout, kh, kw = weight.shape
+    if min(cin, cout) < 16 or kh < s[0] or kw < s[1]:
+        return False
+    ho = (x.shape[2] - 1) * s[0] - 2 * padding[0] + kh
+    wo = (x.shape[3] - 1) * s[1] - 2 * padding[1] + kw
+    return ho > 0 and wo > 0 and x.shape[0] * ho * wo >= _DECONV_MIN_PIX
+
+
+def _deconv_phase_weights(weight, s, padding, cp, op):
+    """The s*s flipped phase sub-kernels of a (frozen) transposed-conv weight, cached on the
+    weight's storage and version counter (FlowNet2's decoders never change)."""
+    cache = isinstance(weight, torch.nn.Parameter)  # a temporary's address can be reused
+    key = (weight.data_ptr(), weight._version, tuple(weight.shape), s, padding)
+    hit = _DECONV_WEIGHTS.get(key) if cache else None
+    if hit is None:
+        wb = _pad_rows(_pad_channels(weight.detach(), op, torch.bfloat16), cp)
+        hit = {}
+        for ry in range(s):
+            for rx in range(s):
+                hit[(ry, rx)] = _ext.ext().conv_weight_flip_t(
+                    wb, s, (ry + padding[0]) % s, (rx + padding[1]) % s, 1)
+        hit = (wb, hit)
+        if cache:
+            if len(_DECONV_WEIGHTS) > 256:
+                _DECONV_WEIGHTS.clear()
+            _DECONV_WEIGHTS[key] = hit
+    return hit
 
 
 def conv_transpose2d(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1,
                      dilation=1):
+    """``F.conv_transpose2d``. A strided transposed conv is the data gradient of the strided
+    conv with the same weight ([Cin_t, Cout_t, KH, KW] read as [Cout, Cin, KH, KW]), so on
+    eligible inference calls (FlowNet2's 4x4 / stride-2 decoders) it runs as the s*s k10
+    phase convolutions of :func:`_strided_dgrad` instead of MIOpen's backward-data solvers."""
+    st, pd = _pair(stride), _pair(padding)
+    if deconv_eligible(x, weight, st, pd, _pair(output_padding), groups, _pair(dilation)):
+        cin, cout, kh, kw = weight.shape
+        cp, op = _round_up(cin, 64), _out_pad(cout)
+        ho = (x.shape[2] - 1) * st[0] - 2 * pd[0] + kh
+        wo = (x.shape[3] - 1) * st[1] - 2 * pd[1] + kw
+        xn, wn = nhwc(x), nhwc(weight)
+
+        def phase():
+            wb, wts = _deconv_phase_weights(weight, st[0], pd, cp, op)
+            y = _strided_dgrad(_pad_channels(x, cp, torch.bfloat16), wb, ho, wo, st[0], pd,
+                               wts)
+            y = y[:, :cout] if op != cout else y
+            return y if bias is None else y + bias.to(y.dtype).view(1, -1, 1, 1)
+
+        def miopen():
+            return F.conv_transpose2d(xn, wn, bias, st, pd)
+
+        # per-shape choice: MIOpen's backward-data solvers range from ~20 to ~140 TF/s over
+        # FlowNet2's decoder shapes, the phase path from ~40 to ~100
+        # (profiles/deconv_probe_mi355x.txt)
+        key = (tuple(x.shape), tuple(weight.shape), st, pd)
+        choice = _DECONV_FORCE or _DECONV_CHOICE.get(key)
+        if choice is None and torch.cuda.is_current_stream_capturing():
+            choice = 'miopen'
+        if choice is None:
+            times = {}
+            for name, fn in (('k10s', phase), ('miopen', miopen)):
+                fn()
+                start, end = torch.cuda.Event(enable_timing=True), \
+                    torch.cuda.Event(enable_timing=True)
+                start.record()
+                for _ in range(3):
+                    fn()
+                end.record()
+                end.synchronize()
+                times[name] = start.elapsed_time(end)
+            choice = _DECONV_CHOICE[key] = min(times, key=times.get)
+        fl = 2.0 * x.shape[0] * x.shape[2] * x.shape[3] * weight.numel()
+        with _Logged('deconv', choice, fl, _gemm_desc(x, weight, st, pd)):
+            return phase() if choice == 'k10s' else miopen()
     if x.is_cuda:
         x = nhwc(x)
         weight = nhwc(weight)

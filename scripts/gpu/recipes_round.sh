@@ -31,10 +31,11 @@ run() {  # name, timeout, args...
     head -25 gpurun_out/recipes/${name}_kernels.txt
   fi
 }
-# MUNIT afhq_dog2cat ampO1 recipe: 256x256, batch 16
+# MUNIT afhq_dog2cat ampO1 recipe: 256x256, batch 16 (gp 0 and consistency_reg 0, as the recipe)
 run munit256 400 --config configs/unit_test/munit.yaml --steps 5 --warmup 2 --set \
   gen.num_filters=64 gen.num_filters_mlp=256 gen.num_res_blocks=4 \
   dis.num_filters=32 dis.max_num_filters=512 dis.num_layers=6 trainer.loss_weight.perceptual=0 \
+  trainer.loss_weight.gp=0 trainer.loss_weight.consistency_reg=0 \
   data.train.batch_size=16 data.train.augmentations.random_crop_h_w=256,256
 # vid2vid cityscapes ampO1 recipe: 512x1024, batch 2, 3-frame sequences, FlowNet2 flow loss
 run vid2vid512x1024 600 --config configs/unit_test/vid2vid_street.yaml --steps 3 --warmup 2 \

@@ -324,6 +324,10 @@ _CONV_CASES = [
     (1, 128, 64, 9, 14, 1, 2, 0, 1),        # 1x1 s2: three phases receive no taps (zeros)
     (1, 64, 128, 11, 13, 5, 2, 2, 1),       # 5x5 s2
     (2, 256, 128, 8, 16, 4, 2, 1, 1),       # PatchGAN 4x4 s2 at a small map
+    # video-model shapes routed to k10 by the relaxed eligibility rules
+    (2, 1026, 2, 4, 8, 3, 1, 1, 1),         # predict_flow on a 1/64 map: tiny grid, split K
+    (1, 32, 128, 16, 24, 1, 1, 0, 1),       # 32-channel 1x1: Cin padded 32 -> 64 (2x waste)
+    (1, 32, 64, 16, 24, 3, 2, 1, 1),        # 32-channel 3x3 s2
 ]
 
 
@@ -963,3 +967,47 @@ def test_avg_pool_nhwc(dtype, cfg):
     y.backward(g.to(dtype).contiguous(memory_format=torch.channels_last))
     yr.backward(g)
     torch.testing.assert_close(x.grad.float(), xr.grad, atol=tol, rtol=tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('shape', [(2, 194, 32, 128, 256), (1, 162, 16, 256, 512),
+                                   (1, 130, 64, 64, 128)])
+def test_conv_transpose_phase_path(shape):
+    """Inference transposed conv (4x4 / s2 / p1) as k10 phase convolutions (ops.conv) vs
+    the fp32 PyTorch transposed conv; the FlowNet2 decoder shapes."""
+    from imaginaire_amd.ops import conv as C
+    b, cin, cout, h, w = shape
+    torch.manual_seed(0)
+    x = torch.randn(b, cin, h, w, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    wt = (torch.randn(cin, cout, 4, 4, device='cuda') / (cin * 4) ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(cout, device='cuda').to(torch.bfloat16)
+    ref = F.conv_transpose2d(x.float(), wt.float(), bias.float(), 2, 1)
+    saved = C._DECONV_MIN_PIX, C._DECONV_FORCE
+    C._DECONV_MIN_PIX = 0
+    try:
+        assert C.deconv_eligible(x, wt, (2, 2), (1, 1), (0, 0), 1, (1, 1))
+        for force in ('k10s', None):  # the phase path, then the tuned choice
+            C._DECONV_FORCE = force
+            for wgt in (wt, torch.nn.Parameter(wt, requires_grad=False)):  # uncached, cached
+                with torch.no_grad():
+                    y = C.conv_transpose2d(x, wgt, bias, 2, 1)
+                assert y.shape == ref.shape
+                err = (y.float() - ref).abs().max() / ref.abs().max()
+                assert err < 2e-2, (force, float(err))
+    finally:
+        C._DECONV_MIN_PIX, C._DECONV_FORCE = saved
+
+
+@pytest.mark.gpu
+def test_flownet_predict_flow_native():
+    from imaginaire_amd.third_party.flow_net.flownet2.networks.submodules import predict_flow
+    torch.manual_seed(0)
+    m = predict_flow(194).cuda().to(torch.bfloat16)
+    x = torch.randn(2, 194, 128, 256, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    with torch.no_grad():
+        y = m(x)
+    ref = F.conv2d(x.float(), m.weight.float(), m.bias.float(), 1, 1)
+    err = (y.float() - ref).abs().max() / ref.abs().max()
+    assert err < 2e-2, float(err)
