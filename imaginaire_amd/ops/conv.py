@@ -661,7 +661,6 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1,
 
 _DECONV_MIN_PIX = int(os.environ.get('IMAGINAIRE_AMD_DECONV_MIN_PIX', 4096))
 _DECONV_CHOICE = {}
-_DECONV_WEIGHTS = {}
 _DECONV_FORCE = os.environ.get('IMAGINAIRE_AMD_DECONV')  # 'k10s' / 'miopen': skip the tuning
 
 
@@ -688,24 +687,22 @@ def deconv_eligible(x, weight, stride, padding, output_padding, groups, dilation
 
 
 def _deconv_phase_weights(weight, s, padding, cp, op):
-    """The s*s flipped phase sub-kernels of a (frozen) transposed-conv weight, cached on the
-    weight's storage and version counter (FlowNet2's decoders never change)."""
-    cache = isinstance(weight, torch.nn.Parameter)  # a temporary's address can be reused
-    key = (weight.data_ptr(), weight._version, tuple(weight.shape), s, padding)
-    hit = _DECONV_WEIGHTS.get(key) if cache else None
-    if hit is None:
-        wb = _pad_rows(_pad_channels(weight.detach(), op, torch.bfloat16), cp)
-        hit = {}
-        for ry in range(s):
-            for rx in range(s):
-                hit[(ry, rx)] = _ext.ext().conv_weight_flip_t(
-                    wb, s, (ry + padding[0]) % s, (rx + padding[1]) % s, 1)
-        hit = (wb, hit)
-        if cache:
-            if len(_DECONV_WEIGHTS) > 256:
-                _DECONV_WEIGHTS.clear()
-            _DECONV_WEIGHTS[key] = hit
-    return hit
+    """The s*s flipped phase sub-kernels of a transposed-conv weight. For a Parameter (FlowNet2's
+    frozen decoders) they are cached on the Parameter itself, keyed on its storage and version
+    counter, so the cache dies with the weight and an in-place update invalidates it."""
+    key = (weight.data_ptr(), weight._version, s, tuple(padding), cp, op)
+    cached = getattr(weight, '_iamd_deconv', None)
+    if cached is not None and cached[0] == key:
+        return cached[1]
+    wb = _pad_rows(_pad_channels(weight.detach(), op, torch.bfloat16), cp)
+    wts = {}
+    for ry in range(s):
+        for rx in range(s):
+            wts[(ry, rx)] = _ext.ext().conv_weight_flip_t(
+                wb, s, (ry + padding[0]) % s, (rx + padding[1]) % s, 1)
+    if isinstance(weight, torch.nn.Parameter):
+        weight._iamd_deconv = (key, (wb, wts))
+    return wb, wts
 
 
 def conv_transpose2d(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1,

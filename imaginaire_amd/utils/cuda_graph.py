@@ -126,6 +126,13 @@ class GraphedStep(object):
             # remember the stream they were created on
             if self.stream is None:
                 self.stream = torch.cuda.Stream()
+                # parameters' AccumulateGrad nodes made by earlier default-stream iterations
+                # meet the side stream here: a one-off stream sync during warm-up, not a
+                # problem for the captured replay (no autograd engine runs there)
+                _quiet = getattr(torch.autograd.graph,
+                                 'set_warn_on_accumulate_grad_stream_mismatch', None)
+                if _quiet is not None:
+                    _quiet(False)
             self.stream.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(self.stream):
                 self.step_fn(data)

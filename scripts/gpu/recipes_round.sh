@@ -9,7 +9,8 @@ mkdir -p gpurun_out/recipes
 : > gpurun_out/recipes/recipes.jsonl
 run() {  # name, timeout, args...
   local name=$1 t=$2; shift 2
-  timeout -k 10 "$t" python scripts/bench_families.py "$@" --conv-log \
+  if [ -n "$ONLY" ] && [[ " $ONLY " != *" $name "* ]]; then return 0; fi
+  timeout -k 10 "$t" python scripts/bench_families.py "$@" --conv-log $EXTRA \
     >> gpurun_out/recipes/recipes.jsonl 2> gpurun_out/recipes/$name.err
   local rc=$?
   echo "[recipes] $name rc=$rc"; tail -1 gpurun_out/recipes/recipes.jsonl
