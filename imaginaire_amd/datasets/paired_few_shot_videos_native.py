@@ -3,9 +3,10 @@ datasets/paired_few_shot_videos_native.py:18-226): each entry is an mp4;
 two frames (random, or first/last with ``first_last_only``) become the
 driving and source images.
 
-Video decoding uses the first available backend (torchvision.io, imageio,
-PyAV); none ships with this stack, so the dataset raises a clear error at
-decode time if none is installed.
+Motion-JPEG clips are demuxed and decoded natively (``datasets/mp4.py``: ISO-BMFF sample
+tables + PIL JPEG decode); other codecs (H.264 / HEVC) use the first available optional
+backend (torchvision.io, imageio, PyAV) — none ships with this stack, so such clips raise an
+error naming the codec.
 """
 import copy
 import io
@@ -17,11 +18,19 @@ import numpy as np
 import torch
 from PIL import Image
 
+from imaginaire_amd.datasets import mp4
 from imaginaire_amd.datasets.base import BaseDataset
 
 
 def read_video_frames(buf):
     """mp4 bytes -> uint8 [T, H, W, 3] numpy array."""
+    codec = None
+    try:
+        codec = mp4.parse_video_track(buf)['codec']
+    except ValueError:
+        pass  # not an ISO-BMFF file the demuxer understands: leave it to the backends
+    if codec in mp4.MJPEG_CODECS:
+        return mp4.decode_mjpeg_mp4(buf)
     try:
         import torchvision.io as tvio
         with tempfile.NamedTemporaryFile(suffix='.mp4') as f:
@@ -41,8 +50,10 @@ def read_video_frames(buf):
         with av.open(io.BytesIO(buf)) as c:
             return np.stack([fr.to_ndarray(format='rgb24') for fr in c.decode(video=0)])
     except ImportError:
-        raise RuntimeError('paired_few_shot_videos_native needs a video decoder '
-                           '(torchvision.io, imageio or av); none is installed')
+        raise RuntimeError('paired_few_shot_videos_native: the %s clip needs a video decoder '
+                           '(torchvision.io, imageio or av; none is installed) or Motion-JPEG '
+                           'encoding' % (repr(codec.decode('latin-1')) if codec else
+                                         'non-mp4'))
 
 
 class Dataset(BaseDataset):
