@@ -433,7 +433,9 @@ class HyperSpatiallyAdaptiveNorm(nn.Module):
             else:
                 gb = self.mlps[i](label_map, conv_weights=norm_weights)
             if mask is not None:
-                gb = gb * (1 - mask)
+                # the mask (fp32 from the flow branch) must not promote the 2C-channel
+                # modulation maps (and everything after them) to fp32
+                gb = gb * (1 - mask.to(gb.dtype))
             gbs.append(gb)
         if len(gbs) == 0:
             return fused_norm_or_none(self.norm, x, act_slope=act_slope)

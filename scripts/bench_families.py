@@ -159,7 +159,9 @@ def main():
     if args.op_sites and device.type == 'cuda':
         sys.path.insert(0, os.path.join(HERE, 'probe'))
         from op_sites import record_sites
-        record_sites(lambda: step(args.warmup + args.steps + 1), out=sys.stderr)
+        record_sites(lambda: step(args.warmup + args.steps + 1), out=sys.stderr,
+                     **({'ops': os.environ['OP_SITES_OPS']} if 'OP_SITES_OPS' in os.environ
+                        else {}))
     if args.conv_log and device.type == 'cuda':
         from imaginaire_amd.ops import conv as conv_ops
         conv_ops.enable_conv_log(True)

@@ -61,7 +61,7 @@ def record_sites(step_fn, ops=DEFAULT_OPS, top=60, out=sys.stdout):
     lock = threading.Lock()
 
     def site():
-        fr = [f for f in traceback.extract_stack()[:-3]
+        fr = [f for f in traceback.extract_stack()
               if HERE in f.filename and 'op_sites' not in f.filename]
         return ' <- '.join('%s:%d' % (os.path.relpath(f.filename, HERE), f.lineno)
                            for f in reversed(fr[-3:])) or '<backward/engine>'
@@ -70,7 +70,10 @@ def record_sites(step_fn, ops=DEFAULT_OPS, top=60, out=sys.stdout):
         def __torch_dispatch__(self, func, types, args=(), kwargs=None):
             out_ = func(*args, **(kwargs or {}))
             name = func.__name__.split('.')[0]
-            if name in wanted:
+            # '@fp32': every op (any name) whose output is a large fp32 tensor (>= 2M elements):
+            # finds the forward producers of fp32 activations in a bf16 step
+            if ('@fp32' in wanted and torch.is_tensor(out_) and out_.dtype == torch.float32 and
+                    out_.numel() >= (1 << 21)) or name in wanted:
                 t = out_ if torch.is_tensor(out_) else (args[0] if args and torch.is_tensor(
                     args[0]) else None)
                 nbytes = t.numel() * t.element_size() if t is not None else 0
