@@ -209,9 +209,8 @@ def fused_norm_or_none(norm, x, gamma=None, beta=None, gb=None, act_slope=1.0):
     if isinstance(norm, _FusedNormBase):
         return norm.fused(x, gamma=gamma, beta=beta, gb=gb, act_slope=act_slope)
     y = norm(x)
-    C = x.shape[1]
     if gb is not None:
-        gamma, beta = gb[:, :C], gb[:, C:]
+        gamma, beta = gb.chunk(2, dim=1)
     if gamma is not None:
         if gamma.dim() == 2:
             gamma, beta = gamma[:, :, None, None], beta[:, :, None, None]
@@ -376,9 +375,11 @@ class SpatiallyAdaptiveNorm(nn.Module):
         if len(gbs) == 1:
             return fused_norm_or_none(self.norm, x, gb=gbs[0], act_slope=act_slope)
         out = fused_norm_or_none(self.norm, x, gb=gbs[0], act_slope=1.0)
-        C = self.num_features
         for gb in gbs[1:]:
-            out = out * (1 + gb[:, :C]) + gb[:, C:]
+            # chunk, not two slices: the slices' backward would scatter each half into its own
+            # zero-filled full-size (NCHW) gradient and add them; chunk's is one concatenation
+            g, b = gb.chunk(2, dim=1)
+            out = out * (1 + g) + b
         if act_slope != 1.0:
             out = F.leaky_relu(out, act_slope) if act_slope > 0 else F.relu(out)
         return out
@@ -442,9 +443,11 @@ class HyperSpatiallyAdaptiveNorm(nn.Module):
         if len(gbs) == 1:
             return fused_norm_or_none(self.norm, x, gb=gbs[0], act_slope=act_slope)
         out = fused_norm_or_none(self.norm, x, gb=gbs[0], act_slope=1.0)
-        C = self.num_features
         for gb in gbs[1:]:
-            out = out * (1 + gb[:, :C]) + gb[:, C:]
+            # chunk, not two slices: the slices' backward would scatter each half into its own
+            # zero-filled full-size (NCHW) gradient and add them; chunk's is one concatenation
+            g, b = gb.chunk(2, dim=1)
+            out = out * (1 + g) + b
         if act_slope != 1.0:
             out = F.leaky_relu(out, act_slope) if act_slope > 0 else F.relu(out)
         return out

@@ -426,7 +426,7 @@ class _MfmaConvPerSample(torch.autograd.Function):
             g = g.permute(0, 2, 3, 1).reshape(B, op, kh, kw, cp)[:, :cout, :, :, :cin]
             dw = g.permute(0, 1, 4, 2, 3).to(wdt)
         if ctx.needs_input_grad[2]:
-            db = dy.float().sum((2, 3))[:, :cout].to(bdt)
+            db = dy.sum((2, 3), dtype=torch.float32)[:, :cout].to(bdt)  # no fp32 copy of dy
         return dx, dw, db, None, None
 
 
