@@ -220,6 +220,18 @@ def fused_norm_or_none(norm, x, gamma=None, beta=None, gb=None, act_slope=1.0):
     return y
 
 
+def _modulate_more(out, gbs, act_slope):
+    """Further SPADE modulations ``out·(1+γ_i) + β_i`` (multi-condition SPADE: label map +
+    warped image / flow mask in vid2vid / fs-vid2vid), the last one followed by the activation:
+    each is one pass of the k1 kernel in 'none' (identity-normalisation) mode, forward and
+    backward, with γ|β read straight from the fused γ|β conv output — instead of separate
+    add / mul / add / leaky-relu passes and their backward, plus two slice-gradient scatters."""
+    for i, gb in enumerate(gbs):
+        out = fused_norm_act(out, 'none', gb=gb,
+                             slope=act_slope if i == len(gbs) - 1 else 1.0)
+    return out
+
+
 class AdaptiveNorm(nn.Module):
     """AdaIN / conditional BN: ``norm(x)·(1+γ(y)) + β(y)`` (activation_norm.py:22-106)."""
 
@@ -374,15 +386,8 @@ class SpatiallyAdaptiveNorm(nn.Module):
             return fused_norm_or_none(self.norm, x, act_slope=act_slope)
         if len(gbs) == 1:
             return fused_norm_or_none(self.norm, x, gb=gbs[0], act_slope=act_slope)
-        out = fused_norm_or_none(self.norm, x, gb=gbs[0], act_slope=1.0)
-        for gb in gbs[1:]:
-            # chunk, not two slices: the slices' backward would scatter each half into its own
-            # zero-filled full-size (NCHW) gradient and add them; chunk's is one concatenation
-            g, b = gb.chunk(2, dim=1)
-            out = out * (1 + g) + b
-        if act_slope != 1.0:
-            out = F.leaky_relu(out, act_slope) if act_slope > 0 else F.relu(out)
-        return out
+        return _modulate_more(fused_norm_or_none(self.norm, x, gb=gbs[0], act_slope=1.0),
+                              gbs[1:], act_slope)
 
 
 class HyperSpatiallyAdaptiveNorm(nn.Module):
@@ -442,15 +447,8 @@ class HyperSpatiallyAdaptiveNorm(nn.Module):
             return fused_norm_or_none(self.norm, x, act_slope=act_slope)
         if len(gbs) == 1:
             return fused_norm_or_none(self.norm, x, gb=gbs[0], act_slope=act_slope)
-        out = fused_norm_or_none(self.norm, x, gb=gbs[0], act_slope=1.0)
-        for gb in gbs[1:]:
-            # chunk, not two slices: the slices' backward would scatter each half into its own
-            # zero-filled full-size (NCHW) gradient and add them; chunk's is one concatenation
-            g, b = gb.chunk(2, dim=1)
-            out = out * (1 + g) + b
-        if act_slope != 1.0:
-            out = F.leaky_relu(out, act_slope) if act_slope > 0 else F.relu(out)
-        return out
+        return _modulate_more(fused_norm_or_none(self.norm, x, gb=gbs[0], act_slope=1.0),
+                              gbs[1:], act_slope)
 
 
 class LayerNorm2d(nn.Module):
