@@ -15,6 +15,7 @@ SPADE MI355X specifics (SpatiallyAdaptiveNorm):
   * the nearest-neighbour resize of the label map is cached per resolution
     for the duration of one generator forward (``LabelMapCache``).
 """
+import os
 from types import SimpleNamespace
 
 import torch
@@ -226,10 +227,20 @@ def _modulate_more(out, gbs, act_slope):
     each is one pass of the k1 kernel in 'none' (identity-normalisation) mode, forward and
     backward, with γ|β read straight from the fused γ|β conv output — instead of separate
     add / mul / add / leaky-relu passes and their backward, plus two slice-gradient scatters."""
-    for i, gb in enumerate(gbs):
-        out = fused_norm_act(out, 'none', gb=gb,
-                             slope=act_slope if i == len(gbs) - 1 else 1.0)
+    if _MULTIMOD_FUSED:
+        for i, gb in enumerate(gbs):
+            out = fused_norm_act(out, 'none', gb=gb,
+                                 slope=act_slope if i == len(gbs) - 1 else 1.0)
+        return out
+    for gb in gbs:  # A/B reference path (IMAGINAIRE_AMD_SPADE_MULTIMOD=0)
+        g, b = gb.chunk(2, dim=1)
+        out = out * (1 + g) + b
+    if act_slope != 1.0:
+        out = F.leaky_relu(out, act_slope) if act_slope > 0 else F.relu(out)
     return out
+
+
+_MULTIMOD_FUSED = os.environ.get('IMAGINAIRE_AMD_SPADE_MULTIMOD', '1') == '1'
 
 
 class AdaptiveNorm(nn.Module):
