@@ -679,7 +679,8 @@ def deconv_eligible(x, weight, stride, padding, output_padding, groups, dilation
     if _compute_dtype(x, weight) != torch.bfloat16:
         return False
     cin, cout, kh, kw = weight.shape
-    if min(cin, cout) < 16 or kh < s[0] or kw < s[1]:
+    if min(cin, cout) < 16 or kh < s[0] or kw < s[1] or not (
+            0 <= padding[0] < kh and 0 <= padding[1] < kw):
         return False
     ho = (x.shape[2] - 1) * s[0] - 2 * padding[0] + kh
     wo = (x.shape[3] - 1) * s[1] - 2 * padding[1] + kw
