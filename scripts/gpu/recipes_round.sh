@@ -46,8 +46,9 @@ run vid2vid512x1024 600 --config configs/unit_test/vid2vid_street.yaml --steps 3
   dis.image.max_num_filters=512 dis.temporal.num_filters=64 dis.temporal.max_num_filters=512 \
   data.train.batch_size=2 data.train.augmentations.resize_h_w=512,1024 \
   data.val.augmentations.resize_h_w=512,1024
-# fs_vid2vid faceForensics ampO1 recipe: 512x512, batch 3, 1-shot, 4-frame sequences
-run fsvid2vid512 600 --config configs/unit_test/fs_vid2vid_face.yaml --steps 3 --warmup 2 \
+# fs_vid2vid faceForensics ampO1 recipe: 512x512, batch 3, 1-shot, 4-frame sequences (4 warm-up
+# iterations: with 2, one-off first-time work leaked into the timed ones: 26-40 frames/s)
+run fsvid2vid512 600 --config configs/unit_test/fs_vid2vid_face.yaml --steps 4 --warmup 4 \
   --seq-len 4 --set gen.num_filters=32 gen.num_downsamples=5 gen.hyper.num_hyper_layers=4 \
   gen.hyper.attention.num_filters=32 gen.flow.num_filters=32 gen.flow.max_num_filters=1024 \
   gen.flow.num_res_blocks=6 gen.flow.multi_spade_combine.embed.num_filters=32 \
