@@ -132,15 +132,26 @@ def _parse_video_track(buf):
         samples = []
         s = 0
         for i, (first, per_chunk, _) in enumerate(runs):
+            if i + 1 < len(runs) and runs[i + 1][0] <= first:
+                # chunk runs must start at strictly increasing chunk numbers; a malformed
+                # table could otherwise cost O(runs x chunks) iterations
+                raise ValueError('mp4: stsc run %d does not advance (first chunk %d -> %d)' % (
+                    i, first, runs[i + 1][0]))
             last = runs[i + 1][0] - 1 if i + 1 < len(runs) else len(chunks)
             if first < 1 or last > len(chunks):
                 raise ValueError('mp4: chunk run %d references missing chunks' % i)
+            if per_chunk == 0:
+                continue
             for c in range(first - 1, last):
+                if s == count:
+                    break
                 off = chunks[c]
                 for _ in range(min(per_chunk, count - s)):
                     samples.append((off, sizes[s]))
                     off += sizes[s]
                     s += 1
+            if s == count:
+                break
         if len(samples) != count:
             raise ValueError('mp4: sample table maps %d of %d samples' % (len(samples), count))
         for off, size in samples:

@@ -87,14 +87,15 @@ class PerceptualLoss(nn.Module):
                 loss = loss + weighted_l1([input_features[k] for k in self.layers],
                                           [target_features[k] for k in self.layers],
                                           self.weights)
-                continue
-            for layer, weight in zip(self.layers, self.weights):
-                input_feature = input_features[layer]
-                target_feature = target_features[layer].detach()
-                if self.instance_normalized:
-                    input_feature = F.instance_norm(input_feature)
-                    target_feature = F.instance_norm(target_feature)
-                loss = loss + weight * self.criterion(input_feature, target_feature).float()
+            else:
+                for layer, weight in zip(self.layers, self.weights):
+                    input_feature = input_features[layer]
+                    target_feature = target_features[layer].detach()
+                    if self.instance_normalized:
+                        input_feature = F.instance_norm(input_feature)
+                        target_feature = F.instance_norm(target_feature)
+                    loss = loss + weight * self.criterion(input_feature, target_feature).float()
+            # the next scale sees the half-resolution pair (reference perceptual.py:126-131)
             if scale != self.num_scales - 1:
                 inp = interpolate(inp, mode=self.resize_mode, scale_factor=0.5,
                                     align_corners=False, recompute_scale_factor=True)

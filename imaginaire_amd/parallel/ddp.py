@@ -30,11 +30,14 @@ designed around how the GAN trainers actually use their networks:
   evaluation boundaries), not before every forward;
 * **unused parameters** keep ``grad = None`` (as torch DDP with
   ``find_unused_parameters=True`` leaves them, so Adam skips them instead of
-  decaying their moments on a zero gradient). ``find_unused='local'`` (default)
-  uses this rank's hook arrivals — exact whenever the trainers' control flow
-  is rank-uniform, which it is (it depends on the frame index / phase, never on
-  data). ``find_unused='global'`` all-reduces a used-parameter mask instead
-  (one tiny collective + one host sync per backward, like torch DDP).
+  decaying their moments on a zero gradient). ``find_unused='global'`` (default)
+  all-reduces a used-parameter mask (one tiny collective + one host sync per
+  backward, like torch DDP): a parameter used by ANY rank keeps the reduced
+  gradient on EVERY rank — data-dependent branches such as the vid2vid hand
+  discriminator, skipped when a batch has no hand pixels
+  (model_utils/fs_vid2vid.py crop_hand_from_output), must not let replicas
+  diverge. ``find_unused='local'`` uses this rank's hook arrivals only (no host
+  sync, capturable) and is exact only when the control flow is rank-uniform.
 
 On world size 1 (or no process group) it is a transparent wrapper.
 """
@@ -85,7 +88,7 @@ def _comm_device(group, tensors):
 
 class DistributedDataParallel(nn.Module):
     def __init__(self, module, process_group=None, bucket_cap_mb=256, first_bucket_mb=16,
-                 broadcast_buffers=False, comm_dtype=None, overlap=True, find_unused='local',
+                 broadcast_buffers=False, comm_dtype=None, overlap=True, find_unused='global',
                  **unused):
         super().__init__()
         assert find_unused in ('local', 'global'), find_unused
@@ -268,7 +271,12 @@ class DistributedDataParallel(nn.Module):
         self._drop_unused_grads()
 
     def _drop_unused_grads(self):
-        """grad = None for parameters that received no gradient in this backward."""
+        """grad = None for parameters that received no gradient in this backward.
+
+        'global': a parameter that ANY rank used keeps its (reduced) bucket view on every
+        rank, also where this rank skipped it, so every replica's optimizer applies the same
+        update (torch DDP ``find_unused_parameters=True``); only parameters no rank used get
+        ``grad = None``. 'local' trusts this rank's arrivals (rank-uniform control flow only)."""
         params = [p for p in self._param_list if p.requires_grad]
         if self.find_unused == 'global':
             flags = torch.tensor([1 if p in self._used else 0 for p in params],
@@ -280,6 +288,9 @@ class DistributedDataParallel(nn.Module):
             for p, u in zip(params, used):
                 if not u:
                     p.grad = None
+                elif p.grad is None:
+                    bi, off = self._param_bucket[p]
+                    p.grad = _grad_view(self.buckets[bi].flat, off, p)
             return
         if len(self._used) == len(params):
             return

@@ -135,10 +135,11 @@ class Trainer(BaseTrainer):
     def _start_of_iteration(self, data, current_iteration):
         data = self.pre_process(data)
         if self.amp_dtype is not None and not self.is_inference:
-            # every network input of the training step (label maps, frames, few-shot
-            # references) feeds bf16 convs: cast once per sequence instead of per conv and
-            # per frame (halves the per-frame concatenations, pads and warps)
-            for key in ('label', 'images', 'few_shot_label', 'few_shot_images'):
+            # the label maps feed only bf16 convs: cast once per sequence instead of per conv
+            # and per frame. The real frames stay fp32: they are also the L1 / warp /
+            # perceptual targets and FlowNet2's ground-truth input (reference precision);
+            # autocast casts them where they enter a conv.
+            for key in ('label', 'few_shot_label'):
                 v = data.get(key)
                 if torch.is_tensor(v) and v.is_floating_point():
                     data[key] = v.to(self.amp_dtype)

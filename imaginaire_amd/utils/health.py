@@ -84,22 +84,44 @@ class Watchdog(object):
             self._file = open(self.path, 'w')
         return self._file
 
-    def beat(self, iteration=None, phase='iteration'):
+    def beat(self, iteration=None, phase='iteration', grace=False):
         """Re-arm the deadline. Writes a one-line header naming the last completed
         iteration so the report says *where* the job stalled, then re-arms the native
-        watchdog thread (the traceback goes right after the header)."""
+        watchdog thread (the traceback goes right after the header).
+
+        ``grace=True`` arms the long ``first_timeout`` bound instead: for phases that are
+        legitimately slower than a steady-state iteration (checkpoint save, FID / metrics,
+        end of epoch, data-loader start-up and first use of new shapes in the next
+        iteration). The next plain beat restores the steady-state bound."""
         if not self.enabled:
             return
+        deadline = self.first_timeout if grace else self._deadline()
         f = self._open()
         f.seek(0)
         f.truncate()
         f.write('rank %d: no progress within %.0f s after %s %s (beat %d, %s)\n' % (
-            self.rank, self._deadline(), phase, iteration, self.beats,
+            self.rank, deadline, phase, iteration, self.beats,
             time.strftime('%Y-%m-%d %H:%M:%S')))
         f.flush()
-        faulthandler.dump_traceback_later(self._deadline(), repeat=False, file=f,
+        faulthandler.dump_traceback_later(deadline, repeat=False, file=f,
                                           exit=self.exit_on_hang)
         self.beats += 1
+
+    def grace(self, iteration=None, phase='phase'):
+        """Context manager: the body runs under the long bound; leaving it re-arms the
+        steady-state bound (the following iteration must then finish within ``timeout``)."""
+        wd = self
+
+        class _Grace(object):
+            def __enter__(self):
+                wd.beat(iteration, phase, grace=True)
+                return wd
+
+            def __exit__(self, *exc):
+                if exc[0] is None:
+                    wd.beat(iteration, 'after ' + phase)
+                return False
+        return _Grace()
 
     def _deadline(self):
         return self.first_timeout if self.beats == 0 else self.timeout

@@ -126,7 +126,7 @@ def _wrap_model(cfg, model):
                                        broadcast_buffers=getattr(cfg.trainer,
                                                                  'ddp_broadcast_buffers', False),
                                        find_unused=getattr(cfg.trainer, 'ddp_find_unused',
-                                                           'local'))
+                                                           'global'))
     return WrappedModel(model)
 
 

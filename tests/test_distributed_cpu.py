@@ -156,6 +156,61 @@ def _unused_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+def _rank_skip_worker(rank, world, port, q):
+    """Rank 1 skips a branch that rank 0 uses (data-dependent control flow, e.g. the
+    vid2vid hand discriminator on a batch without hand pixels)."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from imaginaire_amd.optimizers import FusedAdam
+    from imaginaire_amd.parallel import DistributedDataParallel
+    torch.manual_seed(0)
+    trunk = torch.nn.Linear(4, 4)
+    hand = torch.nn.Linear(4, 4)
+    never = torch.nn.Linear(4, 4)
+    net = torch.nn.ModuleDict({'trunk': trunk, 'hand': hand, 'never': never})
+    ddp = DistributedDataParallel(net)  # default: find_unused='global'
+    opt = FusedAdam(net.parameters(), lr=0.1)
+    grads = []
+    for it in range(3):
+        x = torch.randn(3, 4, generator=torch.Generator().manual_seed(10 * it + rank))
+        ddp.begin()
+        loss = trunk(x).sum()
+        if rank == 0 or it == 0:
+            loss = loss + hand(x).pow(2).sum()
+        loss.backward()
+        ddp.finish()
+        grads.append((hand.weight.grad is None, never.weight.grad is None,
+                      None if hand.weight.grad is None else hand.weight.grad.clone().numpy()))
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+    params = torch.cat([p.detach().reshape(-1) for p in net.parameters()]).numpy()
+    q.put((rank, params, grads))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_ddp_rank_dependent_skip_keeps_replicas_identical():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_skip_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda t: t[0])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    import numpy as np
+    (_, p0, g0), (_, p1, g1) = res
+    assert np.array_equal(p0, p1), 'replicas diverged after a rank-local skip'
+    for it in range(3):
+        # the branch rank 1 skipped still carries the averaged gradient on rank 1
+        assert g0[it][0] is False and g1[it][0] is False
+        assert np.allclose(g0[it][2], g1[it][2])
+        # a branch no rank used keeps grad None everywhere
+        assert g0[it][1] is True and g1[it][1] is True
+
+
 def test_ddp_unused_parameters_keep_grad_none():
     ctx = mp.get_context('spawn')
     q = ctx.Queue()

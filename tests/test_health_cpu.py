@@ -79,6 +79,50 @@ def test_watchdog_clean_exit_leaves_no_report(tmp_path):
     assert not os.path.exists(os.path.join(str(tmp_path), 'hang_rank0.txt'))
 
 
+def test_watchdog_grace_covers_slow_phase(tmp_path):
+    """A phase longer than the steady-state bound (snapshot save / FID) under grace does
+    not fire; a plain iteration that stalls afterwards still does."""
+    code = ('import time\n'
+            'from imaginaire_amd.utils.health import Watchdog\n'
+            'w = Watchdog(1.0, %r, first_timeout=8.0)\n'
+            'w.beat(1)\n'
+            'w.beat(2)\n'
+            'with w.grace(2, "write_metrics"):\n'
+            '    time.sleep(2.5)\n'
+            'print("survived", flush=True)\n'
+            'def stalled_iteration():\n'
+            '    time.sleep(60)\n'
+            'stalled_iteration()\n' % str(tmp_path))
+    r = subprocess.run([sys.executable, '-c', code], env=_env(), capture_output=True,
+                       text=True, timeout=60)
+    assert 'survived' in r.stdout
+    assert r.returncode != 0
+    rep = open(os.path.join(str(tmp_path), 'hang_rank0.txt')).read()
+    assert 'after write_metrics' in rep and 'stalled_iteration' in rep
+
+
+def test_train_py_slow_end_of_iteration_under_watchdog(tmp_path):
+    """train.py with a 1 s watchdog and an end_of_iteration (checkpoint + metrics) that
+    takes 2.5 s: the run finishes instead of being killed mid-eval."""
+    cfg = _cfg(tmp_path, max_iter=3, snapshot_save_iter=2, logging_iter=1)
+    logdir = os.path.join(str(tmp_path), 'log')
+    code = ('import sys, time\n'
+            'sys.argv = ["train.py", "--config", %r, "--logdir", %r, "--single_gpu",\n'
+            '            "--watchdog-timeout", "1", "--watchdog-grace", "600"]\n'
+            'from imaginaire_amd.trainers.base import BaseTrainer\n'
+            '_orig = BaseTrainer.end_of_iteration\n'
+            'def slow(self, *a, **k):\n'
+            '    time.sleep(2.5)\n'
+            '    return _orig(self, *a, **k)\n'
+            'BaseTrainer.end_of_iteration = slow\n'
+            'import train\n'
+            'train.main()\n' % (cfg, logdir))
+    r = subprocess.run([sys.executable, '-c', code], cwd=ROOT, env=_env(),
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert 'Done with training' in r.stdout
+
+
 def _cfg(tmp_path, **over):
     with open(os.path.join(ROOT, 'configs', 'unit_test', 'spade.yaml')) as f:
         cfg = yaml.safe_load(f)
@@ -117,10 +161,13 @@ def test_two_rank_hang_is_detected(tmp_path):
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
            '--master-addr', '127.0.0.1', '--master-port', str(_free_port()), 'train.py',
            '--config', cfg, '--backend', 'gloo', '--logdir', logdir,
-           '--watchdog-timeout', '45']
+           '--watchdog-timeout', '45', '--watchdog-grace', '60']
     r = subprocess.run(cmd, cwd=ROOT, env=_env(IMAGINAIRE_AMD_FAULT='hang@2:1'),
                        capture_output=True, text=True, timeout=900)
     assert r.returncode != 0
     rep1 = open(os.path.join(logdir, 'hang_rank1.txt')).read()
-    assert 'after iteration 2' in rep1 and 'health.py' in rep1, rep1
+    # the header names the last completed iteration (2) and the phase that followed it
+    header = rep1.splitlines()[0]
+    assert header.startswith('rank 1: no progress') and ' 2 (beat' in header, rep1
+    assert 'health.py' in rep1, rep1
     assert os.path.exists(os.path.join(logdir, 'hang_rank0.txt'))

@@ -58,3 +58,20 @@ def test_corrupt_files_raise_value_errors():
             mp4.parse_video_track(bytes(b))
         except ValueError:
             pass
+
+
+def test_stsc_runs_must_advance():
+    """A sample-to-chunk table whose runs do not start at increasing chunks is rejected
+    up front (malformed clips must not cost O(runs x chunks) loader time)."""
+    import struct
+    import time
+    buf = bytearray(mp4.write_mjpeg_mp4(_frames(t=5), samples_per_chunk=2))
+    i = buf.index(b'stsc')
+    n = struct.unpack_from('>I', buf, i + 8)[0]
+    assert n >= 2
+    # second run's first_chunk := first run's first_chunk
+    struct.pack_into('>I', buf, i + 12 + 12, struct.unpack_from('>I', buf, i + 12)[0])
+    t0 = time.perf_counter()
+    with pytest.raises(ValueError, match='does not advance'):
+        mp4.parse_video_track(bytes(buf))
+    assert time.perf_counter() - t0 < 1.0

@@ -43,6 +43,9 @@ def parse_args(argv=None):
                         default=float(os.environ.get('IMAGINAIRE_AMD_WATCHDOG_S', 900)),
                         help='seconds without a finished iteration before the rank dumps its '
                              'stacks to <logdir>/hang_rank<R>.txt and exits (0: off)')
+    parser.add_argument('--watchdog_grace', '--watchdog-grace', type=float, default=None,
+                        help='bound for start-up, checkpoint / FID phases and the first '
+                             'iterations of an epoch (default 10x --watchdog-timeout)')
     return parser.parse_args(argv)
 
 
@@ -74,12 +77,18 @@ def main(argv=None):
     # fault injection, straggler report at logging boundaries
     faults = FaultInjector()
     stragglers = StragglerMonitor()
-    with Watchdog(args.watchdog_timeout, cfg.logdir) as watchdog:
+    start_iteration = current_iteration
+    with Watchdog(args.watchdog_timeout, cfg.logdir,
+                  first_timeout=args.watchdog_grace) as watchdog:
         watchdog.beat(current_iteration, 'start')
         for epoch in range(current_epoch, cfg.max_epoch):
             print('Epoch {} ...'.format(epoch))
             if hasattr(train_data_loader.sampler, 'set_epoch'):
                 train_data_loader.sampler.set_epoch(current_epoch)
+            # epoch start-up (loader workers, temporal-curriculum / local-enhancer switches,
+            # first use of new shapes) runs until the epoch's first iteration ends under the
+            # long grace bound
+            watchdog.beat(current_iteration, 'start of epoch %d' % epoch, grace=True)
             trainer.start_of_epoch(current_epoch)
             for it, data in enumerate(train_data_loader):
                 data = trainer.start_of_iteration(data, current_iteration)
@@ -87,8 +96,13 @@ def main(argv=None):
                     data = faults.apply(current_iteration, data)
                 train_step(data)
                 current_iteration += 1
+                # snapshot save + FID (write_metrics) may run here: long bound
+                watchdog.beat(current_iteration, 'end_of_iteration', grace=True)
                 trainer.end_of_iteration(data, current_epoch, current_iteration)
-                watchdog.beat(current_iteration)
+                # the first iteration of an epoch and the hipGraph warm-up / capture
+                # iterations of the run keep the long bound as well
+                watchdog.beat(current_iteration, grace=(it == 0 or
+                                                        current_iteration < start_iteration + 5))
                 stragglers.tick()
                 if get_world_size() > 1 and current_iteration % cfg.logging_iter == 0:
                     stragglers.report()
@@ -96,7 +110,8 @@ def main(argv=None):
                     print('Done with training!!!')
                     return
             current_epoch += 1
-            trainer.end_of_epoch(data, current_epoch, current_iteration)
+            with watchdog.grace(current_iteration, 'end_of_epoch'):
+                trainer.end_of_epoch(data, current_epoch, current_iteration)
     print('Done with training!!!')
 
 
