@@ -27,7 +27,7 @@ namespace iamd {
 namespace {
 
 constexpr int kT = 256;
-constexpr int kColTile = 256;     // columns per K1 block
+constexpr int kColTile = 4 * kT;  // columns per K1 block (4 per thread)
 constexpr int kRowsPerSplit = 64; // rows per K1 block
 constexpr int kRowsPerBlock = 4;  // rows (waves) per K3 block
 
@@ -41,6 +41,7 @@ struct SnEntry {
   int64_t nsplit;
   int64_t h, w;
   int64_t cl_cin, cl_khw;  // channels-last mapping (0 = none)
+  int64_t vec;             // w % 4 == 0 and W 16-byte aligned: 16-B row loads
 };
 
 // memory column -> logical column (32-bit: every SN weight row is < 2^31 elements).
@@ -68,18 +69,48 @@ __device__ float block_sum(float v, float* sh) {
   return s;
 }
 
-// blocks: {layer, col_tile, row_split}
+// blocks: {layer, col_tile, row_split}. Each thread owns 4 adjacent columns (16-B loads when
+// the row length is a multiple of 4) and keeps 8 rows of loads in flight: the plain
+// one-column-per-thread walk ran at ~1.5 TB/s (profiles/spade_step_latest_mi355x.txt).
 __global__ void __launch_bounds__(kT) sn_colsum(const SnEntry* __restrict__ ents,
                                                  const int* __restrict__ blocks) {
   const int* bm = blocks + 3 * blockIdx.x;
   const SnEntry e = ents[bm[0]];
-  const int64_t c = (int64_t)bm[1] * kColTile + threadIdx.x;
+  const int64_t c = (int64_t)bm[1] * kColTile + threadIdx.x * 4;
   if (c >= e.w) return;
   const int64_t r0 = (int64_t)bm[2] * kRowsPerSplit;
   const int64_t r1 = min(e.h, r0 + kRowsPerSplit);
-  float acc = 0.f;
-  for (int64_t r = r0; r < r1; ++r) acc = fmaf(e.W[r * e.w + c], e.u[r], acc);
-  e.tp[bm[2] * e.w + c] = acc;  // memory order, this row split's slab
+  const bool vec = e.vec;  // then c + 3 < w as well
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t r = r0; r < r1; r += 8) {
+    float wv[8][4], uv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int64_t rr = r + i;
+      const bool ok = rr < r1;
+      uv[i] = ok ? e.u[rr] : 0.f;
+      const float* src = e.W + (ok ? rr : r0) * e.w + c;
+      if (vec) {
+        const float4 v4 = *reinterpret_cast<const float4*>(src);
+        wv[i][0] = v4.x; wv[i][1] = v4.y; wv[i][2] = v4.z; wv[i][3] = v4.w;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) wv[i][k] = c + k < e.w ? src[k] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] = fmaf(wv[i][k], uv[i], acc[k]);
+  }
+  float* o = e.tp + bm[2] * e.w + c;  // memory order, this row split's slab
+  if (vec) {
+    *reinterpret_cast<float4*>(o) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (c + k < e.w) o[k] = acc[k];
+  }
 }
 
 // blocks: {layer, col_tile}: t[c] = sum over row splits of the K1 slabs, in split order
@@ -87,11 +118,14 @@ __global__ void __launch_bounds__(kT) sn_tsum(const SnEntry* __restrict__ ents,
                                                const int* __restrict__ blocks) {
   const int* bm = blocks + 2 * blockIdx.x;
   const SnEntry e = ents[bm[0]];
-  const int64_t c = (int64_t)bm[1] * kColTile + threadIdx.x;
-  if (c >= e.w) return;
-  float acc = 0.f;
-  for (int64_t k = 0; k < e.nsplit; ++k) acc += e.tp[k * e.w + c];
-  e.t[c] = acc;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int64_t c = (int64_t)bm[1] * kColTile + q * kT + threadIdx.x;
+    if (c >= e.w) return;
+    float acc = 0.f;
+    for (int64_t k = 0; k < e.nsplit; ++k) acc += e.tp[k * e.w + c];
+    e.t[c] = acc;
+  }
 }
 
 // one block per layer: sums of squares of t -> scal[l*4 + 0]
@@ -118,14 +152,24 @@ __global__ void __launch_bounds__(64 * kRowsPerBlock) sn_rows(const SnEntry* __r
   const float k = update ? 1.f / fmaxf(sqrtf(scal[4 * bm[0]]), eps) : 1.f;
   const float* row = e.W + r * e.w;
   float acc = 0.f;
-  if (update) {  // t is in memory order: straight (vectorised when rows are 16-B aligned) dot
+  if (update) {  // t is in memory order: straight dot, 16-B loads, 4 per lane in flight
     const float* x = e.t;
-    if ((e.w & 3) == 0) {
+    if (e.vec) {
       const float4* r4 = reinterpret_cast<const float4*>(row);
       const float4* x4 = reinterpret_cast<const float4*>(x);
-      for (int64_t c = lane; c < e.w / 4; c += 64) {
-        const float4 a = r4[c], b = x4[c];
-        acc = fmaf(a.x, b.x, fmaf(a.y, b.y, fmaf(a.z, b.z, fmaf(a.w, b.w, acc))));
+      const int64_t w4 = e.w / 4;
+      for (int64_t c = lane; c < w4; c += 4 * 64) {
+        float4 a[4], b[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bool ok = c + i * 64 < w4;
+          a[i] = ok ? r4[c + i * 64] : make_float4(0.f, 0.f, 0.f, 0.f);
+          b[i] = ok ? x4[c + i * 64] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc = fmaf(a[i].x, b[i].x, fmaf(a[i].y, b[i].y, fmaf(a[i].z, b[i].z,
+                                                               fmaf(a[i].w, b[i].w, acc))));
       }
     } else {
       for (int64_t c = lane; c < e.w; c += 64) acc = fmaf(row[c], x[c], acc);
@@ -192,8 +236,9 @@ SnPlan& get_plan(const std::vector<at::Tensor>& W, const std::vector<at::Tensor>
   int64_t tot_w = 0, tot_h = 0, tot_p = 0;
   for (int i = 0; i < L; ++i) {
     tot_h += W[i].size(0);
-    tot_w += W[i].numel() / W[i].size(0);
-    tot_p += (W[i].size(0) + kRowsPerSplit - 1) / kRowsPerSplit * (W[i].numel() / W[i].size(0));
+    tot_w += (W[i].numel() / W[i].size(0) + 3) / 4 * 4;
+    tot_p += ((W[i].size(0) + kRowsPerSplit - 1) / kRowsPerSplit * (W[i].numel() / W[i].size(0)) +
+              3) / 4 * 4;
   }
   SnPlan p;
   auto fopt = W[0].options().dtype(at::kFloat);
@@ -221,14 +266,16 @@ SnPlan& get_plan(const std::vector<at::Tensor>& W, const std::vector<at::Tensor>
     e.cl_cin = cl ? w.size(1) : 0;
     e.cl_khw = cl ? w.size(2) * w.size(3) : 0;
     e.t = p.t_ws.data_ptr<float>() + ow;
+    // (workspace slices start at multiples of 4 floats: 16-B aligned)
+    e.vec = (e.w % 4 == 0) && (reinterpret_cast<uintptr_t>(e.W) & 15) == 0;
     e.s = p.s_ws.data_ptr<float>() + oh;
     const int ntile = (int)((e.w + kColTile - 1) / kColTile);
     const int nsplit = (int)((e.h + kRowsPerSplit - 1) / kRowsPerSplit);
     e.tp = p.tp_ws.data_ptr<float>() + op;
     e.nsplit = nsplit;
-    ow += e.w;
+    ow += (e.w + 3) / 4 * 4;
     oh += e.h;
-    op += (int64_t)nsplit * e.w;
+    op += ((int64_t)nsplit * e.w + 3) / 4 * 4;
     for (int a = 0; a < ntile; ++a) {
       for (int b = 0; b < nsplit; ++b) {
         cb.push_back(i);
@@ -304,6 +351,7 @@ struct ScEntry {
   const float* W;
   int64_t numel;
   int64_t off;
+  int64_t vec;  // W 16-byte aligned: vector path
 };
 
 __global__ void __launch_bounds__(kT) sn_scale_cast(const ScEntry* __restrict__ ents,
@@ -315,8 +363,21 @@ __global__ void __launch_bounds__(kT) sn_scale_cast(const ScEntry* __restrict__ 
   const float inv = 1.f / sigma[t];
   const int64_t start = (int64_t)chunk * kScChunk;
   const int64_t end = min(e.numel, start + (int64_t)kScChunk);
-  __hip_bfloat16* o = out + e.off;
-  for (int64_t i = start + threadIdx.x; i < end; i += kT) o[i] = __float2bfloat16(e.W[i] * inv);
+  __hip_bfloat16* o = out + e.off;  // 16-B aligned (offsets are multiples of 8 elements)
+  if (e.vec) {  // 8 elements per lane per trip: two 16-B fp32 loads, one 16-B bf16 store
+    const int64_t vend = start + ((end - start) & ~(int64_t)7);
+    for (int64_t i = start + threadIdx.x * 8; i < vend; i += kT * 8) {
+      float v[8];
+      load_vec<float, 4>(e.W + i, *reinterpret_cast<float(*)[4]>(v));
+      load_vec<float, 4>(e.W + i + 4, *reinterpret_cast<float(*)[4]>(v + 4));
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] *= inv;
+      store_vec<__hip_bfloat16, 8>(o + i, v);
+    }
+    for (int64_t i = vend + threadIdx.x; i < end; i += kT) o[i] = __float2bfloat16(e.W[i] * inv);
+  } else {
+    for (int64_t i = start + threadIdx.x; i < end; i += kT) o[i] = __float2bfloat16(e.W[i] * inv);
+  }
 }
 
 struct ScPlan {
@@ -342,7 +403,8 @@ ScPlan& get_sc_plan(const std::vector<at::Tensor>& W) {
   for (size_t i = 0; i < W.size(); ++i) {
     IAMD_CHECK(W[i].scalar_type() == at::kFloat && W[i].is_non_overlapping_and_dense(),
                "mt_sn_scale_cast: weights must be dense fp32");
-    ents.push_back({W[i].data_ptr<float>(), W[i].numel(), off});
+    ents.push_back({W[i].data_ptr<float>(), W[i].numel(), off,
+                    (int64_t)((reinterpret_cast<uintptr_t>(W[i].data_ptr()) & 15) == 0)});
     p.offs.push_back(off);
     const int64_t nch = (W[i].numel() + kScChunk - 1) / kScChunk;
     for (int64_t c = 0; c < nch; ++c) {
@@ -413,14 +475,26 @@ snb_reduce(const G* __restrict__ g, const float* __restrict__ W, int64_t n,
     vm[c] = v[lc];
   }
   float acc = 0.f;
-  if ((n & 7) == 0) {  // 8 elements per lane per trip: 16-B (bf16) / 2x16-B (fp32) loads
-    for (int64_t i = gtid * 8; i < n; i += gsz * 8) {
-      float gv[8], wv[8];
-      load_vec<G, 8>(g + i, gv);
-      load_vec<float, 4>(W + i, *reinterpret_cast<float(*)[4]>(wv));
-      load_vec<float, 4>(W + i + 4, *reinterpret_cast<float(*)[4]>(wv + 4));
+  if ((n & 7) == 0) {  // 8 elements per lane per trip, two trips in flight
+    for (int64_t i = gtid * 8; i < n; i += gsz * 16) {
+      const int64_t j = i + gsz * 8;
+      const bool two = j < n;
+      float gv[2][8], wv[2][8];
+      load_vec<G, 8>(g + i, gv[0]);
+      load_vec<float, 4>(W + i, *reinterpret_cast<float(*)[4]>(wv[0]));
+      load_vec<float, 4>(W + i + 4, *reinterpret_cast<float(*)[4]>(wv[0] + 4));
+      if (two) {
+        load_vec<G, 8>(g + j, gv[1]);
+        load_vec<float, 4>(W + j, *reinterpret_cast<float(*)[4]>(wv[1]));
+        load_vec<float, 4>(W + j + 4, *reinterpret_cast<float(*)[4]>(wv[1] + 4));
+      } else {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) acc = fmaf(gv[k], wv[k], acc);
+        for (int k = 0; k < 8; ++k) gv[1][k] = wv[1][k] = 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc = fmaf(gv[0][k], wv[0][k], acc);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc = fmaf(gv[1][k], wv[1][k], acc);
     }
   } else {
     for (int64_t i = gtid; i < n; i += gsz) acc = fmaf(to_f<G>(g[i]), W[i], acc);
@@ -451,23 +525,30 @@ snb_apply(const G* __restrict__ g, const float* __restrict__ u, const float* __r
   const float s = sigma[0];
   const float inv = 1.f / s;
   const float coef = dot / (s * s);
+  const int64_t n = h * w;
+  if ((w & 7) == 0) {  // flat walk, 8 columns of one row per lane: 16-B loads and stores
+    for (int64_t i = ((int64_t)blockIdx.x * kSnbT + threadIdx.x) * 8; i < n;
+         i += (int64_t)gridDim.x * kSnbT * 8) {
+      const uint32_t r = (uint32_t)i / (uint32_t)w;  // n < 2^31 (checked on the host)
+      const int64_t c = i - (int64_t)r * w;
+      const float cu = coef * u[r];
+      float gv[8], vv[8], o[8];
+      load_vec<G, 8>(g + i, gv);
+      load_vec<float, 4>(vm + c, *reinterpret_cast<float(*)[4]>(vv));
+      load_vec<float, 4>(vm + c + 4, *reinterpret_cast<float(*)[4]>(vv + 4));
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = fmaf(gv[k], inv, -cu * vv[k]);
+      store_vec<float, 4>(dw + i, *reinterpret_cast<float(*)[4]>(o));
+      store_vec<float, 4>(dw + i + 4, *reinterpret_cast<float(*)[4]>(o + 4));
+    }
+    return;
+  }
   for (int64_t r = blockIdx.x; r < h; r += gridDim.x) {
     const float cu = coef * u[r];
     const G* gr = g + r * w;
     float* dr = dw + r * w;
-    if ((w & 3) == 0) {  // 4 columns per lane: 16-B fp32 stores / vm loads
-      for (int64_t c = threadIdx.x * 4; c < w; c += kSnbT * 4) {
-        float gv[4], vv[4], o[4];
-        load_vec<G, 4>(gr + c, gv);
-        load_vec<float, 4>(vm + c, vv);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) o[k] = fmaf(gv[k], inv, -cu * vv[k]);
-        store_vec<float, 4>(dr + c, o);
-      }
-    } else {
-      for (int64_t c = threadIdx.x; c < w; c += kSnbT)
-        dr[c] = fmaf(to_f<G>(gr[c]), inv, -cu * vm[c]);
-    }
+    for (int64_t c = threadIdx.x; c < w; c += kSnbT)
+      dr[c] = fmaf(to_f<G>(gr[c]), inv, -cu * vm[c]);
   }
 }
 
@@ -489,12 +570,15 @@ at::Tensor sn_scale_backward(const at::Tensor& grad_in, const at::Tensor& weight
   IAMD_CHECK(w < (1ll << 31), "sn_scale_backward: row too long");
   const int64_t cl_cin = cl ? weight.size(1) : 0, cl_khw = cl ? weight.size(2) * weight.size(3) : 0;
   auto dw = at::empty_like(weight, fmt);
-  const int P = (int)std::max<int64_t>(1, std::min<int64_t>(512, (n + 4095) / 4096));
+  IAMD_CHECK(n < (1ll << 31), "sn_scale_backward: weight too large");
+  const int P = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (n + 4095) / 4096));
   const int P4 = (P + 3) & ~3;  // keeps vm 16-byte aligned for the vector loads
   auto ws = at::empty({P4 + w}, weight.options());
   float* partial = ws.data_ptr<float>();
   float* vm = partial + P4;
-  const int ablocks = (int)std::max<int64_t>(1, std::min<int64_t>(h, 1024));
+  const int ablocks = (w & 7) == 0
+                          ? (int)std::max<int64_t>(1, std::min<int64_t>(4096, (n + 2047) / 2048))
+                          : (int)std::max<int64_t>(1, std::min<int64_t>(h, 1024));
   hipStream_t st = stream();
   auto run = [&](auto* gp) {
     using G = std::remove_const_t<std::remove_pointer_t<decltype(gp)>>;

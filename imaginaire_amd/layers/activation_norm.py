@@ -24,7 +24,7 @@ from imaginaire_amd.ops import conv as nhwc_conv
 from torch import nn
 from torch.nn import functional as F
 
-from imaginaire_amd.ops.norm import fused_norm_act, prefetch_sync_stats
+from imaginaire_amd.ops.norm import defer_sync_bwd, fused_norm_act, prefetch_sync_stats
 from imaginaire_amd.ops.resize import interpolate
 from .conv import LinearBlock, Conv2dBlock, HyperConv2d, PartialConv2dBlock
 from .misc import PartialSequential
@@ -134,7 +134,7 @@ class _FusedNormBase(nn.Module):
     def _effective_mode(self):
         return self.mode
 
-    def fused(self, x, gamma=None, beta=None, gb=None, act_slope=1.0):
+    def fused(self, x, gamma=None, beta=None, gb=None, act_slope=1.0, deferred=None):
         squeeze = None
         if x.dim() == 2:
             squeeze = x.shape
@@ -151,7 +151,7 @@ class _FusedNormBase(nn.Module):
             running_mean=self.running_mean if self.track_running_stats else None,
             running_var=self.running_var if self.track_running_stats else None,
             training=use_batch, momentum=self._factor() if use_batch else 0.0, eps=self.eps,
-            slope=act_slope, process_group=self.process_group)
+            slope=act_slope, process_group=self.process_group, deferred=deferred)
         if squeeze is not None:
             y = y.reshape(squeeze)
         return y
@@ -187,9 +187,8 @@ class SyncBatchNorm(_FusedNormBase):
     mode = 'sync_batch'
 
     def _effective_mode(self):
-        import torch.distributed as dist
-        if self.training and dist.is_available() and dist.is_initialized() and \
-                dist.get_world_size(self.process_group) > 1:
+        from imaginaire_amd.ops.norm import sync_active
+        if self.training and sync_active(self.process_group):
             return 'sync_batch'
         return 'batch'
 
@@ -203,12 +202,13 @@ class InstanceNorm2d(_FusedNormBase):
         super().__init__(num_features, eps, momentum, affine, track_running_stats)
 
 
-def fused_norm_or_none(norm, x, gamma=None, beta=None, gb=None, act_slope=1.0):
+def fused_norm_or_none(norm, x, gamma=None, beta=None, gb=None, act_slope=1.0, deferred=None):
     """Apply ``norm`` (fused module, torch module or None) + modulation + activation."""
     if norm is None:
         return fused_norm_act(x, 'none', gamma=gamma, beta=beta, gb=gb, slope=act_slope)
     if isinstance(norm, _FusedNormBase):
-        return norm.fused(x, gamma=gamma, beta=beta, gb=gb, act_slope=act_slope)
+        return norm.fused(x, gamma=gamma, beta=beta, gb=gb, act_slope=act_slope,
+                          deferred=deferred)
     y = norm(x)
     if gb is not None:
         gamma, beta = gb.chunk(2, dim=1)
@@ -241,6 +241,8 @@ def _modulate_more(out, gbs, act_slope):
 
 
 _MULTIMOD_FUSED = os.environ.get('IMAGINAIRE_AMD_SPADE_MULTIMOD', '1') == '1'
+# sync-BN data gradient finished by a join node after the γ|β backward (0: synchronous)
+_ASYNC_SYNCBN_BWD = os.environ.get('IMAGINAIRE_AMD_ASYNC_SYNCBN_BWD', '1') == '1'
 
 
 class AdaptiveNorm(nn.Module):
@@ -383,11 +385,17 @@ class SpatiallyAdaptiveNorm(nn.Module):
     def forward(self, x, *cond_inputs, act_slope=1.0, **kwargs):
         active = [i for i in range(len(cond_inputs)) if cond_inputs[i] is not None]
         size = x.shape[2:]
+        deferred = None
         if isinstance(self.norm, SyncBatchNorm) and self.training and \
-                self.norm._effective_mode() == 'sync_batch' and not self.norm.affine:
-            # start the cross-rank statistics exchange of x now: it rides xGMI while the γ|β
-            # convolutions below (independent of it) run
-            prefetch_sync_stats(x, self.norm.eps, self.norm.process_group)
+                self.norm._effective_mode() == 'sync_batch':
+            if not self.norm.affine:
+                # start the cross-rank statistics exchange of x now: it rides xGMI while the
+                # γ|β convolutions below (independent of it) run
+                prefetch_sync_stats(x, self.norm.eps, self.norm.process_group)
+            if _ASYNC_SYNCBN_BWD and active:
+                # backward mirror: the norm's Σg, Σg·x̂ all-reduce runs while the γ|β / mlp
+                # convolution backward runs; this join node (created before them) finishes dx
+                x, deferred = defer_sync_bwd(x)
         gbs = []
         for i in active:
             label_map = LabelMapCache.resize(cond_inputs[i], size,
@@ -396,8 +404,10 @@ class SpatiallyAdaptiveNorm(nn.Module):
         if len(gbs) == 0:
             return fused_norm_or_none(self.norm, x, act_slope=act_slope)
         if len(gbs) == 1:
-            return fused_norm_or_none(self.norm, x, gb=gbs[0], act_slope=act_slope)
-        return _modulate_more(fused_norm_or_none(self.norm, x, gb=gbs[0], act_slope=1.0),
+            return fused_norm_or_none(self.norm, x, gb=gbs[0], act_slope=act_slope,
+                                      deferred=deferred)
+        return _modulate_more(fused_norm_or_none(self.norm, x, gb=gbs[0], act_slope=1.0,
+                                                 deferred=deferred),
                               gbs[1:], act_slope)
 
 
@@ -433,6 +443,11 @@ class HyperSpatiallyAdaptiveNorm(nn.Module):
         self.conditional = True
 
     def forward(self, x, *cond_inputs, norm_weights=(None, None), act_slope=1.0, **kwargs):
+        deferred = None
+        if isinstance(self.norm, SyncBatchNorm) and self.training and _ASYNC_SYNCBN_BWD and \
+                self.norm._effective_mode() == 'sync_batch' and \
+                any(c is not None for c in cond_inputs):
+            x, deferred = defer_sync_bwd(x)  # see SpatiallyAdaptiveNorm.forward
         gbs = []
         for i in range(len(cond_inputs)):
             if cond_inputs[i] is None:
@@ -457,8 +472,10 @@ class HyperSpatiallyAdaptiveNorm(nn.Module):
         if len(gbs) == 0:
             return fused_norm_or_none(self.norm, x, act_slope=act_slope)
         if len(gbs) == 1:
-            return fused_norm_or_none(self.norm, x, gb=gbs[0], act_slope=act_slope)
-        return _modulate_more(fused_norm_or_none(self.norm, x, gb=gbs[0], act_slope=1.0),
+            return fused_norm_or_none(self.norm, x, gb=gbs[0], act_slope=act_slope,
+                                      deferred=deferred)
+        return _modulate_more(fused_norm_or_none(self.norm, x, gb=gbs[0], act_slope=1.0,
+                                                 deferred=deferred),
                               gbs[1:], act_slope)
 
 

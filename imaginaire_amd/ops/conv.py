@@ -529,13 +529,48 @@ def tapsplit_eligible(x, w, stride, padding, dilation, groups):
 
 
 _WGRAD_CHOICE = {}
+# shapes first seen inside a backward under IMAGINAIRE_AMD_MFMA_WGRAD=auto: they run k11 until
+# tune_pending() (called by the trainer at rank-uniform iteration boundaries, never inside a
+# backward) has timed both kernels and agreed the choice across ranks
+_WGRAD_PENDING = {}
 
 
-def _wgrad(dy, xb, wb, stride, padding, dilation, cout=-1, cin=-1, wdt=torch.float32):
-    """Weight gradient: k11 or MIOpen wrw, whichever measured faster for this shape (timed
-    once per shape, both paths warm; ``IMAGINAIRE_AMD_MFMA_WGRAD`` = auto | 1 | 0). k11
-    returns the gradient already cropped to (cout, cin) and in the weight's dtype (bf16 for
-    the bf16 spectral-norm / autocast weights): the crop and cast ride in its split-K sum."""
+def _time_ms(fn, reps=3):
+    fn()  # warm (MIOpen find / compile)
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    start.record()
+    for _ in range(reps):
+        fn()
+    end.record()
+    end.synchronize()
+    return start.elapsed_time(end)
+
+
+def _agree(times):
+    """Sum per-candidate timings over ranks (every rank then takes the same argmin).
+    ``times``: {key: {candidate: ms}} with identical keys and candidates on every rank."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1) or \
+            not times:
+        return times
+    keys = sorted(times, key=repr)
+    cands = [sorted(times[k]) for k in keys]
+    flat = [times[k][c] for k, cs in zip(keys, cands) for c in cs]
+    dev = 'cpu' if dist.get_backend() == 'gloo' else torch.device('cuda',
+                                                                  torch.cuda.current_device())
+    t = torch.tensor(flat, dtype=torch.float64, device=dev)
+    dist.all_reduce(t)
+    t = t.cpu().tolist()
+    out, i = {}, 0
+    for k, cs in zip(keys, cands):
+        out[k] = {}
+        for c in cs:
+            out[k][c] = t[i]
+            i += 1
+    return out
+
+
+def _wgrad_fns(dy, xb, wb, stride, padding, dilation, cout, cin, wdt):
     def k11():
         return _ext.ext().conv2d_wgrad_mfma(dy, xb, wb.shape[2], wb.shape[3], stride[0],
                                             stride[1], padding[0], padding[1], dilation[0],
@@ -545,7 +580,16 @@ def _wgrad(dy, xb, wb, stride, padding, dilation, cout=-1, cin=-1, wdt=torch.flo
         return torch.ops.aten.convolution_backward(
             dy, xb, wb, None, stride, padding, dilation, False, [0, 0], 1,
             [False, True, False])[1]
+    return k11, miopen
 
+
+def _wgrad(dy, xb, wb, stride, padding, dilation, cout=-1, cin=-1, wdt=torch.float32):
+    """Weight gradient: k11 or MIOpen wrw (``IMAGINAIRE_AMD_MFMA_WGRAD`` = 1 | 0 | auto; auto =
+    the faster of the two per shape, timed by :func:`tune_pending` outside the backward and
+    agreed across ranks). k11 returns the gradient already cropped to (cout, cin) and in the
+    weight's dtype (bf16 for the bf16 spectral-norm / autocast weights): the crop and cast ride
+    in its split-K sum."""
+    k11, miopen = _wgrad_fns(dy, xb, wb, stride, padding, dilation, cout, cin, wdt)
     mode = _MFMA_WGRAD
     fl = 2.0 * dy.shape[0] * dy.shape[2] * dy.shape[3] * wb.numel()
     desc = _gemm_desc(xb, wb, stride, padding)
@@ -555,32 +599,52 @@ def _wgrad(dy, xb, wb, stride, padding, dilation, cout=-1, cin=-1, wdt=torch.flo
     if mode == '0':
         with _Logged('wgrad', 'miopen', fl, desc):
             return miopen()
-    key = (tuple(dy.shape), tuple(xb.shape), tuple(wb.shape), stride, padding, dilation)
+    key = (tuple(dy.shape), tuple(xb.shape), tuple(wb.shape), stride, padding, dilation,
+           cout, cin, wdt)
     choice = _WGRAD_CHOICE.get(key)
     if choice is None:
-        if torch.cuda.is_current_stream_capturing():
-            return k11()
-        times = {}
-        for name, fn in (('k11', k11), ('miopen', miopen)):
-            fn()  # warm (MIOpen find / compile)
-            start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            start.record()
-            for _ in range(3):
-                fn()
-            end.record()
-            end.synchronize()
-            times[name] = start.elapsed_time(end)
-        import torch.distributed as dist
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            # every rank must run the same algorithm: sum the timings over ranks
-            dev = 'cpu' if dist.get_backend() == 'gloo' else dy.device
-            t = torch.tensor([times['k11'], times['miopen']], dtype=torch.float64, device=dev)
-            dist.all_reduce(t)
-            times = {'k11': float(t[0]), 'miopen': float(t[1])}
-        choice = min(times, key=times.get)
-        _WGRAD_CHOICE[key] = choice
+        _WGRAD_PENDING.setdefault(key, (dy.dtype, xb.dtype, wb.dtype))
+        choice = 'k11'
     with _Logged('wgrad', choice, fl, desc):
         return k11() if choice == 'k11' else miopen()
+
+
+def routing_table():
+    """The autotuned routing decisions so far (for logs / bench jsonl rows)."""
+    return {'wgrad': {repr(k[:6]): v for k, v in _WGRAD_CHOICE.items()},
+            'deconv': {repr(k): v for k, v in _DECONV_CHOICE.items()}}
+
+
+def tune_pending():
+    """Resolve the per-shape kernel choices first seen since the last call (wgrad k11 vs MIOpen
+    under ``IMAGINAIRE_AMD_MFMA_WGRAD=auto``; FlowNet2 deconv k10 phases vs MIOpen): time each
+    candidate on scratch tensors of the recorded shapes and agree across ranks. Call it at the
+    same iteration on every rank, outside any forward / backward and outside graph capture."""
+    if not (_WGRAD_PENDING or _DECONV_PENDING) or torch.cuda.is_current_stream_capturing():
+        return 0
+    times = {}
+    dev = torch.device('cuda', torch.cuda.current_device())
+    cl = torch.channels_last
+    for key, (dyt, xt, wt) in sorted(_WGRAD_PENDING.items(), key=lambda kv: repr(kv[0])):
+        dys, xs, ws, stride, padding, dilation, cout, cin, wdt = key
+        dy = torch.randn(dys, device=dev).to(dyt).contiguous(memory_format=cl)
+        xb = torch.randn(xs, device=dev).to(xt).contiguous(memory_format=cl)
+        wb = torch.randn(ws, device=dev).to(wt).contiguous(memory_format=cl)
+        k11, miopen = _wgrad_fns(dy, xb, wb, stride, padding, dilation, cout, cin, wdt)
+        times[('w',) + key] = {'k11': _time_ms(k11), 'miopen': _time_ms(miopen)}
+    for key, fns in sorted(_DECONV_PENDING.items(), key=lambda kv: repr(kv[0])):
+        times[('d',) + key] = {name: _time_ms(fn) for name, fn in fns().items()}
+    times = _agree(times)
+    for k, t in times.items():
+        choice = min(t, key=t.get)
+        if k[0] == 'w':
+            _WGRAD_CHOICE[k[1:]] = choice
+        else:
+            _DECONV_CHOICE[k[1:]] = choice
+    n = len(times)
+    _WGRAD_PENDING.clear()
+    _DECONV_PENDING.clear()
+    return n
 
 
 def conv2d_act(x, weight, bias=None, stride=1, padding=0, dilation=1, slope=1.0):
@@ -661,6 +725,7 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1,
 
 _DECONV_MIN_PIX = int(os.environ.get('IMAGINAIRE_AMD_DECONV_MIN_PIX', 4096))
 _DECONV_CHOICE = {}
+_DECONV_PENDING = {}
 _DECONV_FORCE = os.environ.get('IMAGINAIRE_AMD_DECONV')  # 'k10s' / 'miopen': skip the tuning
 
 
@@ -706,6 +771,16 @@ def _deconv_phase_weights(weight, s, padding, cp, op):
     return wb, wts
 
 
+def _deconv_phase(x, weight, bias, st, pd, ho, wo):
+    """Transposed conv as the s*s k10 phase convolutions of :func:`_strided_dgrad`."""
+    cin, cout = weight.shape[0], weight.shape[1]
+    cp, op = _round_up(cin, 64), _out_pad(cout)
+    wb, wts = _deconv_phase_weights(weight, st[0], pd, cp, op)
+    y = _strided_dgrad(_pad_channels(x, cp, torch.bfloat16), wb, ho, wo, st[0], pd, wts)
+    y = y[:, :cout] if op != cout else y
+    return y if bias is None else y + bias.to(y.dtype).view(1, -1, 1, 1)
+
+
 def conv_transpose2d(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1,
                      dilation=1):
     """``F.conv_transpose2d``. A strided transposed conv is the data gradient of the strided
@@ -721,35 +796,39 @@ def conv_transpose2d(x, weight, bias=None, stride=1, padding=0, output_padding=0
         xn, wn = nhwc(x), nhwc(weight)
 
         def phase():
-            wb, wts = _deconv_phase_weights(weight, st[0], pd, cp, op)
-            y = _strided_dgrad(_pad_channels(x, cp, torch.bfloat16), wb, ho, wo, st[0], pd,
-                               wts)
-            y = y[:, :cout] if op != cout else y
-            return y if bias is None else y + bias.to(y.dtype).view(1, -1, 1, 1)
+            return _deconv_phase(x, weight, bias, st, pd, ho, wo)
 
         def miopen():
             return F.conv_transpose2d(xn, wn, bias, st, pd)
 
         # per-shape choice: MIOpen's backward-data solvers range from ~20 to ~140 TF/s over
         # FlowNet2's decoder shapes, the phase path from ~40 to ~100
-        # (profiles/deconv_probe_mi355x.txt)
+        # (profiles/deconv_probe_mi355x.txt). Unseen shapes run MIOpen until tune_pending()
+        # times both at a rank-uniform point and agrees the choice across ranks (a per-rank
+        # choice could give ranks different ground-truth flow at bf16 rounding level).
         key = (tuple(x.shape), tuple(weight.shape), st, pd)
         choice = _DECONV_FORCE or _DECONV_CHOICE.get(key)
-        if choice is None and torch.cuda.is_current_stream_capturing():
-            choice = 'miopen'
         if choice is None:
-            times = {}
-            for name, fn in (('k10s', phase), ('miopen', miopen)):
-                fn()
-                start, end = torch.cuda.Event(enable_timing=True), \
-                    torch.cuda.Event(enable_timing=True)
-                start.record()
-                for _ in range(3):
-                    fn()
-                end.record()
-                end.synchronize()
-                times[name] = start.elapsed_time(end)
-            choice = _DECONV_CHOICE[key] = min(times, key=times.get)
+            if key not in _DECONV_PENDING:
+                shapes = (tuple(x.shape), x.dtype, weight.detach(), bias, st, pd)
+
+                def fns(shapes=shapes):
+                    xs, xdt, w, b, st_, pd_ = shapes
+                    xt = torch.randn(xs, device=w.device).to(xdt)
+                    cin_, cout_, kh_, kw_ = w.shape
+                    ho_ = (xs[2] - 1) * st_[0] - 2 * pd_[0] + kh_
+                    wo_ = (xs[3] - 1) * st_[1] - 2 * pd_[1] + kw_
+
+                    def ph():
+                        with torch.no_grad():
+                            return _deconv_phase(xt, w, b, st_, pd_, ho_, wo_)
+
+                    def mi():
+                        with torch.no_grad():
+                            return F.conv_transpose2d(nhwc(xt), nhwc(w), b, st_, pd_)
+                    return {'k10s': ph, 'miopen': mi}
+                _DECONV_PENDING[key] = fns
+            choice = 'miopen'
         fl = 2.0 * x.shape[0] * x.shape[2] * x.shape[3] * weight.numel()
         with _Logged('deconv', choice, fl, _gemm_desc(x, weight, st, pd)):
             return phase() if choice == 'k10s' else miopen()

@@ -15,6 +15,8 @@ activation is a leaky slope (1.0 = identity, 0.0 = relu, 0.2 = the reference's
 reference below runs. SyncBN exchanges per-rank (count, mean, var) with one
 all-gather in forward and Σg, Σg·x̂ with one all-reduce in backward.
 """
+import os
+
 import torch
 import torch.distributed as dist
 import torch.nn.functional as F
@@ -26,6 +28,15 @@ def _world(group):
     if not (dist.is_available() and dist.is_initialized()):
         return 1
     return dist.get_world_size(group)
+
+
+def sync_active(group):
+    """True when sync-BN exchanges statistics: more than one rank, or a process group of ANY
+    size with ``IMAGINAIRE_AMD_FORCE_DIST=1`` (exercises the collective path — including
+    under hipGraph capture — on a one-GPU RCCL world, tests/test_graph_gpu.py)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    return dist.get_world_size(group) > 1 or os.environ.get('IMAGINAIRE_AMD_FORCE_DIST') == '1'
 
 
 def _merge_stats(cnt, mean, var, group):
@@ -82,7 +93,7 @@ def prefetch_sync_stats(x, eps, group):
     """Compute this rank's batch statistics of ``x`` and START their all-gather (async); the
     sync-BN forward that later normalises ``x`` joins it. No-op unless the HIP path runs with
     more than one rank."""
-    if not (_ext.use_native(x) and _world(group) > 1 and x.dim() == 4):
+    if not (_ext.use_native(x) and sync_active(group) and x.dim() == 4):
         return
     key = _stats_key(x, eps, group, True)
     if getattr(x, '_iamd_bn_stats', (None,))[0] == key:
@@ -117,9 +128,10 @@ def _expand_mod(t, x):
 
 
 class _NormCfg:
-    __slots__ = ('mode', 'training', 'momentum', 'eps', 'slope', 'group', 'use_batch_stats')
+    __slots__ = ('mode', 'training', 'momentum', 'eps', 'slope', 'group', 'use_batch_stats',
+                 'deferred')
 
-    def __init__(self, mode, training, momentum, eps, slope, group):
+    def __init__(self, mode, training, momentum, eps, slope, group, deferred=None):
         self.mode = mode
         self.training = training
         self.momentum = momentum
@@ -127,6 +139,67 @@ class _NormCfg:
         self.slope = slope
         self.group = group
         self.use_batch_stats = mode == 'instance' or (mode in ('batch', 'sync_batch') and training)
+        self.deferred = deferred
+
+
+# ---- asynchronous sync-BN backward -------------------------------------------------------
+# The data gradient of a sync-BN layer needs the GLOBAL Σg and Σg·x̂; the γ|β gradient and the
+# γ|β / mlp convolution backward do not. The norm's backward therefore starts the all-reduce
+# of its local sums (async) and hands the rest of the data-gradient computation to a join node
+# inserted on the norm's input BEFORE the γ|β convolutions in the forward
+# (:func:`defer_sync_bwd`): autograd runs nodes in decreasing creation order, so the γ|β and
+# mlp convolution backward run between the launch and the join, while the sums ride xGMI.
+
+class DeferredSyncBwd(object):
+    """Hand-off between a sync-BN norm's backward and its join node."""
+    __slots__ = ('args', 'work', 'sums')
+    completed = 0  # joins that finished a deferred data gradient (tests / diagnostics)
+
+    def __init__(self):
+        self.args = None
+        self.work = None
+        self.sums = None
+
+
+class _SyncBwdJoin(torch.autograd.Function):
+    """Identity on the norm input; its backward finishes the data gradient that the norm's
+    backward deferred (waits for the all-reduce, then one ``norm_bwd_apply`` pass)."""
+
+    @staticmethod
+    def forward(ctx, x, holder):
+        ctx.holder = holder
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        h = ctx.holder
+        if h.args is None:  # the norm computed dx itself (no deferral happened)
+            return g, None
+        h.work.wait()
+        x, dout, scale, shift, mean, rstd, k1, M, gamma_v, beta_v, slope = h.args
+        s = h.sums
+        k2 = (s[0:1] / M).contiguous()
+        k3 = (s[1:2] / M).contiguous()
+        h.args = h.work = h.sums = None
+        DeferredSyncBwd.completed += 1
+        dx = _ext.ext().norm_bwd_apply(x, dout, scale, shift, mean, rstd, k1, k2, k3,
+                                       gamma_v, beta_v, slope)
+        return dx, None
+
+
+def defer_sync_bwd(x):
+    """``(x', holder)``: x' is x behind a join node whose backward completes the sync-BN data
+    gradient of the norm that consumes x' with ``deferred=holder``. Call it before building the
+    norm's γ|β branch. Inactive (returns ``(x, None)``) off the HIP path or at one rank."""
+    if not (_ext.use_native(x) and x.requires_grad and torch.is_grad_enabled() and
+            x.dim() == 4):
+        return x, None
+    holder = DeferredSyncBwd()
+    x1 = _SyncBwdJoin.apply(x, holder)
+    st = getattr(x, '_iamd_bn_stats', None)
+    if st is not None:  # the prefetched statistics exchange belongs to the same values
+        x1._iamd_bn_stats = st
+    return x1, holder
 
 
 class _FusedNormActFn(torch.autograd.Function):
@@ -151,7 +224,7 @@ class _FusedNormActFn(torch.autograd.Function):
             shift = bf.reshape(1, C).contiguous() if bf is not None else torch.zeros_like(var)
             count = None
         elif cfg.use_batch_stats:
-            sync = cfg.mode == 'sync_batch' and _world(cfg.group) > 1
+            sync = cfg.mode == 'sync_batch' and sync_active(cfg.group)
             shareable = not per_instance and wf is None and bf is None
             key = _stats_key(x, cfg.eps, cfg.group, sync)
             cached = _cached_stats(x, key) if shareable else None
@@ -246,12 +319,19 @@ class _FusedNormActFn(torch.autograd.Function):
             k3 = (S2 / HW).contiguous()
         else:
             s = torch.stack([S1.sum(0), S2.sum(0)], 0)
-            if cfg.mode == 'sync_batch' and _world(cfg.group) > 1:
-                dist.all_reduce(s, group=cfg.group)
-                M = ctx.count.reshape(1, C)
-            else:
-                M = float(N * HW)
+            sync = cfg.mode == 'sync_batch' and sync_active(cfg.group)
+            M = ctx.count.reshape(1, C) if sync else float(N * HW)
             k1 = (rstd * (weight.float().reshape(1, C) if weight is not None else 1.0)).contiguous()
+            h = cfg.deferred
+            if sync and h is not None and ctx.needs_input_grad[0]:
+                # start the exchange and let the join node finish dx after the γ|β backward
+                h.work = dist.all_reduce(s, group=cfg.group, async_op=True)
+                h.sums = s
+                h.args = (x, dout, scale, shift, mean, rstd, k1, M, gamma_v, beta_v, cfg.slope)
+                dx = x.new_zeros(()).expand_as(x)  # placeholder: the join ignores it
+                return dx, dweight, dbias, dgamma, dbeta, dgb, None, None, None
+            if sync:
+                dist.all_reduce(s, group=cfg.group)
             k2 = (s[0:1] / M).contiguous()
             k3 = (s[1:2] / M).contiguous()
         mean_b, rstd_b = mean, rstd
@@ -269,7 +349,7 @@ def _reference(x, mode, weight, bias, gamma, beta, gb, running_mean, running_var
     elif mode == 'instance':
         y = F.instance_norm(x, weight=weight, bias=bias, eps=cfg.eps)
     else:
-        sync = mode == 'sync_batch' and _world(cfg.group) > 1
+        sync = mode == 'sync_batch' and sync_active(cfg.group)
         if cfg.training:
             xf = x.float()
             dims = (0, 2, 3)
@@ -333,7 +413,7 @@ class _SyncStats(torch.autograd.Function):
 
 def fused_norm_act(x, mode='batch', weight=None, bias=None, gamma=None, beta=None, gb=None,
                    running_mean=None, running_var=None, training=True, momentum=0.1,
-                   eps=1e-5, slope=1.0, process_group=None):
+                   eps=1e-5, slope=1.0, process_group=None, deferred=None):
     """``act((norm(x)·w + b)·(1+γ) + β)`` — see module docstring.
 
     ``momentum`` is the already-resolved exponential-average factor.
@@ -344,7 +424,7 @@ def fused_norm_act(x, mode='batch', weight=None, bias=None, gamma=None, beta=Non
         mode_eff = 'batch'
     else:
         mode_eff = mode
-    cfg = _NormCfg(mode_eff, training, momentum, eps, slope, process_group)
+    cfg = _NormCfg(mode_eff, training, momentum, eps, slope, process_group, deferred)
     if gamma is not None and gamma.dim() == 2 and x.shape[2] * x.shape[3] == 1:
         gamma = gamma.reshape(x.shape[0], x.shape[1], 1, 1)
         beta = beta.reshape(x.shape[0], x.shape[1], 1, 1)

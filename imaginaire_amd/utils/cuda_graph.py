@@ -191,11 +191,17 @@ def make_trainer_step(trainer, warmup=None, enabled=True, force=False):
     if warmup is None:
         warmup = int(os.environ.get('IMAGINAIRE_AMD_GRAPH_WARMUP', '3'))
 
+    from imaginaire_amd.ops.conv import tune_pending
+
     def step(data):
         for _ in range(cfg.trainer.dis_step):
             trainer.dis_update(data)
         for _ in range(cfg.trainer.gen_step):
             trainer.gen_update(data)
+        # per-shape kernel choices first seen in this iteration are timed and agreed across
+        # ranks here, between iterations (every rank runs the same iterations), never inside a
+        # backward; no-op once every shape is known and during graph capture
+        tune_pending()
 
     # force: try any trainer (the capture falls back to eager on failure); used by
     # scripts/bench_families.py --graph to evaluate families not yet marked capturable

@@ -12,6 +12,7 @@ MI355X mapping of the reference knobs:
     ``delay_allreduce`` semantics); 'torch' → stock torch DDP;
   * SyncBN layers get a dedicated communicator (parallel/groups.py).
 """
+import os
 import random
 
 import numpy as np
@@ -111,7 +112,10 @@ def _calculate_model_size(model):
 
 
 def _wrap_model(cfg, model):
-    if dist.is_available() and dist.is_initialized() and get_world_size() > 1:
+    # IMAGINAIRE_AMD_FORCE_DIST=1: the distributed wrappers (bucketed DDP, SyncBN exchanges)
+    # also on a one-rank process group, e.g. to capture and test the collective path on one GPU
+    force = os.environ.get('IMAGINAIRE_AMD_FORCE_DIST') == '1'
+    if dist.is_available() and dist.is_initialized() and (get_world_size() > 1 or force):
         assign_syncbn_group(model)
         ddp = getattr(cfg.trainer, 'distributed_data_parallel', 'pytorch')
         bucket_mb = getattr(cfg.trainer, 'ddp_bucket_mb', 256)
@@ -122,6 +126,7 @@ def _wrap_model(cfg, model):
                 model, device_ids=[torch.cuda.current_device()] if torch.cuda.is_available()
                 else None, find_unused_parameters=True, broadcast_buffers=False)
         return DistributedDataParallel(model, bucket_cap_mb=bucket_mb, comm_dtype=comm,
+                                       _force_distributed=force,
                                        overlap=(ddp != 'apex'),
                                        broadcast_buffers=getattr(cfg.trainer,
                                                                  'ddp_broadcast_buffers', False),

@@ -130,11 +130,9 @@ def main():
         train_step, graphed = make_trainer_step(trainer, warmup=max(1, args.warmup - 1),
                                                 force=True)
     else:
-        def train_step(data):
-            for _ in range(cfg.trainer.dis_step):
-                trainer.dis_update(data)
-            for _ in range(cfg.trainer.gen_step):
-                trainer.gen_update(data)
+        # the eager train.py step (incl. the between-iteration kernel-choice tuning)
+        from imaginaire_amd.utils.cuda_graph import make_trainer_step
+        train_step, graphed = make_trainer_step(trainer, enabled=False)
 
     def step(it):
         data = fresh(pool[it % len(pool)])

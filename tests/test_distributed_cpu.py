@@ -225,3 +225,34 @@ def test_ddp_unused_parameters_keep_grad_none():
     for _, r in res:
         for mode in ('local', 'global'):
             assert r[mode] == (True, True, True), (mode, r[mode])
+
+
+def _agree_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from imaginaire_amd.ops.conv import _agree
+    # rank-local timings disagree on which candidate is faster; the summed ones decide
+    times = {('w', (1, 2)): {'k11': 1.0 + 3 * rank, 'miopen': 2.0},
+             ('d', (3,)): {'k10s': 5.0 - 4 * rank, 'miopen': 3.0}}
+    out = _agree(times)
+    q.put((rank, {k: min(v, key=v.get) for k, v in out.items()}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_kernel_choice_agreed_across_ranks():
+    """Per-shape autotune results (k11 vs MIOpen wgrad, k10 phases vs MIOpen deconv) are summed
+    over ranks before the argmin, so every rank runs the same kernel."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_agree_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda t: t[0])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert res[0][1] == res[1][1]
+    assert res[0][1][('w', (1, 2))] == 'miopen'  # 1+4 > 2+2
+    assert res[0][1][('d', (3,))] == 'k10s'      # 5+1 = 6 == 3+3 -> min picks first (k10s)

@@ -128,6 +128,59 @@ def test_hip_syncbn_world2_matches_full_batch(dtype):
         assert torch.allclose(r[7], rv, atol=1e-4, rtol=1e-3)
 
 
+def _spade_norm_worker(rank, world, port, q):
+    """One SPADE norm layer (sync-BN, separate γ / β projections) on this rank's half batch."""
+    if world > 1:
+        dist = _init(rank, world, port)
+    else:
+        import faulthandler
+        import sys
+        faulthandler.dump_traceback_later(150, exit=True, file=sys.__stderr__)
+        torch.cuda.set_device(0)
+    from types import SimpleNamespace as NS
+    from imaginaire_amd.layers.activation_norm import SpatiallyAdaptiveNorm
+    from imaginaire_amd.ops.norm import DeferredSyncBwd
+    torch.manual_seed(3)
+    layer = SpatiallyAdaptiveNorm(64, 8, num_filters=32, kernel_size=3, separate_projection=True,
+                                  activation_norm_type='sync_batch',
+                                  activation_norm_params=NS(affine=False)).cuda()
+    layer = layer.to(memory_format=torch.channels_last)
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(4, 64, 16, 24, generator=g) * 1.5 + 0.3
+    lab = torch.randn(4, 8, 16, 24, generator=g)
+    gout = torch.randn(4, 64, 16, 24, generator=g)
+    n = 4 // world
+    sl = slice(rank * n, (rank + 1) * n)
+    cl = torch.channels_last
+    xr = x[sl].cuda().contiguous(memory_format=cl).requires_grad_(True)
+    y = layer(xr, lab[sl].cuda().contiguous(memory_format=cl), act_slope=0.2)
+    y.backward(gout[sl].cuda().contiguous(memory_format=cl))
+    torch.cuda.synchronize()
+    grads = {k: p.grad.detach().float().cpu() for k, p in layer.named_parameters()
+             if p.grad is not None}
+    q.put((rank, y.detach().float().cpu(), xr.grad.float().cpu(), grads,
+           DeferredSyncBwd.completed))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def test_spade_syncbn_async_backward_world2():
+    """The SPADE norm's deferred sync-BN data gradient (all-reduce overlapped with the γ|β /
+    mlp convolution backward, finished by the join node) == the full batch on one process."""
+    res = _spawn(_spade_norm_worker, 2)
+    ref = _spawn(_spade_norm_worker, 1)[0]
+    assert all(r[4] >= 1 for r in res), 'the deferred (async) sync-BN backward did not run'
+    y = torch.cat([r[1] for r in res])
+    dx = torch.cat([r[2] for r in res])
+    torch.testing.assert_close(y, ref[1], atol=2e-4, rtol=1e-3)
+    torch.testing.assert_close(dx, ref[2], atol=2e-4 * float(ref[2].abs().max()), rtol=1e-3)
+    for k, gr in ref[3].items():  # per-rank weight grads are partial sums of the batch loss
+        gs = res[0][3][k] + res[1][3][k]
+        torch.testing.assert_close(gs, gr, atol=1e-3 * float(gr.abs().max()) + 1e-5, rtol=2e-3,
+                                   msg=k)
+
+
 def _spade_grads(rank, world, comm):
     """G gradients of one SPADE G update (fp32, HIP path), rank's half of a 2-sample batch."""
     from imaginaire_amd.config import Config
