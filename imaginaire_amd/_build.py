@@ -154,7 +154,10 @@ def build(jobs=None, force=False, verbose=True):
     _, lib, _ = _torch_paths()
     cmd = [_hipcc(), '-shared', '-fPIC', '--offload-arch=' + ARCH] + sorted(objs) + [
         '-L' + lib, '-lc10', '-lc10_hip', '-ltorch', '-ltorch_cpu', '-ltorch_hip',
-        '-ltorch_python', '-Wl,-rpath,' + lib, '-o', TARGET + '.tmp']
+        '-ltorch_python', '-Wl,-rpath,' + lib,
+        # RCCL: resolves to the librccl.so.1 torch already loaded (same SONAME)
+        '-L' + os.path.join(os.environ.get('ROCM_PATH', '/opt/rocm'), 'lib'), '-lrccl',
+        '-o', TARGET + '.tmp']
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError('link failed: {}\n{}\n{}'.format(' '.join(cmd), r.stdout, r.stderr))

@@ -128,12 +128,27 @@ at::Tensor mt_sn_power(const std::vector<at::Tensor>& weights, const std::vector
                        const std::vector<at::Tensor>& vs, bool update, double eps);
 }  // namespace iamd
 
+namespace iamd {
+at::Tensor rccl_unique_id();
+int64_t rccl_comm_init(const at::Tensor& uid, int64_t rank, int64_t world);
+void rccl_comm_destroy(int64_t h);
+void rccl_all_reduce(const at::Tensor& t, int64_t h, int64_t op);
+void rccl_all_gather(const at::Tensor& out, const at::Tensor& in, int64_t h);
+}  // namespace iamd
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "imaginaire_amd gfx950 HIP kernels";
   iamd::register_lmdb(m);
   m.def("mt_sn_power", &iamd::mt_sn_power, "batched spectral-norm power iteration (k5b)");
   m.def("mt_sn_scale_cast", &iamd::mt_sn_scale_cast, "batched W/sigma -> bf16 (k5c)");
   m.def("profile_marker", &iamd::profile_marker, "named no-op kernel for trace phase splits");
+  m.def("rccl_unique_id", &iamd::rccl_unique_id, "RCCL unique id (128-byte CPU tensor)");
+  m.def("rccl_comm_init", &iamd::rccl_comm_init, "join an RCCL communicator; returns a handle");
+  m.def("rccl_comm_destroy", &iamd::rccl_comm_destroy, "destroy a native RCCL communicator");
+  m.def("rccl_all_reduce", &iamd::rccl_all_reduce,
+        "in-place all-reduce on the current stream (0 sum, 1 avg, 2 max), capturable");
+  m.def("rccl_all_gather", &iamd::rccl_all_gather,
+        "all-gather into a flat rank-major tensor on the current stream, capturable");
   m.def("conv2d_mfma", &iamd::conv2d_mfma, "MFMA implicit-GEMM NHWC conv + bias + act (k10)",
         py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("sh"), py::arg("sw"), py::arg("ph"),
         py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("slope"), py::arg("nb") = 1);

@@ -183,3 +183,26 @@ def refresh_batched_spectral_norm(net):
     group = getattr(net, '_iamd_sn_group', None)
     if group is not None:
         group(net, ())
+
+
+@torch.no_grad()
+def extra_sn_power_iteration(net):
+    """One more spectral-norm power iteration for every SN layer of ``net`` before its next
+    layer calls — so that a forward that calls each layer ONCE leaves u / v where a forward
+    that calls each layer TWICE (the reference SPADE discriminator's real then fake pass)
+    leaves them. With the batched group installed it is one more k5b pass (the layers then
+    consume the refreshed σ without iterating again); otherwise each layer's own iteration runs
+    once here and once more in its next call."""
+    group = getattr(net, '_iamd_sn_group', None)
+    if group is not None and group.entries and net.training:
+        w0 = getattr(group.entries[0][0], group.entries[0][1].name + '_orig')
+        if _ext.use_native(w0):
+            group(net, ())
+            return
+    if not net.training:
+        return
+    for m in net.modules():
+        for hook in list(m._forward_pre_hooks.values()):
+            if isinstance(hook, _TorchSN) and hasattr(m, hook.name + '_orig'):
+                hook._batched = None
+                _TorchSN.compute_weight(hook, m, do_power_iteration=True)

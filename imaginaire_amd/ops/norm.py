@@ -39,13 +39,45 @@ def sync_active(group):
     return dist.get_world_size(group) > 1 or os.environ.get('IMAGINAIRE_AMD_FORCE_DIST') == '1'
 
 
+def _native(group):
+    if not x_is_hip_group(group):
+        return None
+    from imaginaire_amd.parallel.rccl import native_comm_for
+    return native_comm_for(group)
+
+
+def x_is_hip_group(group):
+    return dist.is_available() and dist.is_initialized() and dist.get_backend(group) == 'nccl'
+
+
+def _all_reduce_sums(s, group, async_op=False):
+    """Σ over ranks of the sync-BN gradient sums (native RCCL when enabled: capturable)."""
+    nc = _native(group)
+    if nc is not None:
+        return nc.all_reduce(s, async_op=async_op)
+    return dist.all_reduce(s, group=group, async_op=async_op)
+
+
+def _gather_rows(allst, stacked, group, async_op=False):
+    """``allst[r] = stacked`` of rank r. RCCL: ONE flat all-gather (native communicator when
+    enabled, else all_gather_into_tensor); gloo (CPU tests) has no flat all-gather: list form
+    plus a copy after the wait."""
+    nc = _native(group)
+    if nc is not None:
+        return nc.all_gather(allst, stacked, async_op=async_op)
+    if dist.get_backend(group) != 'gloo':
+        return dist.all_gather_into_tensor(allst, stacked, group=group, async_op=async_op)
+    bufs = list(allst.unbind(0))
+    return dist.all_gather(bufs, stacked, group=group, async_op=async_op)
+
+
 def _merge_stats(cnt, mean, var, group):
     """All-gather per-rank (count, mean, var) [1, C] and merge (Chan)."""
-    stacked = torch.stack([cnt.reshape(-1), mean.reshape(-1), var.reshape(-1)], 0)
+    stacked = torch.stack([cnt.reshape(-1), mean.reshape(-1), var.reshape(-1)], 0).contiguous()
     world = _world(group)
-    bufs = [torch.empty_like(stacked) for _ in range(world)]
-    dist.all_gather(bufs, stacked.contiguous(), group=group)
-    allst = torch.stack(bufs, 0)  # [W, 3, C]
+    # one flat output tensor (not a list): a single collective, safe under hipGraph capture
+    allst = stacked.new_empty((world,) + tuple(stacked.shape))
+    _gather_rows(allst, stacked, group)  # [W, 3, C]
     n_i, m_i, v_i = allst[:, 0], allst[:, 1], allst[:, 2]
     n = n_i.sum(0)
     mean_g = (n_i * m_i).sum(0) / n.clamp_min(1)
@@ -71,16 +103,16 @@ def _cached_stats(x, key):
     if c is None or c[0] != key:
         return None
     if c[1] == 'pending':
-        work, bufs, local = c[2], c[3], c[4]
+        work, allst, local = c[2], c[3], c[4]
         work.wait()
-        stats = _merge_gathered(bufs, local)
+        stats = _merge_gathered(allst, local)
         x._iamd_bn_stats = (key, 'done', stats)
         return stats
     return c[2]
 
 
-def _merge_gathered(bufs, local=None):
-    allst = torch.stack(bufs, 0)  # [W, 3, C]
+def _merge_gathered(allst, local=None):
+    """Chan merge of the gathered per-rank (count, mean, var) rows ``allst`` [W, 3, C]."""
     n_i, m_i, v_i = allst[:, 0], allst[:, 1], allst[:, 2]
     n = n_i.sum(0)
     mean_g = (n_i * m_i).sum(0) / n.clamp_min(1)
@@ -100,9 +132,9 @@ def prefetch_sync_stats(x, eps, group):
         return
     count, mean, var, _, _ = _ext.ext().norm_stats(x, False, eps, None, None, True)
     stacked = torch.stack([count.reshape(-1), mean.reshape(-1), var.reshape(-1)], 0).contiguous()
-    bufs = [torch.empty_like(stacked) for _ in range(_world(group))]
-    work = dist.all_gather(bufs, stacked, group=group, async_op=True)
-    x._iamd_bn_stats = (key, 'pending', work, bufs, stacked)
+    allst = stacked.new_empty((_world(group),) + tuple(stacked.shape))
+    work = _gather_rows(allst, stacked, group, async_op=True)
+    x._iamd_bn_stats = (key, 'pending', work, allst, stacked)
 
 
 def _update_running(running_mean, running_var, mean, var, count, factor):
@@ -325,13 +357,13 @@ class _FusedNormActFn(torch.autograd.Function):
             h = cfg.deferred
             if sync and h is not None and ctx.needs_input_grad[0]:
                 # start the exchange and let the join node finish dx after the γ|β backward
-                h.work = dist.all_reduce(s, group=cfg.group, async_op=True)
+                h.work = _all_reduce_sums(s, cfg.group, async_op=True)
                 h.sums = s
                 h.args = (x, dout, scale, shift, mean, rstd, k1, M, gamma_v, beta_v, cfg.slope)
                 dx = x.new_zeros(()).expand_as(x)  # placeholder: the join ignores it
                 return dx, dweight, dbias, dgamma, dbeta, dgb, None, None, None
             if sync:
-                dist.all_reduce(s, group=cfg.group)
+                _all_reduce_sums(s, cfg.group)
             k2 = (s[0:1] / M).contiguous()
             k3 = (s[1:2] / M).contiguous()
         mean_b, rstd_b = mean, rstd

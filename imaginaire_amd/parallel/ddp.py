@@ -104,12 +104,18 @@ class DistributedDataParallel(nn.Module):
         self._hooks = []
         self._active = False
         self._avg = False
+        self._native = None
         if self.world > 1 or unused.get('_force_distributed', False):
             self.world = max(self.world, 1)
             self._force = True
             self._broadcast_state()
             self._build_buckets(bucket_cap_mb, first_bucket_mb)
-            self._avg = self._probe_avg()
+            # native RCCL communicator (parallel/rccl.py): bucket all-reduces without torch
+            # Work objects, so a step holding them can be captured into a hipGraph
+            from imaginaire_amd.parallel.rccl import native_comm_for
+            if self.buckets and self.buckets[0].flat.is_cuda:
+                self._native = native_comm_for(process_group)
+            self._avg = True if self._native is not None else self._probe_avg()
         else:
             self._force = False
 
@@ -237,13 +243,17 @@ class DistributedDataParallel(nn.Module):
             run1 = off + p.numel()
         if run0 is not None:
             b.flat[run0:run1].zero_()
-        op = dist.ReduceOp.AVG if self._avg else dist.ReduceOp.SUM
         if self.comm_dtype is not None and self.comm_dtype != b.flat.dtype:
             b.comm = b.flat.to(self.comm_dtype)
-            b.work = dist.all_reduce(b.comm, op=op, group=self.process_group, async_op=True)
+            buf = b.comm
         else:
             b.comm = None
-            b.work = dist.all_reduce(b.flat, op=op, group=self.process_group, async_op=True)
+            buf = b.flat
+        if self._native is not None:
+            b.work = self._native.all_reduce(buf, op='avg', async_op=True)
+        else:
+            op = dist.ReduceOp.AVG if self._avg else dist.ReduceOp.SUM
+            b.work = dist.all_reduce(buf, op=op, group=self.process_group, async_op=True)
 
     def finish(self):
         """Flush incomplete buckets, wait for all reductions, average."""

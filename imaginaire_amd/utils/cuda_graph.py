@@ -152,7 +152,10 @@ class GraphedStep(object):
         try:
             if self.stream is None:
                 self.stream = torch.cuda.Stream()
-            with torch.cuda.graph(g, stream=self.stream):
+            # thread-local capture mode: the RCCL process group's watchdog thread keeps polling
+            # its work events while a (seconds-long) step is being captured; under the default
+            # global mode those calls from another thread are refused and abort the process
+            with torch.cuda.graph(g, stream=self.stream, capture_error_mode='thread_local'):
                 self.step_fn(self.static)
         except Exception as e:  # noqa: BLE001 - any capture failure: stay eager
             if os.environ.get('IMAGINAIRE_AMD_GRAPH_DEBUG'):

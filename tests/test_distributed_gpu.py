@@ -156,9 +156,11 @@ def _spade_norm_worker(rank, world, port, q):
     y = layer(xr, lab[sl].cuda().contiguous(memory_format=cl), act_slope=0.2)
     y.backward(gout[sl].cuda().contiguous(memory_format=cl))
     torch.cuda.synchronize()
-    grads = {k: p.grad.detach().float().cpu() for k, p in layer.named_parameters()
+    # numpy, not torch tensors: a queued CPU tensor travels as a shared-memory fd that dies
+    # with this process (the world-1 reference exits right after the put)
+    grads = {k: p.grad.detach().float().cpu().numpy() for k, p in layer.named_parameters()
              if p.grad is not None}
-    q.put((rank, y.detach().float().cpu(), xr.grad.float().cpu(), grads,
+    q.put((rank, y.detach().float().cpu().numpy(), xr.grad.float().cpu().numpy(), grads,
            DeferredSyncBwd.completed))
     if world > 1:
         dist.barrier()
@@ -171,12 +173,14 @@ def test_spade_syncbn_async_backward_world2():
     res = _spawn(_spade_norm_worker, 2)
     ref = _spawn(_spade_norm_worker, 1)[0]
     assert all(r[4] >= 1 for r in res), 'the deferred (async) sync-BN backward did not run'
-    y = torch.cat([r[1] for r in res])
-    dx = torch.cat([r[2] for r in res])
-    torch.testing.assert_close(y, ref[1], atol=2e-4, rtol=1e-3)
-    torch.testing.assert_close(dx, ref[2], atol=2e-4 * float(ref[2].abs().max()), rtol=1e-3)
+    T = torch.from_numpy
+    y = torch.cat([T(r[1]) for r in res])
+    dx = torch.cat([T(r[2]) for r in res])
+    torch.testing.assert_close(y, T(ref[1]), atol=2e-4, rtol=1e-3)
+    torch.testing.assert_close(dx, T(ref[2]), atol=2e-4 * float(abs(ref[2]).max()), rtol=1e-3)
     for k, gr in ref[3].items():  # per-rank weight grads are partial sums of the batch loss
-        gs = res[0][3][k] + res[1][3][k]
+        gr = T(gr)
+        gs = T(res[0][3][k]) + T(res[1][3][k])
         torch.testing.assert_close(gs, gr, atol=1e-3 * float(gr.abs().max()) + 1e-5, rtol=2e-3,
                                    msg=k)
 

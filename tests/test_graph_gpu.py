@@ -172,6 +172,7 @@ def _dist_capture_worker(port, q, tmp):
     tr = get_trainer(cfg, *nets, train_data_loader=[], val_data_loader=None)
     tr.net_G_module.style_encoder.freeze_random = True
     assert isinstance(tr.net_G, DistributedDataParallel) and tr.net_G._force
+    assert tr.net_G._native is not None, 'GRAPH=force should select the native RCCL comm'
     n = 4
     batches = _batches(cfg, n + 1)
     step, graphed = make_trainer_step(tr, warmup=2, enabled=True)
@@ -237,3 +238,78 @@ def test_graph_capture_with_rccl_collectives(tmp_path):
     assert abs(lg[0] - le[0]) <= 1e-3 * max(1.0, abs(le[0])), (lg, le)
     assert abs(lg[1] - le[1]) <= 5e-2 * max(1.0, abs(le[1])), (lg, le)
     assert den > 0 and num <= 0.1 * den, (num, den)
+
+
+def _native_comm_worker(port, q):
+    import faulthandler
+    import sys
+    import time
+    faulthandler.dump_traceback_later(170, exit=True, file=sys.__stderr__)
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK='0', WORLD_SIZE='1',
+                      IMAGINAIRE_AMD_NATIVE_COMM='1')
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group('nccl', rank=0, world_size=1, device_id=torch.device('cuda', 0))
+    from imaginaire_amd.parallel.rccl import native_comm_for
+    nc = native_comm_for(None)
+    res = {}
+    a = torch.arange(1000, dtype=torch.float32, device='cuda')
+    nc.all_reduce(a, 'avg')
+    b = torch.arange(64, dtype=torch.bfloat16, device='cuda')
+    nc.all_reduce(b, 'sum', async_op=True).wait()
+    out = torch.empty(1, 3, 8, device='cuda')
+    nc.all_gather(out, torch.ones(3, 8, device='cuda') * 7)
+    torch.cuda.synchronize()
+    res['eager'] = bool(torch.equal(a, torch.arange(1000, dtype=torch.float32, device='cuda'))
+                        and torch.equal(b, torch.arange(64, dtype=torch.bfloat16, device='cuda'))
+                        and bool((out == 7).all()))
+    # a LONG capture holding async native collectives (a torch Work created here would be
+    # polled by the ProcessGroupNCCL watchdog mid-capture and abort the process)
+    x = torch.ones(4096, device='cuda')
+    y = torch.zeros(4096, device='cuda')
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        y.copy_(x * 3)
+        nc.all_reduce(y, 'sum', async_op=True).wait()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s, capture_error_mode='thread_local'):
+        y.copy_(x * 3)
+        h = nc.all_reduce(y, 'sum', async_op=True)
+        time.sleep(3)
+        h.wait()
+        y.mul_(2)
+    for _ in range(3):
+        y.zero_()
+        g.replay()
+    torch.cuda.synchronize()
+    time.sleep(2)
+    res['captured'] = bool((y == 6).all())
+    q.put(res)
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_native_rccl_comm_eager_and_long_capture():
+    """csrc/rccl_comm.hip on a world-1 RCCL communicator: all-reduce (sum / avg, fp32 / bf16,
+    sync / async) and all-gather are exact; a seconds-long capture holding them replays
+    correctly and the process survives (no torch Work for the watchdog to poll)."""
+    import socket
+    import torch.multiprocessing as mp
+    sk = socket.socket()
+    sk.bind(('127.0.0.1', 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    p = ctx.Process(target=_native_comm_worker, args=(port, q))
+    p.start()
+    try:
+        res = q.get(timeout=120)
+    finally:
+        p.join(30)
+        if p.is_alive():
+            p.kill()
+    assert p.exitcode == 0
+    assert res == {'eager': True, 'captured': True}, res
