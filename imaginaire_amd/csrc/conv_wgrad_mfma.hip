@@ -71,7 +71,7 @@ __device__ __forceinline__ bf16x4 tr_read(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t)p);
 }
 
-template <int BNO, int BC, bool ROWS>
+template <int BNO, int BC, bool ROWS, int NST>
 __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma(WgradArgs a) {
   // The buffer-resource builtins have no host form; the host pass only needs the launch stub.
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -83,9 +83,10 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma(WgradArgs a) {
   constexpr int LA = kBP * CPA / kThreads;        // glds per thread (dy tile)
   constexpr int LX = kBP * CPX / kThreads;        // glds per thread (x tile)
   constexpr int RSA = kThreads / CPA, RSX = kThreads / CPX;  // rows per glds round
-  __shared__ __attribute__((aligned(16))) char smem[2 * kStage];
+  __shared__ __attribute__((aligned(16))) char smem[NST * kStage];
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   const int wm = wid >> 1, wn = wid & 1;
   const int tiles = a.KK * a.nNt * a.nCt;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -201,15 +202,8 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma(WgradArgs a) {
     return row * RX + ((((colblk + (p >> 1)) ^ swz<RX>(row))) << 4) + ((p & 1) << 3);
   };
 
-  issue(ks0, 0);
-  for (int ks = ks0; ks < ks1; ++ks) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (ks + 1 < ks1) {
-      advance();
-      issue(ks + 1, (ks + 1 - ks0) & 1);
-    }
-    const char* As = smem + ((ks - ks0) & 1) * kStage;
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * kStage;
     const char* Xs = As + kAbytes;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -234,6 +228,42 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma(WgradArgs a) {
 #pragma unroll
         for (int j = 0; j < NI; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], xf[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  if constexpr (NST == 2) {
+    issue(ks0, 0);
+    for (int ks = ks0; ks < ks1; ++ks) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (ks + 1 < ks1) {
+        advance();
+        issue(ks + 1, (ks + 1 - ks0) & 1);
+      }
+      compute((ks - ks0) & 1);
+    }
+  } else {
+    // three-stage ring, counted vmcnt (LA + LX glds per thread per stage), raw barrier: see
+    // conv_wgrad_mfma_mt
+    const int nks = ks1 - ks0;
+    issue(ks0, 0);
+    if (nks > 1) {
+      advance();
+      issue(ks0 + 1, 1);
+    }
+    int rb = 0;
+    for (int it = 0; it < nks; ++it) {
+      if (it + 1 < nks)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LA + LX) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (it + 2 < nks) {
+        advance();
+        issue(ks0 + it + 2, rb == 0 ? 2 : rb - 1);
+      }
+      compute(rb);
+      rb = rb == 2 ? 0 : rb + 1;
     }
   }
 
@@ -263,7 +293,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma(WgradArgs a) {
 // fragments are read from LDS once for all taps. Accumulators: KW x (BNO/2 x BC/2) per wave
 // (tiles: 3 taps 128 x 64, 5 / 7 taps 64 x 64 — the 256-VGPR budget of 2 waves / SIMD, no
 // spills).
-template <int BNO, int BC, int NT>
+template <int BNO, int BC, int NT, int NST>
 __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma_mt(WgradArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   constexpr int RA = BNO * 2, RX = BC * 2;        // image row bytes
@@ -277,9 +307,10 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma_mt(WgradArgs a) {
   constexpr int LA = kBP * CPA / kThreads;
   constexpr int LX = kBP * CPX / kThreads;
   constexpr int RSA = kThreads / CPA, RSX = kThreads / CPX;
-  __shared__ __attribute__((aligned(16))) char smem[2 * kStage];
+  __shared__ __attribute__((aligned(16))) char smem[NST * kStage];
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   const int wm = wid >> 1, wn = wid & 1;
   const int tiles = a.KK / a.KW * a.nNt * a.nCt;    // (ky, n-tile, c-tile)
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -369,15 +400,9 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma_mt(WgradArgs a) {
     return row * RX + ((((colblk + (p >> 1)) ^ swz<RX>(row))) << 4) + ((p & 1) << 3);
   };
 
-  issue(ks0, 0);
-  for (int ks = ks0; ks < ks1; ++ks) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (ks + 1 < ks1) {
-      advance();
-      issue(ks + 1, (ks + 1 - ks0) & 1);
-    }
-    const char* As = smem + ((ks - ks0) & 1) * kStage;
+  // one k-step of MFMAs on the staged LDS buffer ``buf``
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * kStage;
     const char* Xs = As + kAbytes;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -407,6 +432,52 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma_mt(WgradArgs a) {
             acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], xf[j], acc[t][i][j],
                                                                    0, 0, 0);
       }
+    }
+  };
+
+  if constexpr (NST == 2) {
+    // two LDS buffers: every k-step drains its DMA (vmcnt(0) + barrier) before the MFMAs;
+    // the second co-resident block hides the wait
+    issue(ks0, 0);
+    for (int ks = ks0; ks < ks1; ++ks) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (ks + 1 < ks1) {
+        advance();
+        issue(ks + 1, (ks + 1 - ks0) & 1);
+      }
+      compute((ks - ks0) & 1);
+    }
+  } else {
+    // three-stage ring (cdna_hip_programming.md "Pipelining across barriers"): the DMA of
+    // k-step it+1 stays in flight across the barrier of k-step it, retired by a counted
+    // vmcnt (this wave's glds per stage: LA + LX, plus the halo piece on wave 0) — never 0
+    // inside the loop — and a raw s_barrier (a __syncthreads fence would drain it). The
+    // barrier of k-step it also tells every wave that buffer (it+2) % 3 = (it-1) % 3 has been
+    // read, so the DMA of k-step it+2 is issued right after it.
+    const int nks = ks1 - ks0;
+    issue(ks0, 0);
+    if (nks > 1) {
+      advance();
+      issue(ks0 + 1, 1);
+    }
+    int rb = 0;
+    for (int it = 0; it < nks; ++it) {
+      if (it + 1 < nks) {
+        if (wid == 0)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LA + LX + 1) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LA + LX) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      if (it + 2 < nks) {
+        advance();
+        issue(ks0 + it + 2, rb == 0 ? 2 : rb - 1);
+      }
+      compute(rb);
+      rb = rb == 2 ? 0 : rb + 1;
     }
   }
 
@@ -525,15 +596,33 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
   IAMD_CHECK(gx < (1ll << 31), "conv2d_wgrad_mfma: grid too large");
   const dim3 grid((unsigned)gx, (unsigned)nb);
   const bool rows = Wo % kBP == 0;
+  // pipeline depth (IMAGINAIRE_AMD_WGRAD_STAGES = 2 | 3). Default 2: the 3-stage ring with
+  // counted vmcnt measured 0.98-1.01x the 2-stage loop on every SPADE-step shape
+  // (scripts/probe/wgrad_stages_probe.py, profiles/wgrad_stages_probe_mi355x.txt) — two
+  // co-resident blocks per CU already hide the DMA wait, so the extra LDS buys nothing.
+  int nst = 2;
+  if (const char* e = std::getenv("IMAGINAIRE_AMD_WGRAD_STAGES")) nst = std::atoi(e) == 3 ? 3 : 2;
   auto launch = [&](auto bv, auto cv) {
     constexpr int BNO = decltype(bv)::value;
     constexpr int BC = decltype(cv)::value;
-    if (rows)
-      hipLaunchKernelGGL((conv_wgrad_mfma<BNO, BC, true>), grid, dim3(kThreads),
-                         0, stream(), a);
-    else
-      hipLaunchKernelGGL((conv_wgrad_mfma<BNO, BC, false>), grid, dim3(kThreads),
-                         0, stream(), a);
+    // three stages only while two blocks still fit a CU's 160 KB of LDS (the 128 x 128 tile's
+    // 96 KB ring would halve the resident blocks)
+    constexpr bool fits3 = 2 * 3 * kBP * (BNO + BC) * 2 <= 160 * 1024;
+    if (nst == 3 && fits3) {
+      if (rows)
+        hipLaunchKernelGGL((conv_wgrad_mfma<BNO, BC, true, 3>), grid, dim3(kThreads), 0,
+                           stream(), a);
+      else
+        hipLaunchKernelGGL((conv_wgrad_mfma<BNO, BC, false, 3>), grid, dim3(kThreads), 0,
+                           stream(), a);
+    } else {
+      if (rows)
+        hipLaunchKernelGGL((conv_wgrad_mfma<BNO, BC, true, 2>), grid, dim3(kThreads), 0,
+                           stream(), a);
+      else
+        hipLaunchKernelGGL((conv_wgrad_mfma<BNO, BC, false, 2>), grid, dim3(kThreads), 0,
+                           stream(), a);
+    }
   };
   using I64 = std::integral_constant<int, 64>;
   using I128 = std::integral_constant<int, 128>;
@@ -541,8 +630,12 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
     constexpr int BNO = decltype(bv)::value;
     constexpr int BC = decltype(cv)::value;
     constexpr int NT = decltype(tv)::value;
-    hipLaunchKernelGGL((conv_wgrad_mfma_mt<BNO, BC, NT>), grid, dim3(kThreads),
-                       0, stream(), a);
+    if (nst == 3)
+      hipLaunchKernelGGL((conv_wgrad_mfma_mt<BNO, BC, NT, 3>), grid, dim3(kThreads), 0,
+                         stream(), a);
+    else
+      hipLaunchKernelGGL((conv_wgrad_mfma_mt<BNO, BC, NT, 2>), grid, dim3(kThreads), 0,
+                         stream(), a);
   };
   if (mt) {
     using T3 = std::integral_constant<int, 3>;
