@@ -13,10 +13,11 @@ Structure (same modules / state-dict names as the reference):
 * the decoder is a stack of ``HyperRes2dBlock``s whose SPADE and conv
   weights come from the weight generator.
 
-MI355X notes: every hyper convolution runs as ONE grouped MIOpen conv over
-the whole batch (layers/conv.py HyperConv2d) instead of a per-sample loop;
-SPADE normalisation + modulation + activation is the fused HIP kernel k1;
-warps use the k9 HIP kernel. The reference's ``num_downsamples_atn`` typo
+MI355X notes: every hyper convolution runs as ONE batched k10 MFMA launch over
+the whole batch (grid z = sample; layers/conv.py HyperConv2d, ops/conv.py
+conv2d_per_sample) instead of a per-sample loop; SPADE normalisation +
+modulation + activation is the fused HIP kernel k1; warps use the k9 HIP kernel;
+the reference-frame attention softmaxes its bf16 energy in place (no fp32 copy). The reference's ``num_downsamples_atn`` typo
 (fs_vid2vid.py:903 vs 906) is fixed so K > 1 works.
 """
 import copy
@@ -393,7 +394,11 @@ class WeightGenerator(nn.Module):
             encoded_ref = []
             for conv, conv_label in zip(encoded_image_ref, encoded_ref_label):
                 b, c, h, w = conv.size()
-                conv_label = torch.softmax(conv_label, dim=1)
+                if conv_label.is_cuda and conv_label.dtype == torch.bfloat16:
+                    with torch.autocast('cuda', enabled=False):  # bf16 I/O, fp32 accumulation
+                        conv_label = torch.softmax(conv_label, dim=1)
+                else:
+                    conv_label = torch.softmax(conv_label, dim=1)
                 # Σ_hw conv[b, c, hw] * softmax(label)[b, c', hw] as one batched GEMM
                 prod = torch.bmm(conv.reshape(b, c, h * w),
                                  conv_label.reshape(b, c, h * w).transpose(1, 2))
@@ -524,7 +529,16 @@ class AttentionModule(nn.Module):
             atn_query = self.attention_encode(label, 'atn_query')
             atn_key = atn_key.reshape(b, k, c, -1).permute(0, 1, 3, 2).reshape(b, -1, c)
             atn_query = atn_query.reshape(b, c, -1)
-            attention = torch.softmax(torch.bmm(atn_key, atn_query), dim=1)
+            energy = torch.bmm(atn_key, atn_query)
+            if energy.is_cuda and energy.dtype == torch.bfloat16:
+                # softmax over the K*HW reference positions on the bf16 energy itself (fp32
+                # accumulation inside the kernel): autocast would otherwise widen the
+                # B x KHW x HW matrix to fp32, softmax it in fp32 and narrow it back for the
+                # next bmm — three passes over the largest tensor of the generator
+                with torch.autocast('cuda', enabled=False):
+                    attention = torch.softmax(energy, dim=1)
+            else:
+                attention = torch.softmax(energy, dim=1)
         feats = in_features.reshape(b, k, c, h * w).permute(0, 2, 1, 3).reshape(b, c, -1)
         out = torch.bmm(feats, attention).reshape(b, c, h, w)
         atn_vis = attention.reshape(b, k, h * w, h * w).sum(2).reshape(b, k, h, w)
