@@ -95,7 +95,8 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_fwd_mfma(ConvA
   constexpr int kBLoads = BN / RS;            // DMA rounds for the B tile
   __shared__ __attribute__((aligned(16))) char smem[2 * kStage];
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // SGPR: the DMA's LDS base (M0)
   const int wm = wid >> 1, wn = wid & 1;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int mt = bid / a.nNt, nt = bid - mt * a.nNt;
@@ -114,22 +115,23 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_fwd_mfma(ConvA
   const int csw = (tid & 7) ^ (lrow & 7);
   const int HoWo = a.Ho * a.Wo;
   int a_off[4];
-  uint32_t a_rmask[4], a_cmask[4];  // bit ky / kx set when that filter row / column is inside
+  uint64_t a_tmask[4];  // bit (ky * KW + kx) set when that filter tap reads inside the image
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + lrow + RS * i;
     a_off[i] = 0;
-    a_rmask[i] = 0;
-    a_cmask[i] = 0;
+    a_tmask[i] = 0;
     if (m < a.M) {
       const int b = m / HoWo, r = m - b * HoWo;
       const int oh = r / a.Wo, ow = r - oh * a.Wo;
       const int ih0 = oh * a.sh - a.ph, iw0 = ow * a.sw - a.pw;
       a_off[i] = (((b * a.H + ih0) * a.W + iw0) * a.Cin + csw * 8) * 2;
-      for (int ky = 0; ky < a.KH; ++ky)
-        a_rmask[i] |= (uint32_t)((unsigned)(ih0 + ky * a.dh) < (unsigned)a.H) << ky;
-      for (int kx = 0; kx < a.KW; ++kx)
-        a_cmask[i] |= (uint32_t)((unsigned)(iw0 + kx * a.dw) < (unsigned)a.W) << kx;
+      for (int ky = 0; ky < a.KH; ++ky) {
+        if ((unsigned)(ih0 + ky * a.dh) >= (unsigned)a.H) continue;
+        for (int kx = 0; kx < a.KW; ++kx)
+          if ((unsigned)(iw0 + kx * a.dw) < (unsigned)a.W)
+            a_tmask[i] |= 1ull << (ky * a.KW + kx);
+      }
     }
   }
   const int wrow_bytes = a.nk * kBK * 2;  // = KH*KW*Cin*2
@@ -137,17 +139,26 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_fwd_mfma(ConvA
 #pragma unroll
   for (int i = 0; i < kBLoads; ++i) b_off[i] = (n0 + lrow + RS * i) * wrow_bytes + csw * 16;
 
+  // scalar (tap, channel block) cursor of the next k-step to stage, advanced incrementally
+  // (a division per k-step costs ~2 SALU per MFMA: profiles/pmc_conv_r2_mi355x.txt)
+  const int ks0 = blockIdx.y * a.kps;
+  const int ks1 = min(a.nk, ks0 + a.kps);
+  int cky, ckx, cc, ctap;
+  {
+    ctap = ks0 / a.cpt;
+    cc = (ks0 - ctap * a.cpt) * kBK;
+    cky = ctap / a.KW;
+    ckx = ctap - cky * a.KW;
+  }
+  const int row_step = a.dh * a.W * a.Cin * 2, col_step = a.dw * a.Cin * 2;
+  int ctoff = cky * row_step + ckx * col_step + cc * 2;
   auto issue = [&](int ks, int buf) {
-    const int tap = ks / a.cpt;
-    const int c0 = (ks - tap * a.cpt) * kBK;
-    const int ky = tap / a.KW, kx = tap - ky * a.KW;
-    const int tapoff = ((ky * a.dh * a.W + kx * a.dw) * a.Cin + c0) * 2;
     char* As = smem + buf * kStage;
     char* Bs = As + kAbytes;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const bool ok = (a_rmask[i] >> ky) & (a_cmask[i] >> kx) & 1u;
-      const int voff = ok ? a_off[i] + tapoff : kOobOffset;
+      const bool ok = (a_tmask[i] >> ctap) & 1u;
+      const int voff = ok ? a_off[i] + ctoff : kOobOffset;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(As + i * kLoadBytes + wid * 1024),
                                                16, voff, 0, 0, 0);
     }
@@ -155,6 +166,17 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_fwd_mfma(ConvA
     for (int i = 0; i < kBLoads; ++i)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)(Bs + i * kLoadBytes + wid * 1024),
                                                16, b_off[i], ks * kBK * 2, 0, 0);
+    cc += kBK;
+    ctoff += kBK * 2;
+    if (cc == a.Cin) {
+      cc = 0;
+      ++ctap;
+      if (++ckx == a.KW) {
+        ckx = 0;
+        ++cky;
+      }
+      ctoff = cky * row_step + ckx * col_step;
+    }
   };
 
   f32x4 acc[4][NI];
@@ -165,14 +187,13 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_fwd_mfma(ConvA
 
   // fragment read offsets (row & 7 == lane & 7 for every fragment row of this lane)
   const int frow = lane & 15, fsw = lane & 7, fk = lane >> 4;
-  const int ks0 = blockIdx.y * a.kps;
-  const int ks1 = min(a.nk, ks0 + a.kps);
-  issue(ks0, 0);
-  for (int ks = ks0; ks < ks1; ++ks) {
+  // unrolled over the two LDS buffers (b = 0, 1): the fragment addresses are loop-invariant
+  // registers plus immediate offsets
+  auto kstep = [&](int ks, int b) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (ks + 1 < ks1) issue(ks + 1, (ks + 1 - ks0) & 1);
-    const char* As = smem + ((ks - ks0) & 1) * kStage;
+    if (ks + 1 < ks1) issue(ks + 1, b ^ 1);
+    const char* As = smem + b * kStage;
     const char* Bs = As + kAbytes;
     if constexpr (VAR == 2) {
       bf16x8 af[2][4], bfr[2][NI];
@@ -215,6 +236,11 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_fwd_mfma(ConvA
         if constexpr (VAR == 1) __builtin_amdgcn_s_setprio(0);
       }
     }
+  };
+  issue(ks0, 0);
+  for (int ks = ks0; ks < ks1; ks += 2) {
+    kstep(ks, 0);
+    if (ks + 1 < ks1) kstep(ks + 1, 1);
   }
 
   if (a.part) {  // split-K: raw fp32 partials [S][nz][M][Cout], bias/act/bf16 in the reduce
@@ -901,7 +927,7 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
   IAMD_CHECK((int64_t)B * H * W * Cin * 2 < kOobOffset && w.numel() * 2 < kOobOffset &&
                  (int64_t)B * Ho * Wo * Cout < (1ll << 31),
              "conv2d_mfma: tensor too large for 32-bit buffer offsets");
-  IAMD_CHECK(KH <= 32 && KW <= 32, "conv2d_mfma: filter larger than 32x32");
+  IAMD_CHECK(KH * KW <= 64, "conv2d_mfma: filters with more than 64 taps are not supported");
   auto y = at::empty({B, Cout, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   at::Tensor bf;
   if (bias.has_value() && bias->defined()) {

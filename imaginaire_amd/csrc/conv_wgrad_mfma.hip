@@ -202,45 +202,56 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma(WgradArgs a) {
     return row * RX + ((((colblk + (p >> 1)) ^ swz<RX>(row))) << 4) + ((p & 1) << 3);
   };
 
+  // both 32-pixel halves of the k-step read up front, then the MFMAs (see conv_wgrad_mfma_mt)
   auto compute = [&](int buf) {
     const char* As = smem + buf * kStage;
     const char* Xs = As + kAbytes;
+    bf16x8 af[2][MI], xf[2][NI];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int r0 = kk * 32 + g * 8 + q;
-      bf16x8 af[MI], xf[NI];
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         const int cb = (wm * (BNO / 2) + i * 16) >> 3;
         const bf16x4 lo = tr_read(As + a_addr(r0, cb));
         const bf16x4 hi = tr_read(As + a_addr(r0 + 4, cb));
-        af[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        af[kk][i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
       }
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         const int cb = (wn * (BC / 2) + j * 16) >> 3;
         const bf16x4 lo = tr_read(Xs + x_addr(r0, cb));
         const bf16x4 hi = tr_read(Xs + x_addr(r0 + 4, cb));
-        xf[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        xf[kk][j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
       }
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NI; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], xf[j], acc[i][j], 0, 0, 0);
-    }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], xf[kk][j], acc[i][j],
+                                                              0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
   };
 
   if constexpr (NST == 2) {
-    issue(ks0, 0);
-    for (int ks = ks0; ks < ks1; ++ks) {
+    // unrolled over the two buffers: fragment addresses = invariant register + immediate
+    auto step = [&](int ks, int b) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (ks + 1 < ks1) {
         advance();
-        issue(ks + 1, (ks + 1 - ks0) & 1);
+        issue(ks + 1, b ^ 1);
       }
-      compute((ks - ks0) & 1);
+      compute(b);
+    };
+    issue(ks0, 0);
+    for (int ks = ks0; ks < ks1; ks += 2) {
+      step(ks, 0);
+      if (ks + 1 < ks1) step(ks + 1, 1);
     }
   } else {
     // three-stage ring, counted vmcnt (LA + LX glds per thread per stage), raw barrier: see
@@ -400,53 +411,67 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma_mt(WgradArgs a) {
     return row * RX + ((((colblk + (p >> 1)) ^ swz<RX>(row))) << 4) + ((p & 1) << 3);
   };
 
-  // one k-step of MFMAs on the staged LDS buffer ``buf``
+  // one k-step of MFMAs on the staged LDS buffer ``buf``. Every fragment of the k-step (both
+  // 32-pixel halves: MI dy + NT x NI x fragments each) is read into registers BEFORE the first
+  // MFMA, so the LDS latency is paid once per k-step and overlaps the first half's MFMAs,
+  // instead of a read -> lgkmcnt(0) -> 4 MFMAs stall per tap (what the compiler emits when the
+  // tap fragments share one register set: profiles/wgrad_sched_probe_mi355x.txt).
   auto compute = [&](int buf) {
     const char* As = smem + buf * kStage;
     const char* Xs = As + kAbytes;
+    bf16x8 af[2][MI], xf[2][NT][NI];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int r0 = kk * 32 + g * 8 + q;
-      bf16x8 af[MI];
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         const int cb = (wm * (BNO / 2) + i * 16) >> 3;
         const bf16x4 lo = tr_read(As + a_addr(r0, cb));
         const bf16x4 hi = tr_read(As + a_addr(r0 + 4, cb));
-        af[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        af[kk][i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
       }
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        bf16x8 xf[NI];
+      for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
           const int cb = (wn * (BC / 2) + j * 16) >> 3;
           const bf16x4 lo = tr_read(Xs + x_addr(r0 + t, cb));
           const bf16x4 hi = tr_read(Xs + x_addr(r0 + t + 4, cb));
-          xf[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          xf[kk][t][j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
         }
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
           for (int j = 0; j < NI; ++j)
-            acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], xf[j], acc[t][i][j],
-                                                                   0, 0, 0);
-      }
-    }
+            acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], xf[kk][t][j],
+                                                                   acc[t][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
   };
 
   if constexpr (NST == 2) {
     // two LDS buffers: every k-step drains its DMA (vmcnt(0) + barrier) before the MFMAs;
-    // the second co-resident block hides the wait
-    issue(ks0, 0);
-    for (int ks = ks0; ks < ks1; ++ks) {
+    // the second co-resident block hides the wait. The loop is unrolled over the two buffers
+    // so every fragment address is a loop-invariant register plus an immediate offset (no
+    // per-read address VALU).
+    auto step = [&](int ks, int b) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (ks + 1 < ks1) {
         advance();
-        issue(ks + 1, (ks + 1 - ks0) & 1);
+        issue(ks + 1, b ^ 1);
       }
-      compute((ks - ks0) & 1);
+      compute(b);
+    };
+    issue(ks0, 0);
+    for (int ks = ks0; ks < ks1; ks += 2) {
+      step(ks, 0);
+      if (ks + 1 < ks1) step(ks + 1, 1);
     }
   } else {
     // three-stage ring (cdna_hip_programming.md "Pipelining across barriers"): the DMA of
@@ -492,6 +517,239 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma_mt(WgradArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int n = n0 + wm * (BNO / 2) + i * 16 + g * 4 + r;
+          const int ci = c0 + wn * (BC / 2) + j * 16 + (lane & 15);
+          o[((size_t)n * a.KK + tap) * a.Cin + ci] = acc[t][i][j][r];
+        }
+  }
+#endif  // __HIP_DEVICE_COMPILE__
+}
+
+// ---- k11 v2: 128 x 128 x KW-tap tile, one wave per SIMD ----------------------------------
+//
+// The multi-tap kernel above keeps two blocks (8 waves) per CU, which caps a wave at 256 VGPRs
+// and its tile at 32 x 32 per tap (5 taps): every MFMA then needs ~0.6 KB of LDS fragment
+// reads, close to the CU's 1 KB-per-16x16x32-MFMA LDS budget once the DMA writes are added.
+// This kernel runs ONE 256-thread block per CU (one wave per SIMD, up to 512 VGPR/AGPR) with
+// a 64 (Cout) x 64 (Cin) x KW-tap accumulator per wave (KW = 5: 320 accumulators), so a
+// 32-pixel k-fragment of dy (4 fragments) is read once for all KW taps and every x fragment
+// feeds 4 MFMAs: ~0.3 KB of LDS reads per MFMA. The block owns 128 output x 128 input
+// channels of one filter row ky and stages, per 64-pixel k-step, the dy tile (64 px x 128 ch)
+// and ONE input window per output-row segment — R = 64 / WSEG segments of WSEG output pixels,
+// each needing WSEG + KW - 1 input pixels (rows padded to L: the k-fragment offsets stay
+// multiples of 16 rows, where the 16-B chunk swizzle repeats) — so each staged x byte feeds KW
+// taps. Output rows shorter than 64 pixels (16 x 32 / 32 x 64 maps, WSEG = 16 / 32) are
+// covered too: a 32-pixel k-fragment never straddles a segment. Staging is buffer_load ...
+// lds (zeros for padding pixels) into an NST-deep ring, drained by a counted vmcnt (never 0
+// in the loop) and a raw s_barrier, so the next k-steps' DMA stays in flight while this one
+// computes; the single wave per SIMD relies on that depth instead of a co-resident block.
+template <int NT, int BC, int WSEG, int NST>
+__global__ __launch_bounds__(kThreads, 1) void conv_wgrad_mfma_w4(WgradArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  constexpr int RB = 256;                                   // dy row bytes (128 channels)
+  constexpr int RX = BC * 2;                                // x row bytes
+  constexpr int NJ = BC / 32;                               // 16-channel x fragments per wave
+  constexpr int R = kBP / WSEG;                             // window segments per k-step
+  constexpr int L = WSEG == 64 ? 64 + NT - 1 : (WSEG + NT - 1 + 15) / 16 * 16;
+  constexpr int XRPR = 1024 / (BC * 2);                     // x rows per wave DMA instruction
+  constexpr int XROWS = (R * L + 4 * XRPR - 1) / (4 * XRPR) * (4 * XRPR);  // whole DMA rounds
+  constexpr int KKOFF = WSEG == 64 ? 32 : (WSEG == 32 ? L : 2 * L);  // rows of k-fragment 1
+  static_assert(KKOFF % 16 == 0, "k-fragment offset must keep the swizzle phase");
+  constexpr int kAbytes = kBP * RB;                         // 16 KB
+  constexpr int kXbytes = XROWS * RX;
+  constexpr int kStage = kAbytes + kXbytes;
+  constexpr int LA = kBP / 16;                              // glds per thread: dy (4)
+  constexpr int LX = XROWS / (4 * XRPR);                    // glds per thread: x window
+  static_assert(XROWS % (4 * XRPR) == 0, "window rows must fill whole DMA rounds");
+  __shared__ __attribute__((aligned(16))) char smem[NST * kStage];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tiles = (a.KK / a.KW) * a.nNt * a.nCt;          // (ky, n-tile, c-tile)
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / tiles;
+  const int tile = bid - split * tiles;
+  const int ky = tile / (a.nNt * a.nCt);
+  const int r2 = tile - ky * a.nNt * a.nCt;
+  const int nt = r2 / a.nCt, ct = r2 - nt * a.nCt;
+  const int n0 = nt * 128, c0 = ct * BC;
+  const int ks0 = split * a.kps;
+  const int ks1 = min(a.nks, ks0 + a.kps);
+
+  const __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__hip_bfloat16*>(a.dy), 0, a.dybytes, kBufCfg);
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__hip_bfloat16*>(a.x), 0, a.xbytes, kBufCfg);
+
+  // ---- DMA geometry: glds round i of wave w covers rows 16 i + 4 w + (lane >> 4), 16-B
+  // chunk (lane & 15) (lane-linear 1 KB per wave instruction = 4 rows of 256 B) ----------
+  const int drow = lane >> 4, dchunk = lane & 15;
+  int dy_off[LA];
+#pragma unroll
+  for (int i = 0; i < LA; ++i) {
+    const int row = i * 16 + wid * 4 + drow;
+    dy_off[i] = (row * a.Cout + n0 + ((dchunk ^ swz<RB>(row)) << 3)) * 2;
+  }
+  const int dy_step = kBP * a.Cout * 2;
+  // window rows: segment s = row / L (>= R: padding row), column j = row % L
+  int xseg[LX], xcol[LX], xch[LX];
+  {
+    const int xr = lane / (RX / 16), xc = lane % (RX / 16);
+#pragma unroll
+    for (int i = 0; i < LX; ++i) {
+      const int row = i * 4 * XRPR + wid * XRPR + xr;
+      xseg[i] = row / L;
+      xcol[i] = row - xseg[i] * L;
+      xch[i] = (c0 + ((xc ^ swz<RX>(row)) << 3)) * 2;
+    }
+  }
+  // scalar pixel cursor of the next k-step to stage: image sb, output row soh, column sow
+  const int HoWo = a.Ho * a.Wo;
+  int sb, soh, sow;
+  {
+    const int m = ks0 * kBP;
+    sb = m / HoWo;
+    const int r = m - sb * HoWo;
+    soh = r / a.Wo;
+    sow = r - soh * a.Wo;
+  }
+  const int rowbytes = a.W * a.Cin * 2;
+
+  auto issue = [&](int ks, int buf) {
+    char* As = smem + buf * kStage;
+    char* Xs = As + kAbytes;
+#pragma unroll
+    for (int i = 0; i < LA; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(dyr, (lds_ptr_t)(As + i * 4096 + wid * 1024), 16,
+                                               dy_off[i], ks * dy_step, 0, 0);
+    const int imgoff = sb * a.H * rowbytes;
+#pragma unroll
+    for (int i = 0; i < LX; ++i) {
+      const int ih = soh + xseg[i] - a.ph + ky * a.dh;        // segment s = output row soh + s
+      const int iw = sow + xcol[i] - a.pw;
+      const bool ok = xseg[i] < R && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          xrs, (lds_ptr_t)(Xs + i * 4096 + wid * 1024), 16,
+          ok ? imgoff + ih * rowbytes + iw * a.Cin * 2 + xch[i] : kOobOffset, 0, 0, 0);
+    }
+  };
+  auto advance = [&]() {
+    sow += kBP;
+    if (sow >= a.Wo) {  // WSEG < 64: a k-step covers R whole output rows
+      soh += WSEG == 64 ? 1 : R;
+      sow = 0;
+      if (soh >= a.Ho) { soh = 0; ++sb; }
+    }
+  };
+
+  f32x4 acc[NT][4][NJ];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // transposed-read lane geometry (see conv_wgrad_mfma): group g reads pixel rows 8g + q and
+  // 8g + q + 4 of a 32-pixel k-fragment, lane p's 8-byte quarter of a 16-channel block
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  auto addr = [&](int row, int colblk) {
+    return row * RB + ((((colblk + (p >> 1)) ^ swz<RB>(row))) << 4) + ((p & 1) << 3);
+  };
+  auto xaddr = [&](int row, int colblk) {
+    return row * RX + ((((colblk + (p >> 1)) ^ swz<RX>(row))) << 4) + ((p & 1) << 3);
+  };
+  // window row of k-fragment 0, pixel 8g + q (+4), tap 0
+  const int px0 = g * 8 + q;
+  const int wrow0 = (px0 / WSEG) * L + (px0 % WSEG);
+  const int wrow1 = ((px0 + 4) / WSEG) * L + ((px0 + 4) % WSEG);
+
+  // per 32-pixel half: its fragments are read while the previous half's MFMAs run
+  auto readkk = [&](const char* As, const char* Xs, int kk, bf16x8 (&af)[4],
+                    bf16x8 (&xf)[NT][NJ]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int cb = (wm * 64 + i * 16) >> 3;
+      const bf16x4 lo = tr_read(As + kk * 32 * RB + addr(px0, cb));
+      const bf16x4 hi = tr_read(As + kk * 32 * RB + addr(px0 + 4, cb));
+      af[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int cb = (wn * (BC / 2) + j * 16) >> 3;
+        const bf16x4 lo = tr_read(Xs + kk * KKOFF * RX + xaddr(wrow0 + t, cb));
+        const bf16x4 hi = tr_read(Xs + kk * KKOFF * RX + xaddr(wrow1 + t, cb));
+        xf[t][j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+  };
+  auto mfmas = [&](const bf16x8 (&af)[4], const bf16x8 (&xf)[NT][NJ]) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], xf[t][j], acc[t][i][j],
+                                                                 0, 0, 0);
+  };
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * kStage;
+    const char* Xs = As + kAbytes;
+    bf16x8 af0[4], xf0[NT][NJ], af1[4], xf1[NT][NJ];
+    readkk(As, Xs, 0, af0, xf0);
+    readkk(As, Xs, 1, af1, xf1);
+    mfmas(af0, xf0);
+    mfmas(af1, xf1);
+  };
+
+  // NST-deep ring: k-step it lives in slot it % NST; its DMA (LA + LX glds per thread) is
+  // retired by a counted vmcnt that leaves the NST - 2 younger stages in flight, and the
+  // barrier after it also tells every wave that slot (it - 1) % NST has been read, so the
+  // DMA of k-step it + NST - 1 goes there right away.
+  const int nks = ks1 - ks0;
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s) {
+    if (s < nks) {
+      if (s > 0) advance();
+      issue(ks0 + s, s);
+    }
+  }
+  auto body = [&](int it, int slot) {
+    const int ahead = min(NST - 2, nks - 1 - it);  // younger stages issued before this wait
+    if (ahead >= 2)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (LA + LX)) : "memory");
+    else if (ahead == 1)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LA + LX) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (it + NST - 1 < nks) {
+      advance();
+      issue(ks0 + it + NST - 1, (slot + NST - 1) % NST);
+    }
+    compute(slot);
+  };
+  // unrolled over the ring slots: fragment addresses are invariant registers + immediates
+  for (int it = 0; it < nks; it += NST) {
+#pragma unroll
+    for (int s = 0; s < NST; ++s)
+      if (it + s < nks) body(it + s, s);
+  }
+
+  // ---- fp32 partial slab [S][Cout][KK][Cin]: row n (4 per lane), column ci (16 lanes) ------
+  float* o = a.out + (size_t)split * a.Cout * a.KK * a.Cin;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int tap = ky * a.KW + t;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = n0 + wm * 64 + i * 16 + g * 4 + r;
           const int ci = c0 + wn * (BC / 2) + j * 16 + (lane & 15);
           o[((size_t)n * a.KK + tap) * a.Cin + ci] = acc[t][i][j][r];
         }
@@ -551,22 +809,48 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
   a.nCt = Cin / (bc128 ? 128 : 64);
   // multi-tap kernel: stride-1, undilated, whole-row k-steps, KW in {3, 5, 7}
   const char* mt_env = std::getenv("IMAGINAIRE_AMD_WGRAD_MT");
-  const bool mt = (mt_env == nullptr || mt_env[0] != '0') && Wo % kBP == 0 && sw == 1 &&
+  // v2 (one wave per SIMD, 128 x 128 x KW tile): stride 1, undilated, KW in {3, 5}, both
+  // channel counts multiples of 128, output rows of 16 / 32 pixels or multiples of 64 with
+  // whole k-steps per image (IMAGINAIRE_AMD_WGRAD_V2=0 disables it)
+  const char* v2_env = std::getenv("IMAGINAIRE_AMD_WGRAD_V2");
+  const int wseg = Wo % kBP == 0 ? 64 : (Wo == 32 || Wo == 16) ? Wo : 0;
+  const bool v2 = (v2_env == nullptr || v2_env[0] != '0') && nb == 1 && sh == 1 && sw == 1 &&
+                  dh == 1 && dw == 1 && (KW == 3 || KW == 5) && bno128 && wseg > 0 &&
+                  (Ho * Wo) % kBP == 0;
+  const bool mt = !v2 && (mt_env == nullptr || mt_env[0] != '0') && Wo % kBP == 0 && sw == 1 &&
                   dw == 1 && (KW == 3 || KW == 5 || KW == 7);
+  // x tile: 128 input channels for 3 taps (192 accumulators per wave), 64 for 5 taps (160) or
+  // when Cin % 128 != 0 — the 256 accumulation registers of a wave
+  const int v2_bc = (KW == 3 && bc128) ? 128 : 64;
+  if (v2) {
+    a.nNt = Cout / 128;
+    a.nCt = Cin / v2_bc;
+  }
   if (mt) {  // tiles sized to the 256-VGPR budget of 2 waves / SIMD without spills:
     // 3 taps 128 x 64 (or 64 x 64), 5 / 7 taps 64 x 64
     a.nNt = Cout / ((KW == 3 && bno128) ? 128 : 64);
     a.nCt = Cin / 64;
   }
-  const int tiles = (mt ? (int)KH : KK) * a.nNt * a.nCt;
+  const int tiles = ((mt || v2) ? (int)KH : KK) * a.nNt * a.nCt;
   // split-K factor: fill the chip in whole rounds of co-resident blocks (2 / 3 / 5 blocks
   // per CU for the 64 / 48 / 32 KB LDS variants): a 2.3-round grid leaves the last round a
   // third full (measured: 1200 blocks ran at 28% MFMA issue vs 44% for k10,
   // profiles/pmc_conv_mi355x.txt)
-  const int slots = (mt ? 512 : 256 * ((bno128 && bc128) ? 2 : (bno128 || bc128) ? 3 : 5)) /
+  const int slots = v2 ? 256 : (mt ? 512 : 256 * ((bno128 && bc128) ? 2 : (bno128 || bc128) ? 3 : 5)) /
                     (int)nb;
   int S = 1;
-  if (tiles < slots) {
+  if (v2) {
+    // one block per CU: the split count that fills whole rounds of 256 best, with at least
+    // 8 k-steps per block (the ring's prologue / epilogue amortised)
+    const int smax = std::max(1, std::min(1024, a.nks / 8));
+    double best = -1.0;
+    for (int s = 1; s <= smax; ++s) {
+      const int blocks = tiles * s;
+      const double eff = (double)blocks / ((double)ceil_div(blocks, slots) * slots);
+      if (eff > best + 0.02) { best = eff; S = s; }
+      if (blocks >= 4 * slots) break;
+    }
+  } else if (tiles < slots) {
     // up to 1024 splits: a 1x1 conv's gradient is ONE 64 x 64 tile reduced over ~10^6 pixels
     const int smax = std::max(1, std::min(1024, a.nks / 4));
     double best = -1.0;
@@ -637,7 +921,31 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
       hipLaunchKernelGGL((conv_wgrad_mfma_mt<BNO, BC, NT, 2>), grid, dim3(kThreads), 0,
                          stream(), a);
   };
-  if (mt) {
+  if (v2) {
+    auto lv2 = [&](auto tv, auto sv) {
+      constexpr int NT = decltype(tv)::value;
+      constexpr int WS = decltype(sv)::value;
+      if constexpr (NT == 3) {
+        if (v2_bc == 128) {
+          hipLaunchKernelGGL((conv_wgrad_mfma_w4<NT, 128, WS, 3>), grid, dim3(kThreads), 0,
+                             stream(), a);
+          return;
+        }
+      }
+      hipLaunchKernelGGL((conv_wgrad_mfma_w4<NT, 64, WS, 3>), grid, dim3(kThreads), 0,
+                         stream(), a);
+    };
+    using S64 = std::integral_constant<int, 64>;
+    using S32 = std::integral_constant<int, 32>;
+    using S16 = std::integral_constant<int, 16>;
+    auto by_seg = [&](auto tv) {
+      if (wseg == 64) lv2(tv, S64());
+      else if (wseg == 32) lv2(tv, S32());
+      else lv2(tv, S16());
+    };
+    if (KW == 3) by_seg(std::integral_constant<int, 3>());
+    else by_seg(std::integral_constant<int, 5>());
+  } else if (mt) {
     using T3 = std::integral_constant<int, 3>;
     using T5 = std::integral_constant<int, 5>;
     if (KW == 3) {

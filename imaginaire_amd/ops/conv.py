@@ -224,7 +224,7 @@ def mfma_eligible(x, w, stride, padding, dilation, groups):
     if cp * op * 3 > cin * cout * 4 and min(cin, cout) > 16 and cp * op > 2 * cin * cout:
         return False
     ho, wo = _out_hw(x.shape[2], x.shape[3], w.shape[2:], stride, padding, dilation)
-    if ho <= 0 or wo <= 0:
+    if ho <= 0 or wo <= 0 or w.shape[2] * w.shape[3] > 64:  # k10 tap masks are 64-bit
         return False
     # 32-bit buffer byte offsets (k10 < 2 GiB operands, k11 < 1 GiB)
     if x.shape[0] * cp * x.shape[2] * x.shape[3] * 2 >= (1 << 30) or \

@@ -27,8 +27,8 @@ sys.path.insert(0, os.path.dirname(HERE))
 def main():
     p = argparse.ArgumentParser()
     p.add_argument('--config', required=True)
-    p.add_argument('--steps', type=int, default=5)
-    p.add_argument('--warmup', type=int, default=2)
+    p.add_argument('--steps', type=int, default=20)
+    p.add_argument('--warmup', type=int, default=4)
     p.add_argument('--batch', type=int, default=None)
     p.add_argument('--seq-len', type=int, default=None,
                    help='video families: frames per training sequence')
@@ -149,11 +149,24 @@ def main():
         data = step(it)
         print('[bench_families] warmup %d done' % it, flush=True)
     sync()
+    if device.type == 'cuda':
+        try:  # steady-state marker for scripts/gpu/summarize_kernels.py (after warm-up/autotune)
+            from imaginaire_amd.ops import _ext
+            _ext.ext().profile_marker(1)
+        except Exception:  # noqa: BLE001 - the marker is a profiling aid only
+            pass
+    # per-iteration wall times (synchronised each iteration) -> median and spread; the mean over
+    # the whole timed window is reported too (what a throughput number over K steps means)
+    times = []
     t0 = time.perf_counter()
     for it in range(args.steps):
+        t1 = time.perf_counter()
         data = step(args.warmup + it)
-    sync()
+        sync()
+        times.append(time.perf_counter() - t1)
     dt = (time.perf_counter() - t0) / args.steps
+    st = sorted(times)
+    med = st[len(st) // 2] if len(st) % 2 else 0.5 * (st[len(st) // 2 - 1] + st[len(st) // 2])
     if args.op_sites and device.type == 'cuda':
         sys.path.insert(0, os.path.join(HERE, 'probe'))
         from op_sites import record_sites
@@ -188,6 +201,12 @@ def main():
         'resolution': '%dx%d' % (h, w), 'batch': bs, 'frames_per_sample': frames,
         'ms_per_iteration': round(dt * 1e3, 2),
         'samples_per_s': round(bs / dt, 3), 'frames_per_s': round(bs * frames / dt, 3),
+        'timed_iterations': args.steps, 'warmup': args.warmup,
+        'median_ms': round(med * 1e3, 2), 'min_ms': round(st[0] * 1e3, 2),
+        'max_ms': round(st[-1] * 1e3, 2),
+        'spread_pct': round(100.0 * (st[-1] - st[0]) / med, 2),
+        'median_frames_per_s': round(bs * frames / med, 3),
+        'routing': _routing(),
         'device': torch.cuda.get_device_name(0) if device.type == 'cuda' else 'cpu',
         'data': 'synthetic, random-init weights',
         'peak_mem_gb': round(torch.cuda.max_memory_allocated() / 2 ** 30, 2)
@@ -195,6 +214,18 @@ def main():
         'hipgraph': bool(graphed is not None and graphed.graph is not None),
         'losses': {k: round(float(v), 5) for k, v in trainer.gen_losses.items()
                    if torch.is_tensor(v) and v.numel() == 1}}), flush=True)
+
+
+def _routing():
+    """Autotuned kernel choices of this process (k11 vs MIOpen wgrad, FlowNet2 deconv path) so
+    run-to-run throughput differences can be attributed to routing."""
+    try:
+        from imaginaire_amd.ops import conv as conv_ops
+        r = conv_ops.routing_table()
+        return {k: {'n': len(v), 'counts': {c: list(v.values()).count(c) for c in set(v.values())}}
+                for k, v in r.items()}
+    except Exception:  # noqa: BLE001
+        return None
 
 
 if __name__ == '__main__':

@@ -712,14 +712,52 @@ def test_conv2d_wgrad_multitap(case):
         memory_format=torch.channels_last)
     got = _ext.ext().conv2d_wgrad_mfma(dy, x, k, k, 1, 1, p, p, 1, 1)
     os.environ['IMAGINAIRE_AMD_WGRAD_MT'] = '0'
+    os.environ['IMAGINAIRE_AMD_WGRAD_V2'] = '0'
     try:
         one = _ext.ext().conv2d_wgrad_mfma(dy, x, k, k, 1, 1, p, p, 1, 1)
     finally:
         os.environ.pop('IMAGINAIRE_AMD_WGRAD_MT')
+        os.environ.pop('IMAGINAIRE_AMD_WGRAD_V2')
     ref = torch.nn.grad.conv2d_weight(x.float(), (cout, cin, k, k), dy.float(), 1, p)
     scale = max(1.0, ref.abs().max().item())
     assert (got - ref).abs().max().item() <= 2e-3 * scale
     assert torch.allclose(got, one, atol=1e-3 * scale, rtol=1e-3)
+
+
+@pytest.mark.parametrize('case', [
+    # B, Cin, Cout, H, W, k, pad: the one-wave-per-SIMD 128 x 128 (x 3 taps) / 128 x 64 (x 5
+    # taps) k11 v2 over each output-row class (Wo multiple of 64, 32, 16)
+    (2, 128, 256, 6, 128, 3, 1),    # 3 taps, x tile 128, two k-steps per output row
+    (2, 128, 256, 16, 32, 3, 1),    # 3 taps, two output rows per k-step (WSEG 32)
+    (2, 256, 128, 8, 16, 3, 1),     # 3 taps, four output rows per k-step (WSEG 16)
+    (2, 192, 128, 4, 64, 5, 2),     # 5 taps, x tile 64 (Cin 192: SPADE mlp_shared)
+    (4, 128, 1024, 16, 32, 5, 2),   # 5 taps, SPADE gamma|beta at 16 x 32, split-K
+    (1, 128, 128, 12, 16, 5, 2),    # 5 taps, WSEG 16
+    (1, 128, 128, 10, 68, 5, 0),    # no padding: Wo = 64
+    (2, 64, 128, 33, 64, 3, 1),     # Cin 64, odd output-row count
+])
+def test_conv2d_wgrad_v2(case):
+    """k11 v2 (one block per CU, 64 x 64 x KW-tap accumulators per wave, per-segment input
+    windows) vs fp32 autograd and vs the 2-waves-per-SIMD kernels (IMAGINAIRE_AMD_WGRAD_V2=0)."""
+    import os
+    from imaginaire_amd.ops import _ext
+    B, cin, cout, H, W, k, p = case
+    torch.manual_seed(15)
+    x = torch.randn(B, cin, H, W, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    Ho, Wo = H + 2 * p - k + 1, W + 2 * p - k + 1
+    dy = torch.randn(B, cout, Ho, Wo, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    got = _ext.ext().conv2d_wgrad_mfma(dy, x, k, k, 1, 1, p, p, 1, 1)
+    os.environ['IMAGINAIRE_AMD_WGRAD_V2'] = '0'
+    try:
+        old = _ext.ext().conv2d_wgrad_mfma(dy, x, k, k, 1, 1, p, p, 1, 1)
+    finally:
+        os.environ.pop('IMAGINAIRE_AMD_WGRAD_V2')
+    ref = torch.nn.grad.conv2d_weight(x.float(), (cout, cin, k, k), dy.float(), 1, p)
+    scale = max(1.0, ref.abs().max().item())
+    assert (got - ref).abs().max().item() <= 2e-3 * scale
+    assert torch.allclose(got, old, atol=1e-3 * scale, rtol=1e-3)
 
 
 def test_cat0_view_of_adjacent_weights():
