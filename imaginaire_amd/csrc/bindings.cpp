@@ -94,7 +94,9 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
 at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t KH, int64_t KW,
                              int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh,
                              int64_t dw, int64_t out_cout, int64_t out_cin, bool out_bf16,
-                             int64_t nb);
+                             int64_t nb, int64_t variant);
+bool conv2d_wgrad_v2_eligible(const at::Tensor& dy, const at::Tensor& x, int64_t KH, int64_t KW,
+                              int64_t sh, int64_t sw, int64_t dh, int64_t dw, int64_t nb);
 // conv_tapsplit.hip
 at::Tensor conv_tap_sum(const at::Tensor& z, const c10::optional<at::Tensor>& bias, int64_t Cout,
                         int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t dh, int64_t dw);
@@ -155,7 +157,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv2d_wgrad_mfma", &iamd::conv2d_wgrad_mfma, "MFMA conv weight gradient (k11)",
         py::arg("dy"), py::arg("x"), py::arg("KH"), py::arg("KW"), py::arg("sh"), py::arg("sw"),
         py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("out_cout") = -1,
-        py::arg("out_cin") = -1, py::arg("out_bf16") = false, py::arg("nb") = 1);
+        py::arg("out_cin") = -1, py::arg("out_bf16") = false, py::arg("nb") = 1,
+        py::arg("variant") = 0);
+  m.def("conv2d_wgrad_v2_eligible", &iamd::conv2d_wgrad_v2_eligible,
+        "whether the k11 v2 (one wave per SIMD) kernel can run this weight gradient",
+        py::arg("dy"), py::arg("x"), py::arg("KH"), py::arg("KW"), py::arg("sh"), py::arg("sw"),
+        py::arg("dh"), py::arg("dw"), py::arg("nb") = 1);
   m.def("conv_tap_sum", &iamd::conv_tap_sum, "tap-split conv: sum of per-tap partials (+bias)");
   m.def("conv_tap_gather", &iamd::conv_tap_gather, "tap-split conv backward: dy -> per-tap dZ");
   m.def("conv_phase_scatter", &iamd::conv_phase_scatter,

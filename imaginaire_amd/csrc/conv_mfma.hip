@@ -743,6 +743,226 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v3(ConvArgs a) {
 #endif  // __HIP_DEVICE_COMPILE__
 }
 
+// ---- k10 v4: row-window implicit GEMM (stride 1), 256 x 128 tile, KW-tap input windows ----
+//
+// In v1 / v3 every filter tap re-stages its A tile (BM shifted input pixels x 64 channels) from
+// L2, so an input byte crosses the L2 -> LDS path KH * KW times. Here the 256 output pixels of a
+// block are R = 256 / SW output-row segments of SW pixels (SW = 256, or the whole row when
+// Wo divides 256), and for one filter row ky and 64-channel block the block stages ONE input
+// window per segment — SW + KW - 1 consecutive pixels — then runs the KW taps of that filter row
+// from it, tap kx reading the window rows shifted by kx (the 16-B chunk swizzle is keyed on the
+// LDS row, so a shifted 16-row fragment read stays conflict free). Only the weight tile (128
+// output channels x 64) is staged per tap. Per tap step: 16 KB of weights + 1/KW of a 40 KB
+// window, against 256 x 128 x 64 MACs: ~2.9x fewer L2 -> LDS bytes per MFMA than the v1 tile.
+//   8 waves as 4 (M) x 2 (N), 64 x 64 accumulators each; LDS: two window buffers (the next
+//   (ky, channel block)'s window is staged during the first tap of the current one) and a
+//   KW-slot weight ring (tap kx in slot kx, staged two tap steps ahead), 160 KB for KW = 5.
+//   DMA is buffer_load ... lds (zeros for padding pixels and past the k range); waits are
+//   counted vmcnt (2 or 7 glds per thread still in flight, never 0 in the loop) + raw s_barrier.
+// The data gradient of a stride-1 conv runs here too (flipped / transposed weight, as v1).
+template <int KW, bool HAS_BIAS>
+__global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v4(ConvArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  constexpr int BM = 256, BN = 128;
+  constexpr int kArows = 320;                     // window rows per buffer: 5 DMA rounds of 64
+  constexpr int kAbytes = kArows * kRowBytes;     // 40 KB
+  constexpr int kBbytes = BN * kRowBytes;         // 16 KB per tap slot
+  constexpr int kBoff = 2 * kAbytes;              // weight ring after the two windows
+  __shared__ __attribute__((aligned(16))) char smem[2 * kAbytes + KW * kBbytes];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid / a.nNt, nt = bid - mt * a.nNt;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int HoWo = a.Ho * a.Wo;
+  const int SW = a.Wo >= BM ? BM : a.Wo;          // pixels per output-row segment
+  const int L = SW + KW - 1;                      // window rows per segment
+  const int R = BM / SW;
+
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__hip_bfloat16*>(a.x), 0, a.xbytes, kBufCfg);
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__hip_bfloat16*>(a.w), 0, a.wbytes, kBufCfg);
+
+  // ---- window DMA: round r of wave w moves rows 64 r + 8 w + (lane >> 3), 16-B chunk
+  // (lane & 7) ^ (row & 7) of the source (the LDS write is lane-linear) -------------------
+  const int dr = lane >> 3;
+  const int csw = (lane & 7) ^ dr;                // row & 7 == dr for every staged row
+  const int rowbytes = a.W * a.Cin * 2;           // input row stride (bytes)
+  int a_off[5];
+  uint32_t a_km[5];                               // bit ky: this window row reads inside
+#pragma unroll
+  for (int r = 0; r < 5; ++r) {
+    const int row = r * 64 + wid * 8 + dr;
+    const int s = row / L, j = row - s * L;
+    a_off[r] = 0;
+    a_km[r] = 0;
+    if (s < R) {
+      const int m = m0 + s * SW;                  // first output pixel of segment s
+      const int b = m / HoWo, rr = m - b * HoWo;
+      const int oh = rr / a.Wo, ow0 = rr - oh * a.Wo;
+      const int ih0 = oh - a.ph, iw = ow0 - a.pw + j;
+      if ((unsigned)iw < (unsigned)a.W) {
+        a_off[r] = (b * a.H + ih0) * rowbytes + (iw * a.Cin + csw * 8) * 2;
+        for (int ky = 0; ky < a.KH; ++ky)
+          a_km[r] |= (uint32_t)((unsigned)(ih0 + ky) < (unsigned)a.H) << ky;
+      }
+    }
+  }
+  // weight DMA: rows 64 i + 8 w + (lane >> 3) of the 128-row tap tile
+  const int wrow_bytes = a.nk * kBK * 2;
+  int b_off[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) b_off[i] = (n0 + i * 64 + wid * 8 + dr) * wrow_bytes + csw * 16;
+
+  // ---- k range of this split in outer steps o = (ky, channel block) ------------------------
+  const int o0 = blockIdx.y * a.kps;
+  const int o1 = min(a.nk / KW, o0 + a.kps);      // nk = KH * KW * cpt: KH * cpt outer steps
+  // scalar cursors (filter row, channel offset) of outer step o (being computed) and o + 1,
+  // advanced once per outer step (no division in the loop)
+  int cky = o0 / a.cpt, ccc = (o0 - (o0 / a.cpt) * a.cpt) * kBK;
+  int nky = cky, ncc = ccc + kBK;
+  if (ncc == a.Cin) { ncc = 0; ++nky; }
+  auto issueA = [&](int o, int ky, int cc, int buf) {  // window of outer step o into buf
+    const bool live = o < o1;
+    const int koff = ky * rowbytes + cc * 2;
+    char* As = smem + buf * kAbytes;
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      const bool ok = live && ((a_km[r] >> (ky & 31)) & 1u);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          xrs, (lds_ptr_t)(As + r * 8192 + wid * 1024), 16, ok ? a_off[r] + koff : kOobOffset,
+          0, 0, 0);
+    }
+  };
+  auto issueB = [&](int o, int ky, int cc, int kx, int slot) {  // weight tap (ky, kx), block cc
+    const int soff = o < o1 ? ((ky * KW + kx) * a.Cin + cc) * 2 : kOobOffset;
+    char* Bs = smem + kBoff + slot * kBbytes;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)(Bs + i * 8192 + wid * 1024), 16,
+                                               b_off[i], soff, 0, 0);
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment rows: A = window row of output pixel wm*64 + i*16 + frow (+ kx), B = channel row
+  const int frow = lane & 15, fsw = lane & 7, fk = lane >> 4;
+  int wrow[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int p = wm * 64 + i * 16 + frow;
+    const int s = p / SW;
+    wrow[i] = s * L + (p - s * SW);
+  }
+  auto tapstep = [&](int abuf, int kx) {
+    const char* As = smem + abuf * kAbytes;
+    const char* Bs = smem + kBoff + kx * kBbytes;
+    bf16x8 af[2][4], bfr[2][4];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = wrow[i] + kx;
+        af[kk][i] = *reinterpret_cast<const bf16x8*>(
+            As + row * kRowBytes + (((kk * 4 + fk) ^ (row & 7)) << 4));
+      }
+      const int coff = ((kk * 4 + fk) ^ fsw) << 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bfr[kk][j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * 64 + j * 16 + frow) * kRowBytes +
+                                                      coff);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0,
+                                                              0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // one outer step (window buffer abuf static): KW tap steps; tap step q stages the weights of
+  // tap step q + 2 into its ring slot and, at kx == 0, the next outer step's window
+  auto outer = [&](int o, int abuf) {
+#pragma unroll
+    for (int kx = 0; kx < KW; ++kx) {
+      if (kx == 1)
+        asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // younger: window(o+1) 5 + weights 2
+      else
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // younger: the next weights 2
+      __builtin_amdgcn_s_barrier();
+      if (kx == 0) issueA(o + 1, nky, ncc, abuf ^ 1);
+      if (kx + 2 < KW) issueB(o, cky, ccc, kx + 2, kx + 2);
+      else issueB(o + 1, nky, ncc, kx + 2 - KW, kx + 2 - KW);
+      tapstep(abuf, kx);
+    }
+    cky = nky;
+    ccc = ncc;
+    ncc += kBK;
+    if (ncc == a.Cin) { ncc = 0; ++nky; }
+  };
+  // prologue: window of o0, weights of its taps 0 and 1
+  issueA(o0, cky, ccc, 0);
+  issueB(o0, cky, ccc, 0, 0);
+  issueB(o0, cky, ccc, 1, 1);
+  for (int o = o0; o < o1; o += 2) {
+    outer(o, 0);
+    if (o + 1 < o1) outer(o + 1, 1);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // trailing (zero) prefetches landed and every wave is done reading
+
+  if (a.part) {  // split-K: raw fp32 partials, bias/act/bf16 in conv_splitk_reduce
+    float* o = a.part + (size_t)blockIdx.y * a.M * a.Cout;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+          if (m < a.M) o[(size_t)m * a.Cout + n0 + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+        }
+    return;
+  }
+  char* E = smem;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int cl = wn * 64 + j * 16 + (lane & 15);
+    const float bv = HAS_BIAS ? a.bias[n0 + cl] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rl = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        float v = acc[i][j][r] + bv;
+        v = v > 0.f ? v : v * a.slope;
+        *reinterpret_cast<__hip_bfloat16*>(E + rl * kEpiStride + cl * 2) = __float2bfloat16(v);
+      }
+  }
+  __syncthreads();
+  const int ch = tid & 15, rr = tid >> 4;  // 16 chunks per row, 32 rows per pass
+#pragma unroll
+  for (int p = 0; p < BM / 32; ++p) {
+    const int rl = p * 32 + rr;
+    const int m = m0 + rl;
+    if (m < a.M) {
+      const uint4 v = *reinterpret_cast<const uint4*>(E + rl * kEpiStride + ch * 16);
+      *reinterpret_cast<uint4*>(a.y + out_row(a, m) * a.Cout + n0 + ch * 8) = v;
+    }
+  }
+#endif  // __HIP_DEVICE_COMPILE__
+}
+
 // y = act(sum_s part[s] + bias) in bf16, 8 channels per thread.
 __global__ void __launch_bounds__(256)
 conv_splitk_reduce(const float* __restrict__ part, const float* __restrict__ bias,
@@ -804,6 +1024,48 @@ void run_conv(ConvArgs& a, const at::Tensor& x) {
     S = std::max(1, std::min(S, a.nk));
     return ceil_div(a.nk, ceil_div(a.nk, S));
   };
+  // v4 (row-window, 256 x 128): stride 1, undilated, KW 3 / 5, whole 256-pixel tiles made of
+  // output-row segments (Wo a multiple of 256, or 16..128 dividing 256)
+  const bool v4_ok = a.nz == 1 && a.omode == 0 && a.sh == 1 && a.sw == 1 && a.dh == 1 &&
+                     a.dw == 1 && (KW == 3 || KW == 5) && KH <= 31 && bn128 &&
+                     (a.Wo % 256 == 0 || (a.Wo >= 16 && a.Wo <= 128 && 256 % a.Wo == 0)) &&
+                     ((int64_t)a.Ho * a.Wo) % 256 == 0;
+  // default: every eligible conv (1.02-1.52x v1 and 1.0-1.08x v3 on the SPADE-step shapes,
+  // the N = 128 data gradients 1.36-1.52x: profiles/conv_v4_probe_mi355x.txt)
+  if ((ver == 4 || ver == 0) && v4_ok) {
+    a.nNt = Cout / 128;
+    const int64_t tiles4 = (int64_t)(a.M / 256) * a.nNt;
+    const int nout = a.nk / KW;  // (filter row, channel block) outer steps
+    int S4 = 1;
+    if (tiles4 < 256 && nout >= 8) S4 = (int)std::min<int64_t>((256 + tiles4 - 1) / tiles4, nout / 4);
+    if (const char* e = std::getenv("IMAGINAIRE_AMD_CONV_SPLITK")) S4 = std::max(1, std::atoi(e));
+    S4 = std::max(1, std::min(S4, nout));
+    a.kps = ceil_div(nout, S4);
+    S4 = ceil_div(nout, a.kps);
+    at::Tensor part4;
+    a.part = nullptr;
+    if (S4 > 1) {
+      part4 = at::empty({(int64_t)S4 * a.M * Cout}, x.options().dtype(at::kFloat));
+      a.part = part4.data_ptr<float>();
+    }
+    const dim3 grid4((unsigned)tiles4, (unsigned)S4, 1);
+    if (KW == 5) {
+      if (a.bias) hipLaunchKernelGGL((conv_fwd_mfma_v4<5, true>), grid4, dim3(512), 0, stream(), a);
+      else hipLaunchKernelGGL((conv_fwd_mfma_v4<5, false>), grid4, dim3(512), 0, stream(), a);
+    } else {
+      if (a.bias) hipLaunchKernelGGL((conv_fwd_mfma_v4<3, true>), grid4, dim3(512), 0, stream(), a);
+      else hipLaunchKernelGGL((conv_fwd_mfma_v4<3, false>), grid4, dim3(512), 0, stream(), a);
+    }
+    if (S4 > 1) {
+      IAMD_LAUNCH_CHECK();
+      const int64_t MC = (int64_t)a.M * Cout;
+      const int blocks = (int)std::min<int64_t>((MC / 8 + 255) / 256, 8192);
+      hipLaunchKernelGGL(conv_splitk_reduce, dim3(blocks), dim3(256), 0, stream(), a.part, a.bias,
+                         a.y, S4, MC, Cout, a.slope, a);
+    }
+    IAMD_LAUNCH_CHECK();
+    return;
+  }
   bool v3 = false, v2 = false;
   if (ver == 3) {
     v3 = v3_ok;
@@ -812,8 +1074,11 @@ void run_conv(ConvArgs& a, const at::Tensor& x) {
   } else if (ver == 0 && v3_ok && v3_bn == 256) {
     // (the 512 x 128 variant measured 0.88-0.98x v1 on the 128-channel SPADE / dgrad shapes:
     // selectable with IMAGINAIRE_AMD_CONV_V=3 only)
+    // only grids that fill the chip without split-K: with the incremental-cursor v1 the split
+    // v3 grids measured 0.87-0.96x v1 (G head 2048 @ 16x32, up0 1024 @ 32x64), the unsplit
+    // ones 1.06-1.13x (profiles/conv_v1_cursor_probe_mi355x.txt)
     const int64_t t3 = (int64_t)ceil_div(a.M, v3_bm) * (Cout / v3_bn);
-    v3 = ceil_div(a.nk, split_for(t3, 256)) >= 40;
+    v3 = split_for(t3, 256) == 1 && a.nk >= 40;
   }
   int bm = 128;
   if (v3) {

@@ -305,7 +305,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma(WgradArgs a) {
 // (tiles: 3 taps 128 x 64, 5 / 7 taps 64 x 64 — the 256-VGPR budget of 2 waves / SIMD, no
 // spills).
 template <int BNO, int BC, int NT, int NST>
-__global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma_mt(WgradArgs a) {
+__global__ __launch_bounds__(kThreads, NT == 5 ? 3 : 2) void conv_wgrad_mfma_mt(WgradArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   constexpr int RA = BNO * 2, RX = BC * 2;        // image row bytes
   constexpr int kAbytes = kBP * RA;
@@ -416,19 +416,22 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma_mt(WgradArgs a) {
   // MFMA, so the LDS latency is paid once per k-step and overlaps the first half's MFMAs,
   // instead of a read -> lgkmcnt(0) -> 4 MFMAs stall per tap (what the compiler emits when the
   // tap fragments share one register set: profiles/wgrad_sched_probe_mi355x.txt).
-  auto compute = [&](int buf) {
+  // 5 taps: one half at a time (48 fragment registers instead of 96: 168 VGPRs, three blocks
+  // per CU — the 5x5 shapes whose tile grid needs no split-K fill 768 block slots in one round)
+  constexpr int NH = NT >= 5 ? 1 : 2;  // 32-pixel halves whose fragments are read together
+  auto compute_halves = [&](int buf, int h0) {
     const char* As = smem + buf * kStage;
     const char* Xs = As + kAbytes;
-    bf16x8 af[2][MI], xf[2][NT][NI];
+    bf16x8 af[NH][MI], xf[NH][NT][NI];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int r0 = kk * 32 + g * 8 + q;
+    for (int hh = 0; hh < NH; ++hh) {
+      const int r0 = (h0 + hh) * 32 + g * 8 + q;
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         const int cb = (wm * (BNO / 2) + i * 16) >> 3;
         const bf16x4 lo = tr_read(As + a_addr(r0, cb));
         const bf16x4 hi = tr_read(As + a_addr(r0 + 4, cb));
-        af[kk][i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        af[hh][i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
       }
 #pragma unroll
       for (int t = 0; t < NT; ++t)
@@ -437,21 +440,25 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma_mt(WgradArgs a) {
           const int cb = (wn * (BC / 2) + j * 16) >> 3;
           const bf16x4 lo = tr_read(Xs + x_addr(r0 + t, cb));
           const bf16x4 hi = tr_read(Xs + x_addr(r0 + t + 4, cb));
-          xf[kk][t][j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          xf[hh][t][j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
         }
     }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+    for (int hh = 0; hh < NH; ++hh)
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
           for (int j = 0; j < NI; ++j)
-            acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], xf[kk][t][j],
+            acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[hh][i], xf[hh][t][j],
                                                                    acc[t][i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
+  };
+  auto compute = [&](int buf) {
+#pragma unroll
+    for (int h0 = 0; h0 < 2; h0 += NH) compute_halves(buf, h0);
   };
 
   if constexpr (NST == 2) {
@@ -768,10 +775,27 @@ at::Tensor wgrad_finalize(const at::Tensor& part, int64_t S, int64_t Cop, int64_
 // when out_bf16; out_cout / out_cin < 0 keep the (padded) channel counts of dy / x. Cropping
 // and casting ride in the split-K reduction (wgrad_finalize) instead of separate copies.
 // nb > 1: nb independent weight gradients (per-sample weights) -> [nb * Cout, Cin, KH, KW].
+// k11 v2 eligibility (shape rules only; the default routing additionally prefers it for 3 taps
+// on <= 32-pixel output rows, and ops/conv.py times both per shape under autotuning)
+static bool wgrad_v2_shape_ok(int Cout, int Ho, int Wo, int64_t KW, int64_t sh, int64_t sw,
+                              int64_t dh, int64_t dw, int64_t nb) {
+  const int wseg = Wo % 64 == 0 ? 64 : (Wo == 32 || Wo == 16) ? Wo : 0;
+  return nb == 1 && sh == 1 && sw == 1 && dh == 1 && dw == 1 && (KW == 3 || KW == 5) &&
+         Cout % 128 == 0 && wseg > 0 && (Ho * Wo) % 64 == 0;
+}
+
+bool conv2d_wgrad_v2_eligible(const at::Tensor& dy, const at::Tensor& x, int64_t KH, int64_t KW,
+                              int64_t sh, int64_t sw, int64_t dh, int64_t dw, int64_t nb) {
+  return x.size(1) % 64 == 0 &&
+         wgrad_v2_shape_ok((int)dy.size(1), (int)dy.size(2), (int)dy.size(3), KW, sh, sw, dh, dw,
+                           nb);
+}
+
+// variant: 0 = default routing, 1 = never v2, 2 = v2 whenever eligible
 at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t KH, int64_t KW,
                              int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh,
                              int64_t dw, int64_t out_cout, int64_t out_cin, bool out_bf16,
-                             int64_t nb) {
+                             int64_t nb, int64_t variant) {
   IAMD_CHECK(dy.is_cuda() && x.is_cuda(), "conv2d_wgrad_mfma: CUDA tensors expected");
   IAMD_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16,
              "conv2d_wgrad_mfma: bf16 operands expected");
@@ -814,9 +838,13 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
   // whole k-steps per image (IMAGINAIRE_AMD_WGRAD_V2=0 disables it)
   const char* v2_env = std::getenv("IMAGINAIRE_AMD_WGRAD_V2");
   const int wseg = Wo % kBP == 0 ? 64 : (Wo == 32 || Wo == 16) ? Wo : 0;
-  const bool v2 = (v2_env == nullptr || v2_env[0] != '0') && nb == 1 && sh == 1 && sw == 1 &&
-                  dh == 1 && dw == 1 && (KW == 3 || KW == 5) && bno128 && wseg > 0 &&
-                  (Ho * Wo) % kBP == 0;
+  // default: 3 taps on <= 32-pixel output rows only (1.09-1.39x there, 0.70-0.89x elsewhere:
+  // profiles/wgrad_v2_probe_mi355x.txt); IMAGINAIRE_AMD_WGRAD_V2=force / variant 2 take every
+  // eligible shape, IMAGINAIRE_AMD_WGRAD_V2=0 / variant 1 none
+  const bool v2_force = variant == 2 || (v2_env != nullptr && v2_env[0] == 'f');
+  const bool v2_off = variant == 1 || (v2_env != nullptr && v2_env[0] == '0');
+  const bool v2 = !v2_off && (v2_force || (KW == 3 && Wo <= 32)) &&
+                  wgrad_v2_shape_ok(Cout, Ho, Wo, KW, sh, sw, dh, dw, nb);
   const bool mt = !v2 && (mt_env == nullptr || mt_env[0] != '0') && Wo % kBP == 0 && sw == 1 &&
                   dw == 1 && (KW == 3 || KW == 5 || KW == 7);
   // x tile: 128 input channels for 3 taps (192 accumulators per wave), 64 for 5 taps (160) or
@@ -836,7 +864,9 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
   // per CU for the 64 / 48 / 32 KB LDS variants): a 2.3-round grid leaves the last round a
   // third full (measured: 1200 blocks ran at 28% MFMA issue vs 44% for k10,
   // profiles/pmc_conv_mi355x.txt)
-  const int slots = v2 ? 256 : (mt ? 512 : 256 * ((bno128 && bc128) ? 2 : (bno128 || bc128) ? 3 : 5)) /
+  // (multi-tap: 2 blocks per CU, 3 for the 5-tap kernel's 168-VGPR build)
+  const int slots = v2 ? 256 : (mt ? (KW == 5 ? 768 : 512)
+                                   : 256 * ((bno128 && bc128) ? 2 : (bno128 || bc128) ? 3 : 5)) /
                     (int)nb;
   int S = 1;
   if (v2) {

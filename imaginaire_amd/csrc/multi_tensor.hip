@@ -289,14 +289,30 @@ sn_sigma_kernel(const TensorEntry* __restrict__ ents, const int* __restrict__ bl
   const int64_t start = (int64_t)chunk * kChunk;
   const int64_t end = min(e.numel, start + (int64_t)kChunk);
   float acc = 0.f;
-  // (row, column) walked incrementally: no 64-bit division per element
-  const int64_t i0 = start + threadIdx.x;
-  int64_t r = i0 / ncol;
-  int64_t c = i0 - r * ncol;
-  for (int64_t i = i0; i < end; i += kThreads) {
-    acc = fmaf(u[r] * W[i], v[c], acc);
-    c += kThreads;
-    while (c >= ncol) { c -= ncol; ++r; }
+  if ((ncol & 3) == 0 && (reinterpret_cast<uintptr_t>(W) & 15) == 0 &&
+      (reinterpret_cast<uintptr_t>(v) & 15) == 0) {
+    // 4 consecutive elements (one row: ncol % 4 == 0) per lane and trip, 16-B loads of W and v;
+    // chunk starts are multiples of 4 (kChunk % 4 == 0)
+    const int64_t i0 = start + threadIdx.x * 4;
+    int64_t r = i0 / ncol;
+    int64_t c = i0 - r * ncol;
+    for (int64_t i = i0; i < end; i += kThreads * 4) {
+      const float4 w4 = *reinterpret_cast<const float4*>(W + i);
+      const float4 v4 = *reinterpret_cast<const float4*>(v + c);
+      acc = fmaf(u[r], fmaf(w4.x, v4.x, fmaf(w4.y, v4.y, fmaf(w4.z, v4.z, w4.w * v4.w))), acc);
+      c += kThreads * 4;
+      while (c >= ncol) { c -= ncol; ++r; }
+    }
+  } else {
+    // (row, column) walked incrementally: no 64-bit division per element
+    const int64_t i0 = start + threadIdx.x;
+    int64_t r = i0 / ncol;
+    int64_t c = i0 - r * ncol;
+    for (int64_t i = i0; i < end; i += kThreads) {
+      acc = fmaf(u[r] * W[i], v[c], acc);
+      c += kThreads;
+      while (c >= ncol) { c -= ncol; ++r; }
+    }
   }
   acc = wave_sum(acc);
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;

@@ -34,10 +34,12 @@ __device__ __forceinline__ float window_count(const PoolGeom& g, int oy, int ox)
   return (float)((yb - ya) * (xb - xa));
 }
 
-template <typename T>
+// V channels per thread: 8 (16-byte accesses) when C % 8 == 0, else 1 (the 185-channel COCO
+// label maps the FPSE discriminator pools)
+template <typename T, int V>
 __global__ void __launch_bounds__(kT)
 avgpool_fwd(const T* __restrict__ x, T* __restrict__ y, PoolGeom g) {
-  const int cv = g.C / 8;
+  const int cv = g.C / V;
   const int64_t total = (int64_t)g.B * g.Ho * g.Wo * cv;
   for (int64_t t = (int64_t)blockIdx.x * kT + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * kT) {
@@ -48,30 +50,32 @@ avgpool_fwd(const T* __restrict__ x, T* __restrict__ y, PoolGeom g) {
     const int oy = (int)(p % g.Ho);
     const int b = (int)(p / g.Ho);
     const int y0 = oy * g.sh - g.ph, x0 = ox * g.sw - g.pw;
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float acc[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) acc[k] = 0.f;
     for (int dy = 0; dy < g.kh; ++dy) {
       const int iy = y0 + dy;
       if (iy < 0 || iy >= g.H) continue;
       for (int dx = 0; dx < g.kw; ++dx) {
         const int ix = x0 + dx;
         if (ix < 0 || ix >= g.W) continue;
-        float v[8];
-        load_vec<T, 8>(x + (((int64_t)b * g.H + iy) * g.W + ix) * g.C + c8 * 8, v);
+        float v[V];
+        load_vec<T, V>(x + (((int64_t)b * g.H + iy) * g.W + ix) * g.C + c8 * V, v);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] += v[k];
+        for (int k = 0; k < V; ++k) acc[k] += v[k];
       }
     }
     const float inv = 1.f / window_count(g, oy, ox);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] *= inv;
-    store_vec<T, 8>(y + t * 8, acc);
+    for (int k = 0; k < V; ++k) acc[k] *= inv;
+    store_vec<T, V>(y + t * V, acc);
   }
 }
 
-template <typename T>
+template <typename T, int V>
 __global__ void __launch_bounds__(kT)
 avgpool_bwd(const T* __restrict__ dy, T* __restrict__ dx, PoolGeom g) {
-  const int cv = g.C / 8;
+  const int cv = g.C / V;
   const int64_t total = (int64_t)g.B * g.H * g.W * cv;
   for (int64_t t = (int64_t)blockIdx.x * kT + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * kT) {
@@ -86,19 +90,21 @@ avgpool_bwd(const T* __restrict__ dy, T* __restrict__ dx, PoolGeom g) {
     const int oy_hi = min(g.Ho - 1, (iy + g.ph) / g.sh);
     const int ox_lo = max(0, (ix + g.pw - g.kw + g.sw) / g.sw);
     const int ox_hi = min(g.Wo - 1, (ix + g.pw) / g.sw);
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float acc[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) acc[k] = 0.f;
     for (int oy = oy_lo; oy <= oy_hi; ++oy) {
       if (iy < oy * g.sh - g.ph || iy >= oy * g.sh - g.ph + g.kh) continue;
       for (int ox = ox_lo; ox <= ox_hi; ++ox) {
         if (ix < ox * g.sw - g.pw || ix >= ox * g.sw - g.pw + g.kw) continue;
-        float v[8];
-        load_vec<T, 8>(dy + (((int64_t)b * g.Ho + oy) * g.Wo + ox) * g.C + c8 * 8, v);
+        float v[V];
+        load_vec<T, V>(dy + (((int64_t)b * g.Ho + oy) * g.Wo + ox) * g.C + c8 * V, v);
         const float inv = 1.f / window_count(g, oy, ox);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] += v[k] * inv;
+        for (int k = 0; k < V; ++k) acc[k] += v[k] * inv;
       }
     }
-    store_vec<T, 8>(dx + t * 8, acc);
+    store_vec<T, V>(dx + t * V, acc);
   }
 }
 
@@ -112,7 +118,6 @@ PoolGeom geom(const at::Tensor& x, int64_t Ho, int64_t Wo, int64_t kh, int64_t k
   g.B = (int)x.size(0); g.C = (int)x.size(1); g.H = (int)x.size(2); g.W = (int)x.size(3);
   g.Ho = (int)Ho; g.Wo = (int)Wo; g.kh = (int)kh; g.kw = (int)kw; g.sh = (int)sh; g.sw = (int)sw;
   g.ph = (int)ph; g.pw = (int)pw; g.include_pad = include_pad;
-  IAMD_CHECK(g.C % 8 == 0, "avg_pool_nhwc: channels must be a multiple of 8");
   IAMD_CHECK(kh >= 1 && kw >= 1 && sh >= 1 && sw >= 1 && ph >= 0 && pw >= 0 && 2 * ph <= kh &&
                  2 * pw <= kw && Ho >= 1 && Wo >= 1,
              "avg_pool_nhwc: bad geometry");
@@ -132,11 +137,17 @@ at::Tensor avg_pool_nhwc_fwd(const at::Tensor& x, int64_t kh, int64_t kw, int64_
   const int64_t Ho = (x.size(2) + 2 * ph - kh) / sh + 1, Wo = (x.size(3) + 2 * pw - kw) / sw + 1;
   const PoolGeom g = geom(x, Ho, Wo, kh, kw, sh, sw, ph, pw, include_pad);
   auto y = at::empty({g.B, g.C, g.Ho, g.Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  const int64_t n = (int64_t)g.B * g.Ho * g.Wo * (g.C / 8);
+  const bool v8 = g.C % 8 == 0;
+  const int64_t n = (int64_t)g.B * g.Ho * g.Wo * (v8 ? g.C / 8 : g.C);
   IAMD_DISPATCH_FLOAT_TYPES(x.scalar_type(), "avg_pool_nhwc_fwd", [&] {
-    hipLaunchKernelGGL((avgpool_fwd<scalar_t>), dim3(grid_for(n)), dim3(kT), 0, stream(),
-                       reinterpret_cast<const scalar_t*>(x.data_ptr()),
-                       reinterpret_cast<scalar_t*>(y.data_ptr()), g);
+    if (v8)
+      hipLaunchKernelGGL((avgpool_fwd<scalar_t, 8>), dim3(grid_for(n)), dim3(kT), 0, stream(),
+                         reinterpret_cast<const scalar_t*>(x.data_ptr()),
+                         reinterpret_cast<scalar_t*>(y.data_ptr()), g);
+    else
+      hipLaunchKernelGGL((avgpool_fwd<scalar_t, 1>), dim3(grid_for(n)), dim3(kT), 0, stream(),
+                         reinterpret_cast<const scalar_t*>(x.data_ptr()),
+                         reinterpret_cast<scalar_t*>(y.data_ptr()), g);
   });
   IAMD_LAUNCH_CHECK();
   return y;
@@ -152,11 +163,17 @@ at::Tensor avg_pool_nhwc_bwd(const at::Tensor& dy, int64_t H, int64_t W, int64_t
   IAMD_CHECK(dy.size(2) == (H + 2 * ph - kh) / sh + 1 && dy.size(3) == (W + 2 * pw - kw) / sw + 1,
              "avg_pool_nhwc_bwd: gradient size does not match the pooled input");
   const PoolGeom g = geom(dx, dy.size(2), dy.size(3), kh, kw, sh, sw, ph, pw, include_pad);
-  const int64_t n = (int64_t)g.B * g.H * g.W * (g.C / 8);
+  const bool v8 = g.C % 8 == 0;
+  const int64_t n = (int64_t)g.B * g.H * g.W * (v8 ? g.C / 8 : g.C);
   IAMD_DISPATCH_FLOAT_TYPES(dy.scalar_type(), "avg_pool_nhwc_bwd", [&] {
-    hipLaunchKernelGGL((avgpool_bwd<scalar_t>), dim3(grid_for(n)), dim3(kT), 0, stream(),
-                       reinterpret_cast<const scalar_t*>(dy.data_ptr()),
-                       reinterpret_cast<scalar_t*>(dx.data_ptr()), g);
+    if (v8)
+      hipLaunchKernelGGL((avgpool_bwd<scalar_t, 8>), dim3(grid_for(n)), dim3(kT), 0, stream(),
+                         reinterpret_cast<const scalar_t*>(dy.data_ptr()),
+                         reinterpret_cast<scalar_t*>(dx.data_ptr()), g);
+    else
+      hipLaunchKernelGGL((avgpool_bwd<scalar_t, 1>), dim3(grid_for(n)), dim3(kT), 0, stream(),
+                         reinterpret_cast<const scalar_t*>(dy.data_ptr()),
+                         reinterpret_cast<scalar_t*>(dx.data_ptr()), g);
   });
   IAMD_LAUNCH_CHECK();
   return dx;

@@ -570,17 +570,28 @@ def _agree(times):
     return out
 
 
-def _wgrad_fns(dy, xb, wb, stride, padding, dilation, cout, cin, wdt):
-    def k11():
+def _wgrad_fns(dy, xb, wb, stride, padding, dilation, cout, cin, wdt, variant=0):
+    def k11(v=variant):
         return _ext.ext().conv2d_wgrad_mfma(dy, xb, wb.shape[2], wb.shape[3], stride[0],
                                             stride[1], padding[0], padding[1], dilation[0],
-                                            dilation[1], cout, cin, wdt == torch.bfloat16)
+                                            dilation[1], cout, cin, wdt == torch.bfloat16, 1, v)
 
     def miopen():
         return torch.ops.aten.convolution_backward(
             dy, xb, wb, None, stride, padding, dilation, False, [0, 0], 1,
             [False, True, False])[1]
     return k11, miopen
+
+
+def _k11_variants(dy, xb, wb, stride, dilation):
+    """k11 kernel variants that can run this weight gradient: 'k11' (multi-tap / one-tap, two
+    or three blocks per CU) and, where eligible, 'k11v2' (one block per CU, 64 x 64 x KW-tap
+    accumulators per wave). Neither wins everywhere (profiles/wgrad_readahead_probe_mi355x.txt),
+    so the autotuner times both per shape."""
+    if _ext.ext().conv2d_wgrad_v2_eligible(dy, xb, wb.shape[2], wb.shape[3], stride[0],
+                                           stride[1], dilation[0], dilation[1]):
+        return ('k11', 'k11v2')
+    return ('k11',)
 
 
 def _wgrad(dy, xb, wb, stride, padding, dilation, cout=-1, cin=-1, wdt=torch.float32):
@@ -593,12 +604,15 @@ def _wgrad(dy, xb, wb, stride, padding, dilation, cout=-1, cin=-1, wdt=torch.flo
     mode = _MFMA_WGRAD
     fl = 2.0 * dy.shape[0] * dy.shape[2] * dy.shape[3] * wb.numel()
     desc = _gemm_desc(xb, wb, stride, padding)
-    if mode == '1':
-        with _Logged('wgrad', 'k11', fl, desc):
-            return k11()
     if mode == '0':
         with _Logged('wgrad', 'miopen', fl, desc):
             return miopen()
+    variants = _k11_variants(dy, xb, wb, stride, dilation)
+    if mode == '1' and len(variants) == 1:
+        with _Logged('wgrad', 'k11', fl, desc):
+            return k11()
+    # per-shape choice among the candidates (mode 1: the k11 variants; auto: those and MIOpen),
+    # timed by tune_pending() between iterations; the default routing runs until then
     key = (tuple(dy.shape), tuple(xb.shape), tuple(wb.shape), stride, padding, dilation,
            cout, cin, wdt)
     choice = _WGRAD_CHOICE.get(key)
@@ -606,7 +620,11 @@ def _wgrad(dy, xb, wb, stride, padding, dilation, cout=-1, cin=-1, wdt=torch.flo
         _WGRAD_PENDING.setdefault(key, (dy.dtype, xb.dtype, wb.dtype))
         choice = 'k11'
     with _Logged('wgrad', choice, fl, desc):
-        return k11() if choice == 'k11' else miopen()
+        if choice == 'miopen':
+            return miopen()
+        if choice == 'k11v2':
+            return k11(2)
+        return k11(1 if len(variants) > 1 and key in _WGRAD_CHOICE else 0)
 
 
 def routing_table():
@@ -631,7 +649,15 @@ def tune_pending():
         xb = torch.randn(xs, device=dev).to(xt).contiguous(memory_format=cl)
         wb = torch.randn(ws, device=dev).to(wt).contiguous(memory_format=cl)
         k11, miopen = _wgrad_fns(dy, xb, wb, stride, padding, dilation, cout, cin, wdt)
-        times[('w',) + key] = {'k11': _time_ms(k11), 'miopen': _time_ms(miopen)}
+        cand = {}
+        if _MFMA_WGRAD != '1':
+            cand['miopen'] = _time_ms(miopen)
+        if len(_k11_variants(dy, xb, wb, stride, dilation)) > 1:
+            cand['k11'] = _time_ms(lambda: k11(1))
+            cand['k11v2'] = _time_ms(lambda: k11(2))
+        else:
+            cand['k11'] = _time_ms(k11)
+        times[('w',) + key] = cand
     for key, fns in sorted(_DECONV_PENDING.items(), key=lambda kv: repr(kv[0])):
         times[('d',) + key] = {name: _time_ms(fn) for name, fn in fns().items()}
     times = _agree(times)

@@ -1,8 +1,9 @@
 """NHWC average pooling (k14, ``csrc/pool.hip``) with a gather backward.
 
 ``avg_pool2d`` / ``AvgPool2d`` are drop-ins for ``F.avg_pool2d`` / ``nn.AvgPool2d`` (no
-parameters, identical state dicts). Packed channels-last bf16 / fp32 activations with a
-channel count divisible by 8 run the HIP kernels; anything else (CPU, NCHW, ``ceil_mode``,
+parameters, identical state dicts). Packed channels-last bf16 / fp32 activations run the HIP
+kernels (16-byte accesses when the channel count divides by 8, per-channel otherwise: the
+185-channel COCO-Stuff label maps); anything else (CPU, NCHW, ``ceil_mode``,
 ``divisor_override``) falls back to PyTorch.
 """
 import torch
@@ -37,7 +38,7 @@ def avg_pool2d(x, kernel_size, stride=None, padding=0, ceil_mode=False, count_in
     s = _pair(stride if stride is not None else kernel_size)
     p = _pair(padding)
     if x.is_cuda and x.dim() == 4 and not ceil_mode and divisor_override is None and \
-            x.dtype in (torch.bfloat16, torch.float32) and x.shape[1] % 8 == 0 and \
+            x.dtype in (torch.bfloat16, torch.float32) and \
             x.is_contiguous(memory_format=torch.channels_last) and _ext.use_native(x) and \
             2 * p[0] <= k[0] and 2 * p[1] <= k[1] and \
             x.shape[2] + 2 * p[0] >= k[0] and x.shape[3] + 2 * p[1] >= k[1]:

@@ -29,6 +29,10 @@ shapes = [
     ('spade gb 5x5 128->4096 16x32', 4, 128, 4096, 5, 16, 32, 1, 2),
     ('dgrad gb 5x5 1024->128 128x256', 4, 1024, 128, 5, 128, 256, 1, 2),
     ('dgrad gb 5x5 4096->128 32x64', 4, 4096, 128, 5, 32, 64, 1, 2),
+    ('dgrad gb 5x5 2048->128 64x128', 4, 2048, 128, 5, 64, 128, 1, 2),
+    ('dgrad gb 5x5 512->128 256x512', 4, 512, 128, 5, 256, 512, 1, 2),
+    ('spade mlp 5x5 192->128 128x256', 4, 192, 128, 5, 128, 256, 1, 2),
+    ('dgrad G 3x3 512->256 128x256', 4, 512, 256, 3, 128, 256, 1, 1),
     ('D l1 4x4s2 128->256 128x256', 4, 128, 256, 4, 128, 256, 2, 1),
     ('D l2 4x4s2 256->512 64x128', 4, 256, 512, 4, 64, 128, 2, 1),
     ('vgg 3x3 128->128 128x256', 4, 128, 128, 3, 128, 256, 1, 1),

@@ -45,7 +45,7 @@ for name, B, cin, cout, k, H, W in shapes:
     errs = {}
     for rnd in range(5):
         for v in res:
-            os.environ['IMAGINAIRE_AMD_WGRAD_V2'] = '1' if v == 'v2' else '0'
+            os.environ['IMAGINAIRE_AMD_WGRAD_V2'] = 'force' if v == 'v2' else '0'
 
             def run():
                 return ext.conv2d_wgrad_mfma(dy, x, k, k, 1, 1, pad, pad, 1, 1, -1, -1, False, 1)

@@ -173,7 +173,8 @@ def test_multi_tensor_adam_and_ema(layout):
         assert torch.allclose(p.detach(), r, atol=1e-6, rtol=1e-5)
     # EMA with spectral-norm absorption
     ws = [fmt(torch.randn(8, 3, 3, 3, device='cuda')), torch.randn(16, 40, device='cuda'),
-          fmt(torch.randn(32, 16, 5, 5, device='cuda'))]
+          fmt(torch.randn(32, 16, 5, 5, device='cuda')),
+          fmt(torch.randn(256, 128, 3, 3, device='cuda'))]  # many chunks, 16-B path
     us = [torch.nn.functional.normalize(torch.randn(w.shape[0], device='cuda'), dim=0) for w in ws]
     vs = [torch.nn.functional.normalize(torch.randn(w[0].numel(), device='cuda'), dim=0)
           for w in ws]
@@ -748,9 +749,10 @@ def test_conv2d_wgrad_v2(case):
     Ho, Wo = H + 2 * p - k + 1, W + 2 * p - k + 1
     dy = torch.randn(B, cout, Ho, Wo, device='cuda').to(torch.bfloat16).contiguous(
         memory_format=torch.channels_last)
-    got = _ext.ext().conv2d_wgrad_mfma(dy, x, k, k, 1, 1, p, p, 1, 1)
-    os.environ['IMAGINAIRE_AMD_WGRAD_V2'] = '0'
+    os.environ['IMAGINAIRE_AMD_WGRAD_V2'] = 'force'
     try:
+        got = _ext.ext().conv2d_wgrad_mfma(dy, x, k, k, 1, 1, p, p, 1, 1)
+        os.environ['IMAGINAIRE_AMD_WGRAD_V2'] = '0'
         old = _ext.ext().conv2d_wgrad_mfma(dy, x, k, k, 1, 1, p, p, 1, 1)
     finally:
         os.environ.pop('IMAGINAIRE_AMD_WGRAD_V2')
@@ -1015,7 +1017,8 @@ def test_flow_warp_backward_modes():
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('cfg', [
     (2, 2, 0, True), (3, 2, 1, True), (3, 2, 1, False), (3, 1, 1, False), (4, 3, 2, True)])
-def test_avg_pool_nhwc(dtype, cfg):
+@pytest.mark.parametrize('channels', [24, 185])
+def test_avg_pool_nhwc(dtype, cfg, channels):
     """k14 NHWC average pool (ResDiscriminator 2x2, pix2pixHD/vid2vid 3x3/s2/p1 with and
     without count_include_pad, odd sizes) forward and gather backward == fp32 F.avg_pool2d on
     an NCHW copy. (PyTorch-ROCm's own channels-last avg_pool2d backward is wrong for
@@ -1024,9 +1027,10 @@ def test_avg_pool_nhwc(dtype, cfg):
     from imaginaire_amd.ops.pool import avg_pool2d
     k, s, p, inc = cfg
     torch.manual_seed(8)
-    x = torch.randn(2, 24, 19, 26, device='cuda').to(dtype).contiguous(
+    x = torch.randn(2, channels, 19, 26, device='cuda').to(dtype).contiguous(
         memory_format=torch.channels_last).requires_grad_(True)
     y = avg_pool2d(x, k, s, p, count_include_pad=inc)
+    assert y.grad_fn is not None and 'AvgPoolNHWC' in type(y.grad_fn).__name__  # HIP path
     xr = x.detach().float().contiguous().requires_grad_(True)
     yr = F.avg_pool2d(xr, k, s, p, count_include_pad=inc)
     assert y.shape == yr.shape and y.dtype == dtype
@@ -1126,3 +1130,38 @@ def test_multi_condition_spade_fused_modulation():
                     assert e < 8e-2, (n, float(e))
         else:
             assert (dx - dxr).abs().mean() / dxr.abs().mean() < 2e-2
+
+
+@pytest.mark.parametrize('case', [
+    # B, Cin, Cout, H, W, k, pad — k10 v4 row-window kernel over each segment class
+    (2, 128, 128, 16, 256, 5, 2),    # one 256-pixel segment per tile
+    (2, 192, 128, 8, 64, 5, 2),      # four 64-pixel rows per tile, Cin 192 (3 channel blocks)
+    (1, 256, 256, 16, 32, 3, 1),     # eight 32-pixel rows per tile, two N tiles
+    (2, 64, 128, 32, 16, 5, 2),      # sixteen 16-pixel rows per tile
+    (1, 1024, 128, 8, 128, 5, 2),    # dgrad-like (wide K, N 128): split-K over filter rows
+    (1, 128, 128, 12, 260, 5, 0),    # no padding: Wo = 256
+    (2, 128, 256, 4, 512, 3, 1),     # two tiles per output row
+])
+def test_conv2d_mfma_v4_row_window(case):
+    """k10 v4 (input windows shared by the KW taps of a filter row) vs fp32 F.conv2d with bias
+    and leaky-ReLU, and vs the v1 kernel."""
+    import os
+    from imaginaire_amd.ops import _ext
+    B, cin, cout, H, W, k, p = case
+    torch.manual_seed(16)
+    x = torch.randn(B, cin, H, W, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    w = (torch.randn(cout, cin, k, k, device='cuda') / (cin * k * k) ** 0.5).to(
+        torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    bias = torch.randn(cout, device='cuda')
+    ref = F.leaky_relu(F.conv2d(x.float(), w.float(), bias, 1, p), 0.2)
+    try:
+        os.environ['IMAGINAIRE_AMD_CONV_V'] = '4'
+        y4 = _ext.ext().conv2d_mfma(x, w, bias, 1, 1, p, p, 1, 1, 0.2)
+        os.environ['IMAGINAIRE_AMD_CONV_V'] = '1'
+        y1 = _ext.ext().conv2d_mfma(x, w, bias, 1, 1, p, p, 1, 1, 0.2)
+    finally:
+        os.environ.pop('IMAGINAIRE_AMD_CONV_V')
+    scale = ref.abs().max().item()
+    assert (y4.float() - ref).abs().max().item() <= 1e-2 * scale
+    assert (y4.float() - y1.float()).abs().max().item() <= 1e-2 * scale
