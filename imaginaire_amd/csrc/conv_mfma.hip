@@ -32,8 +32,10 @@ namespace iamd {
 namespace {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(3))) bf16x4* lds_bf16x4_t;
 
 constexpr int kBK = 64;
 constexpr int kRowBytes = kBK * 2;  // 128 B per staged row
@@ -760,7 +762,12 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v3(ConvArgs a) {
 //   DMA is buffer_load ... lds (zeros for padding pixels and past the k range); waits are
 //   counted vmcnt (2 or 7 glds per thread still in flight, never 0 in the loop) + raw s_barrier.
 // The data gradient of a stride-1 conv runs here too (flipped / transposed weight, as v1).
-template <int KW, bool HAS_BIAS>
+// BT (data gradient without a flipped weight copy): a.w is the FORWARD weight [K][KH][KW][N]
+// (K = a.Cin = dy channels, N = a.Cout = dx channels) and tap (ky, kx) reads forward tap
+// (KH-1-ky, KW-1-kx). Its weight tile is staged k-major (64 rows of 128 n-channels, 256 B,
+// 16-byte chunks swizzled per row) and the B fragments are read with the transposing
+// ds_read_b64_tr_b16 (two 4-row reads per 8-deep fragment, as the k11 weight gradient does).
+template <int KW, bool HAS_BIAS, bool BT>
 __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v4(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   constexpr int BM = 256, BN = 128;
@@ -811,11 +818,21 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v4(ConvArgs a) {
       }
     }
   }
-  // weight DMA: rows 64 i + 8 w + (lane >> 3) of the 128-row tap tile
+  // weight DMA: rows 64 i + 8 w + (lane >> 3) of the 128-row tap tile (BT: k-rows
+  // 32 i + 4 w + (lane >> 4) of 256 B, source chunk (lane & 15) ^ swz(row))
   const int wrow_bytes = a.nk * kBK * 2;
+  const int KK = a.KH * KW;
   int b_off[2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) b_off[i] = (n0 + i * 64 + wid * 8 + dr) * wrow_bytes + csw * 16;
+  for (int i = 0; i < 2; ++i) {
+    if constexpr (BT) {
+      const int row = i * 32 + wid * 4 + (lane >> 4);
+      const int sch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
+      b_off[i] = (row * KK * a.Cout + n0 + sch * 8) * 2;
+    } else {
+      b_off[i] = (n0 + i * 64 + wid * 8 + dr) * wrow_bytes + csw * 16;
+    }
+  }
 
   // ---- k range of this split in outer steps o = (ky, channel block) ------------------------
   const int o0 = blockIdx.y * a.kps;
@@ -838,7 +855,12 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v4(ConvArgs a) {
     }
   };
   auto issueB = [&](int o, int ky, int cc, int kx, int slot) {  // weight tap (ky, kx), block cc
-    const int soff = o < o1 ? ((ky * KW + kx) * a.Cin + cc) * 2 : kOobOffset;
+    int soff;
+    if constexpr (BT)  // forward tap (KH-1-ky, KW-1-kx), k rows cc.. of [K][KK][N]
+      soff = o < o1 ? ((cc * KK + (a.KH - 1 - ky) * KW + (KW - 1 - kx)) * a.Cout) * 2
+                    : kOobOffset;
+    else
+      soff = o < o1 ? ((ky * KW + kx) * a.Cin + cc) * 2 : kOobOffset;
     char* Bs = smem + kBoff + slot * kBbytes;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -873,11 +895,29 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v4(ConvArgs a) {
         af[kk][i] = *reinterpret_cast<const bf16x8*>(
             As + row * kRowBytes + (((kk * 4 + fk) ^ (row & 7)) << 4));
       }
-      const int coff = ((kk * 4 + fk) ^ fsw) << 4;
+      if constexpr (BT) {
+        // lane (g, q, p): rows kk*32 + 8g + q (+4), 8-byte quarter p of a 16-column block
+        const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+        const int r0 = kk * 32 + g * 8 + q;
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        bfr[kk][j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * 64 + j * 16 + frow) * kRowBytes +
-                                                      coff);
+        for (int j = 0; j < 4; ++j) {
+          const int cb = (wn * 64 + j * 16) >> 3;
+          auto baddr = [&](int row) {
+            return row * 256 + (((cb + (p >> 1)) ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4) +
+                   ((p & 1) << 3);
+          };
+          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t)(Bs + baddr(r0)));
+          const bf16x4 hi =
+              __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t)(Bs + baddr(r0 + 4)));
+          bfr[kk][j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+      } else {
+        const int coff = ((kk * 4 + fk) ^ fsw) << 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          bfr[kk][j] = *reinterpret_cast<const bf16x8*>(
+              Bs + (wn * 64 + j * 16 + frow) * kRowBytes + coff);
+      }
     }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -998,6 +1038,63 @@ conv_splitk_reduce(const float* __restrict__ part, const float* __restrict__ bia
 
 namespace {
 
+// v4 (row-window, 256 x 128): stride 1, undilated, KW 3..5, whole 256-pixel tiles made of
+// output-row segments (Wo a multiple of 256, or 16..128 dividing 256)
+bool v4_eligible(const ConvArgs& a) {
+  static const bool off = [] {
+    const char* e = std::getenv("IMAGINAIRE_AMD_CONV_V4");  // 0: A/B switch back to v1 / v3
+    return e != nullptr && e[0] == '0';
+  }();
+  return !off && a.nz == 1 && a.omode == 0 && a.sh == 1 && a.sw == 1 && a.dh == 1 && a.dw == 1 &&
+         (a.KW >= 3 && a.KW <= 5) && a.KH <= 31 && a.Cout % 128 == 0 &&
+         (a.Wo % 256 == 0 || (a.Wo >= 16 && a.Wo <= 128 && 256 % a.Wo == 0)) &&
+         ((int64_t)a.Ho * a.Wo) % 256 == 0;
+}
+
+void run_v4(ConvArgs& a, const at::Tensor& x, bool bt) {
+  const int Cout = a.Cout, KW = a.KW;
+  a.nNt = Cout / 128;
+  const int64_t tiles4 = (int64_t)(a.M / 256) * a.nNt;
+  const int nout = a.nk / KW;  // (filter row, channel block) outer steps
+  int S4 = 1;
+  if (tiles4 < 256 && nout >= 8) S4 = (int)std::min<int64_t>((256 + tiles4 - 1) / tiles4, nout / 4);
+  if (const char* e = std::getenv("IMAGINAIRE_AMD_CONV_SPLITK")) S4 = std::max(1, std::atoi(e));
+  S4 = std::max(1, std::min(S4, nout));
+  a.kps = ceil_div(nout, S4);
+  S4 = ceil_div(nout, a.kps);
+  at::Tensor part4;
+  a.part = nullptr;
+  if (S4 > 1) {
+    part4 = at::empty({(int64_t)S4 * a.M * Cout}, x.options().dtype(at::kFloat));
+    a.part = part4.data_ptr<float>();
+  }
+  const dim3 grid4((unsigned)tiles4, (unsigned)S4, 1);
+  auto launch = [&](auto kv, auto hbv, auto btv) {
+    constexpr int K = decltype(kv)::value;
+    constexpr bool HB = decltype(hbv)::value, BTV = decltype(btv)::value;
+    hipLaunchKernelGGL((conv_fwd_mfma_v4<K, HB, BTV>), grid4, dim3(512), 0, stream(), a);
+  };
+  auto by_bt = [&](auto kv, auto hbv) {
+    if (bt) launch(kv, hbv, std::true_type());
+    else launch(kv, hbv, std::false_type());
+  };
+  auto by_bias = [&](auto kv) {
+    if (a.bias) by_bt(kv, std::true_type());
+    else by_bt(kv, std::false_type());
+  };
+  if (KW == 5) by_bias(std::integral_constant<int, 5>());
+  else if (KW == 4) by_bias(std::integral_constant<int, 4>());
+  else by_bias(std::integral_constant<int, 3>());
+  if (S4 > 1) {
+    IAMD_LAUNCH_CHECK();
+    const int64_t MC = (int64_t)a.M * Cout;
+    const int blocks = (int)std::min<int64_t>((MC / 8 + 255) / 256, 8192);
+    hipLaunchKernelGGL(conv_splitk_reduce, dim3(blocks), dim3(256), 0, stream(), a.part, a.bias,
+                       a.y, S4, MC, Cout, a.slope, a);
+  }
+  IAMD_LAUNCH_CHECK();
+}
+
 // Kernel choice, split-K and launch for a filled-in ConvArgs (x supplies the tensor options of
 // the split-K slabs).
 void run_conv(ConvArgs& a, const at::Tensor& x) {
@@ -1024,46 +1121,10 @@ void run_conv(ConvArgs& a, const at::Tensor& x) {
     S = std::max(1, std::min(S, a.nk));
     return ceil_div(a.nk, ceil_div(a.nk, S));
   };
-  // v4 (row-window, 256 x 128): stride 1, undilated, KW 3 / 5, whole 256-pixel tiles made of
-  // output-row segments (Wo a multiple of 256, or 16..128 dividing 256)
-  const bool v4_ok = a.nz == 1 && a.omode == 0 && a.sh == 1 && a.sw == 1 && a.dh == 1 &&
-                     a.dw == 1 && (KW == 3 || KW == 5) && KH <= 31 && bn128 &&
-                     (a.Wo % 256 == 0 || (a.Wo >= 16 && a.Wo <= 128 && 256 % a.Wo == 0)) &&
-                     ((int64_t)a.Ho * a.Wo) % 256 == 0;
-  // default: every eligible conv (1.02-1.52x v1 and 1.0-1.08x v3 on the SPADE-step shapes,
-  // the N = 128 data gradients 1.36-1.52x: profiles/conv_v4_probe_mi355x.txt)
-  if ((ver == 4 || ver == 0) && v4_ok) {
-    a.nNt = Cout / 128;
-    const int64_t tiles4 = (int64_t)(a.M / 256) * a.nNt;
-    const int nout = a.nk / KW;  // (filter row, channel block) outer steps
-    int S4 = 1;
-    if (tiles4 < 256 && nout >= 8) S4 = (int)std::min<int64_t>((256 + tiles4 - 1) / tiles4, nout / 4);
-    if (const char* e = std::getenv("IMAGINAIRE_AMD_CONV_SPLITK")) S4 = std::max(1, std::atoi(e));
-    S4 = std::max(1, std::min(S4, nout));
-    a.kps = ceil_div(nout, S4);
-    S4 = ceil_div(nout, a.kps);
-    at::Tensor part4;
-    a.part = nullptr;
-    if (S4 > 1) {
-      part4 = at::empty({(int64_t)S4 * a.M * Cout}, x.options().dtype(at::kFloat));
-      a.part = part4.data_ptr<float>();
-    }
-    const dim3 grid4((unsigned)tiles4, (unsigned)S4, 1);
-    if (KW == 5) {
-      if (a.bias) hipLaunchKernelGGL((conv_fwd_mfma_v4<5, true>), grid4, dim3(512), 0, stream(), a);
-      else hipLaunchKernelGGL((conv_fwd_mfma_v4<5, false>), grid4, dim3(512), 0, stream(), a);
-    } else {
-      if (a.bias) hipLaunchKernelGGL((conv_fwd_mfma_v4<3, true>), grid4, dim3(512), 0, stream(), a);
-      else hipLaunchKernelGGL((conv_fwd_mfma_v4<3, false>), grid4, dim3(512), 0, stream(), a);
-    }
-    if (S4 > 1) {
-      IAMD_LAUNCH_CHECK();
-      const int64_t MC = (int64_t)a.M * Cout;
-      const int blocks = (int)std::min<int64_t>((MC / 8 + 255) / 256, 8192);
-      hipLaunchKernelGGL(conv_splitk_reduce, dim3(blocks), dim3(256), 0, stream(), a.part, a.bias,
-                         a.y, S4, MC, Cout, a.slope, a);
-    }
-    IAMD_LAUNCH_CHECK();
+  if ((ver == 4 || ver == 0) && v4_eligible(a)) {
+    // default: every eligible conv (1.02-1.52x v1 and 1.0-1.08x v3 on the SPADE-step shapes,
+    // the N = 128 data gradients 1.36-1.52x: profiles/conv_v4_probe_mi355x.txt)
+    run_v4(a, x, false);
     return;
   }
   bool v3 = false, v2 = false;
@@ -1221,6 +1282,59 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
   a.omode = 0;
   a.oH = Ho; a.oW = Wo; a.osy = 1; a.osx = 1; a.ory = 0; a.orx = 0;
   run_conv(a, x);
+  return y;
+}
+
+
+at::Tensor conv_weight_flip_t(const at::Tensor& w, int64_t s, int64_t qy, int64_t qx, int64_t nb);
+
+// Data gradient of a stride-1, undilated conv with forward weight w [Cout, Cin, KH, KW]
+// (channels-last): dx [B, Cin, H, W] = conv(dy, flip_t(w), padding (KH-1-ph, KW-1-pw)). On the v4
+// path the forward weight is read directly (tap-flipped, k-major, transposing LDS reads): no
+// flipped copy of the weight per backward; other shapes flip once and run the k10 routing.
+at::Tensor conv2d_dgrad_mfma(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int64_t pw) {
+  IAMD_CHECK(dy.is_cuda() && w.is_cuda() && dy.scalar_type() == at::kBFloat16 &&
+                 w.scalar_type() == at::kBFloat16 && dy.dim() == 4 && w.dim() == 4,
+             "conv2d_dgrad_mfma: 4-D bf16 CUDA tensors expected");
+  IAMD_CHECK(dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                 w.is_contiguous(at::MemoryFormat::ChannelsLast),
+             "conv2d_dgrad_mfma: packed channels-last operands expected");
+  const int KH = (int)w.size(2), KW = (int)w.size(3);
+  IAMD_CHECK(dy.size(1) == w.size(0), "conv2d_dgrad_mfma: dy channels != weight rows");
+  IAMD_CHECK(ph <= KH - 1 && pw <= KW - 1 && ph >= 0 && pw >= 0,
+             "conv2d_dgrad_mfma: padding outside the filter");
+  const int64_t tph = KH - 1 - ph, tpw = KW - 1 - pw;
+  const int B = (int)dy.size(0), K = (int)dy.size(1), H = (int)dy.size(2), W = (int)dy.size(3);
+  const int N = (int)w.size(1);
+  ConvArgs a;
+  a.H = H; a.W = W; a.Cin = K; a.Cout = N; a.KH = KH; a.KW = KW;
+  a.sh = a.sw = a.dh = a.dw = 1; a.ph = (int)tph; a.pw = (int)tpw;
+  a.Ho = H + 2 * (int)tph - (KH - 1);
+  a.Wo = W + 2 * (int)tpw - (KW - 1);
+  a.nz = 1; a.omode = 0;
+  const bool ok = K % kBK == 0 && a.Ho > 0 && a.Wo > 0 && v4_eligible(a) &&
+                  (int64_t)B * H * W * K * 2 < kOobOffset && w.numel() * 2 < kOobOffset &&
+                  (int64_t)B * a.Ho * a.Wo * N < (1ll << 31) &&
+                  std::getenv("IMAGINAIRE_AMD_DGRAD_FLIP") == nullptr;
+  if (!ok) {
+    const at::Tensor wt = conv_weight_flip_t(w, 1, 0, 0, 1);
+    return conv2d_mfma(dy, wt, c10::nullopt, 1, 1, tph, tpw, 1, 1, 1.0, 1);
+  }
+  auto y = at::empty({B, N, a.Ho, a.Wo}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  a.x = reinterpret_cast<const __hip_bfloat16*>(dy.data_ptr());
+  a.w = reinterpret_cast<const __hip_bfloat16*>(w.data_ptr());
+  a.bias = nullptr;
+  a.y = reinterpret_cast<__hip_bfloat16*>(y.data_ptr());
+  a.xbytes = (int)(dy.numel() * 2);
+  a.wbytes = (int)(w.numel() * 2);
+  a.xbs = a.wbs = a.ybs = 0;
+  a.bbs = 0;
+  a.M = B * a.Ho * a.Wo;
+  a.cpt = K / kBK;
+  a.nk = KH * KW * a.cpt;
+  a.slope = 1.f;
+  a.oH = a.Ho; a.oW = a.Wo; a.osy = 1; a.osx = 1; a.ory = 0; a.orx = 0;
+  run_v4(a, dy, true);
   return y;
 }
 

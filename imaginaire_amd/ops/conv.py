@@ -343,7 +343,13 @@ class _MfmaConv2d(torch.autograd.Function):
             # the dgrad GEMM has N = Cin (few tiles, K = taps x Cout for the SPADE γ/β convs):
             # k10 splits K over the grid's y dimension for those
             fl = 2.0 * dy.shape[0] * dy.shape[2] * dy.shape[3] * wb.numel()
-            if stride == (1, 1) and pt[0] >= 0 and pt[1] >= 0 and \
+            if stride == (1, 1) and dilation == (1, 1) and pt[0] >= 0 and pt[1] >= 0 and \
+                    dblocks >= _MFMA_MIN_DGRAD_BLOCKS:
+                # k10 v4 reads the forward weight tap-flipped and transposed in-kernel (no
+                # flipped weight copy); other shapes flip once inside and run the k10 routing
+                with _Logged('dgrad', 'k10', fl, _gemm_desc(dy, wb.transpose(0, 1), (1, 1), pt)):
+                    dx = _ext.ext().conv2d_dgrad_mfma(dy, wb, padding[0], padding[1])
+            elif stride == (1, 1) and pt[0] >= 0 and pt[1] >= 0 and \
                     dblocks >= _MFMA_MIN_DGRAD_BLOCKS:
                 wt = _flip_t(wb)
                 with _Logged('dgrad', 'k10', fl, _gemm_desc(dy, wt, (1, 1), pt)):

@@ -52,6 +52,11 @@ def _save_video(path, frames, fps):
 
 
 class Trainer(BaseTrainer):
+    # one training iteration = the whole per-frame D / G update loop over the sequence: replayed
+    # from one hipGraph per sequence length (captured again when the length changes, as the
+    # batch shape does; tests/test_graph_families_gpu.py)
+    graph_capturable = True
+
     def __init__(self, cfg, net_G, net_D, opt_G, opt_D, sch_G, sch_D, train_data_loader,
                  val_data_loader):
         super().__init__(cfg, net_G, net_D, opt_G, opt_D, sch_G, sch_D, train_data_loader,

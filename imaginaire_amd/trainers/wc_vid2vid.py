@@ -23,6 +23,9 @@ from imaginaire_amd.utils.visualization import tensor2flow, tensor2im
 
 
 class Trainer(Vid2VidTrainer):
+    # the world-consistent renderer keeps host-side point-cloud state between frames
+    graph_capturable = False
+
     def __init__(self, cfg, net_G, net_D, opt_G, opt_D, sch_G, sch_D, train_data_loader,
                  val_data_loader):
         super().__init__(cfg, net_G, net_D, opt_G, opt_D, sch_G, sch_D, train_data_loader,

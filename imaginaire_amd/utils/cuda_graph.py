@@ -82,13 +82,35 @@ def _same_structure(a, b):
     return a == b
 
 
+def _signature(x):
+    """Hashable structure of a batch (tensor shapes / dtypes / strides, nested containers)."""
+    if torch.is_tensor(x):
+        return ('T', tuple(x.shape), str(x.dtype), tuple(x.stride()))
+    if isinstance(x, dict):
+        return ('D',) + tuple((k, _signature(v)) for k, v in sorted(x.items(), key=lambda kv: str(kv[0])))
+    if isinstance(x, (list, tuple)):
+        return ('L',) + tuple(_signature(v) for v in x)
+    if isinstance(x, str):
+        return ('S',)  # file keys / names: never steer the computation
+    try:
+        hash(x)
+        return ('V', x)
+    except TypeError:
+        return ('V', repr(x))
+
+
 class GraphedStep(object):
     """Runs ``step_fn(data)`` eagerly for ``warmup`` iterations (on a side stream, as
     stream capture requires), then captures it and replays the graph from then on.
 
-    ``step_fn`` must be the steady-state iteration: no host synchronisation, fixed shapes.
+    One graph per batch structure (shapes / dtypes of the inputs): a new structure — the
+    video trainers' growing sequence length, a ragged last batch — gets its own warm-up and
+    capture; the graphs share one memory pool. ``step_fn`` must be the steady-state
+    iteration for a given structure: no host synchronisation.
     ``pre_replay`` / ``post_replay`` are host hooks run around every replay.
     """
+
+    MAX_GRAPHS = 8
 
     def __init__(self, step_fn, warmup=3, pre_replay=None, post_replay=None, name='step',
                  save_host=None, restore_host=None):
@@ -100,70 +122,93 @@ class GraphedStep(object):
         self.save_host = save_host
         self.restore_host = restore_host
         self.name = name
-        self.graph = None
-        self.static = None
-        self.n_eager = 0
+        self.entries = {}  # signature -> {'graph', 'static', 'n_eager'}
         self.failed = False
         self.capture_s = None
         self.stream = None
+        self.pool = None
+        self._last = None
+
+    # the most recently used entry (tests and bench scripts read .graph / .static)
+    @property
+    def graph(self):
+        return self._last['graph'] if self._last else None
+
+    @property
+    def static(self):
+        return self._last['static'] if self._last else None
+
+    @property
+    def n_eager(self):
+        return self._last['n_eager'] if self._last else 0
+
+    def _side_stream(self):
+        if self.stream is None:
+            self.stream = torch.cuda.Stream()
+            # parameters' AccumulateGrad nodes made by earlier default-stream iterations
+            # meet the side stream here: a one-off stream sync during warm-up, not a
+            # problem for the captured replay (no autograd engine runs there)
+            _quiet = getattr(torch.autograd.graph,
+                             'set_warn_on_accumulate_grad_stream_mismatch', None)
+            if _quiet is not None:
+                _quiet(False)
+        return self.stream
 
     def __call__(self, data):
         if self.failed:
             return self.step_fn(data)
-        if self.graph is not None:
-            if not _same_structure(self.static, data):
-                # e.g. a ragged last batch: run it eagerly, keep the graph
-                return self.step_fn(data)
-            _static_copy(self.static, data)
+        sig = _signature(data)
+        ent = self.entries.get(sig)
+        if ent is None:
+            if len(self.entries) >= self.MAX_GRAPHS:
+                return self.step_fn(data)  # structure churn: stay eager for new ones
+            ent = self.entries[sig] = {'graph': None, 'static': None, 'n_eager': 0}
+        self._last = ent
+        if ent['graph'] is not None:
+            _static_copy(ent['static'], data)
             if self.pre_replay:
                 self.pre_replay()
-            self.graph.replay()
+            ent['graph'].replay()
             if self.post_replay:
                 self.post_replay()
             return None
-        if self.n_eager < self.warmup:
+        if ent['n_eager'] < self.warmup:
             # warm up on the stream the capture will use: autograd's AccumulateGrad nodes
             # remember the stream they were created on
-            if self.stream is None:
-                self.stream = torch.cuda.Stream()
-                # parameters' AccumulateGrad nodes made by earlier default-stream iterations
-                # meet the side stream here: a one-off stream sync during warm-up, not a
-                # problem for the captured replay (no autograd engine runs there)
-                _quiet = getattr(torch.autograd.graph,
-                                 'set_warn_on_accumulate_grad_stream_mismatch', None)
-                if _quiet is not None:
-                    _quiet(False)
-            self.stream.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(self.stream):
+            st = self._side_stream()
+            st.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(st):
                 self.step_fn(data)
-            torch.cuda.current_stream().wait_stream(self.stream)
-            self.n_eager += 1
+            torch.cuda.current_stream().wait_stream(st)
+            ent['n_eager'] += 1
             return None
-        return self._capture_and_run(data)
+        return self._capture_and_run(ent, data)
 
-    def _capture_and_run(self, data):
+    def _capture_and_run(self, ent, data):
         from imaginaire_amd.ops import _ext
         torch.cuda.synchronize()
         t0 = time.time()
         # private copies: the batch source may hand out views of its own pool
-        self.static = _clone(data)
+        ent['static'] = _clone(data)
         saved = self.save_host() if self.save_host else None
         g = torch.cuda.CUDAGraph()
         try:
-            if self.stream is None:
-                self.stream = torch.cuda.Stream()
+            st = self._side_stream()
+            if self.pool is None:
+                self.pool = torch.cuda.graph_pool_handle()
             # thread-local capture mode: the RCCL process group's watchdog thread keeps polling
             # its work events while a (seconds-long) step is being captured; under the default
             # global mode those calls from another thread are refused and abort the process
-            with torch.cuda.graph(g, stream=self.stream, capture_error_mode='thread_local'):
-                self.step_fn(self.static)
+            with torch.cuda.graph(g, pool=self.pool, stream=st,
+                                  capture_error_mode='thread_local'):
+                self.step_fn(ent['static'])
         except Exception as e:  # noqa: BLE001 - any capture failure: stay eager
             if os.environ.get('IMAGINAIRE_AMD_GRAPH_DEBUG'):
                 raise
             print('[graph] capture of {} failed ({}: {}); running eagerly'.format(
                 self.name, type(e).__name__, str(e).splitlines()[0][:200]))
             self.failed = True
-            self.static = None
+            ent['static'] = None
             if self.restore_host:
                 self.restore_host(saved)
             torch.cuda.synchronize()
@@ -173,9 +218,11 @@ class GraphedStep(object):
         if _ext.available():
             _ext.ext().flush_deferred_uploads()
         torch.cuda.synchronize()
-        self.graph = g
+        ent['graph'] = g
         self.capture_s = time.time() - t0
-        print('[graph] captured {} in {:.1f} s'.format(self.name, self.capture_s))
+        print('[graph] captured {} ({} graph(s)) in {:.1f} s'.format(
+            self.name, sum(1 for e in self.entries.values() if e['graph'] is not None),
+            self.capture_s))
         # the capture itself executed nothing: run this iteration as the first replay
         if self.pre_replay:
             self.pre_replay()

@@ -22,6 +22,12 @@ run() {  # name, timeout, cmd...
 [ -z "$CPROBE" ] || run cprobe 600 python scripts/probe/conv_v2_probe.py ${CVERS:-1,0}
 [ -z "$PROBE" ] || run probe 600 python $PROBE
 [ -z "$BENCH" ] || run bench 600 python bench.py --steps 20 --warmup 6
+# AB="VAR=val ...": the same bench again with those variables (same box: a fair A/B), then the
+# default once more (order effects)
+if [ -n "$AB" ]; then
+  run bench_ab 600 env $AB python bench.py --steps 20 --warmup 6
+  run bench_again 600 python bench.py --steps 20 --warmup 6
+fi
 [ -z "$CONVLOG" ] || run convlog 600 python bench.py --steps 1 --warmup 3 --conv-log
 [ -z "$GRAPH" ] || run graph 1000 bash scripts/gpu/r3_graph.sh
 [ -z "$OPS" ] || TAILN=60 run ops 600 python bench.py --steps 1 --warmup 3 --no-graph --op-profile --op-stack

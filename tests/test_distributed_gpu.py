@@ -44,9 +44,45 @@ def _init(rank, world, port):
     return dist
 
 
+def _to_np(obj):
+    if torch.is_tensor(obj):
+        return ('__tensor__', obj.detach().cpu().numpy())
+    if isinstance(obj, dict):
+        return {k: _to_np(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_to_np(o) for o in obj)
+    return obj
+
+
+def _to_torch(obj):
+    if isinstance(obj, tuple) and len(obj) == 2 and isinstance(obj[0], str) and \
+            obj[0] == '__tensor__':
+        return torch.from_numpy(obj[1])
+    if isinstance(obj, dict):
+        return {k: _to_torch(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_to_torch(o) for o in obj)
+    return obj
+
+
+class _NpQueue:
+    """Results travel as numpy arrays: a CPU tensor put on a multiprocessing queue is shared
+    through a file descriptor served by the SENDING process, which may already have exited
+    when the parent unpickles it (FileNotFoundError on the resource-sharer socket)."""
+
+    def __init__(self, q):
+        self.q = q
+
+    def put(self, obj):
+        self.q.put(_to_np(obj))
+
+    def get(self, timeout=None):
+        return _to_torch(self.q.get(timeout=timeout))
+
+
 def _spawn(target, world, *args):
     ctx = mp.get_context('spawn')
-    q = ctx.Queue()
+    q = _NpQueue(ctx.Queue())
     port = _free_port()
     procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
     for p in procs:

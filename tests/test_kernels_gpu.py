@@ -1141,6 +1141,9 @@ def test_multi_condition_spade_fused_modulation():
     (1, 1024, 128, 8, 128, 5, 2),    # dgrad-like (wide K, N 128): split-K over filter rows
     (1, 128, 128, 12, 260, 5, 0),    # no padding: Wo = 256
     (2, 128, 256, 4, 512, 3, 1),     # two tiles per output row
+    (1, 256, 128, 35, 67, 4, 2),     # 4x4 (PatchGAN head) p2: Wo = 68 -> not eligible (v1)
+    (1, 256, 128, 17, 35, 4, 1),     # 4x4 p1: Ho x Wo = 16 x 34 -> not eligible
+    (2, 128, 128, 3, 63, 4, 2),      # 4x4 p2 (PatchGAN head): 4 x 64 output on v4 (KW 4)
 ])
 def test_conv2d_mfma_v4_row_window(case):
     """k10 v4 (input windows shared by the KW taps of a filter row) vs fp32 F.conv2d with bias
@@ -1165,3 +1168,31 @@ def test_conv2d_mfma_v4_row_window(case):
     scale = ref.abs().max().item()
     assert (y4.float() - ref).abs().max().item() <= 1e-2 * scale
     assert (y4.float() - y1.float()).abs().max().item() <= 1e-2 * scale
+
+
+@pytest.mark.parametrize('case', [
+    # B, Cin, Cout, H, W, k, pad: the stride-1 data gradient from the forward weight
+    (2, 128, 1024, 16, 256, 5, 2),   # SPADE gamma|beta dgrad: v4 transposed-weight path
+    (1, 128, 512, 8, 64, 5, 2),      # four output rows per tile
+    (2, 256, 128, 16, 32, 3, 1),     # 3x3, two N tiles
+    (1, 128, 128, 12, 256, 5, 1),    # padding 1 of a 5x5 (dgrad padding 3)
+    (2, 192, 128, 8, 64, 5, 2),      # N = 192: not a multiple of 128 -> flip + k10 fallback
+    (1, 64, 128, 10, 70, 3, 0),      # W 70, no padding: dx 72 wide -> fallback
+    (2, 128, 256, 16, 64, 4, 2),     # 4x4 s1 p2 (PatchGAN head): dx 16 x 64 on v4 (KW 4)
+])
+def test_conv2d_dgrad_mfma(case):
+    """conv2d_dgrad_mfma (k10 v4 reading the forward weight tap-flipped / transposed, or the
+    flip + k10 fallback) vs fp32 torch.nn.grad.conv2d_input."""
+    from imaginaire_amd.ops import _ext
+    B, cin, cout, H, W, k, p = case
+    torch.manual_seed(17)
+    Ho, Wo = H + 2 * p - k + 1, W + 2 * p - k + 1
+    dy = torch.randn(B, cout, Ho, Wo, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    w = (torch.randn(cout, cin, k, k, device='cuda') / (cout * k * k) ** 0.5).to(
+        torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    got = _ext.ext().conv2d_dgrad_mfma(dy, w, p, p)
+    ref = torch.nn.grad.conv2d_input((B, cin, H, W), w.float(), dy.float(), 1, p)
+    assert got.shape == ref.shape
+    scale = ref.abs().max().item()
+    assert (got.float() - ref).abs().max().item() <= 1e-2 * scale
