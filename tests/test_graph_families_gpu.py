@@ -121,6 +121,9 @@ def test_family_graph_replay_matches_eager(name, seq_len):
     le = _losses(tr)
     de = [p.detach() - q for p, q in zip(gparams, p0)]
     print(name, 'graph', lg, '\n', name, 'eager', le)
+    names = [n for n, _ in tr.net_G.named_parameters()]
+    bad = [n for n, x in zip(names, dg) if not torch.isfinite(x).all()]
+    assert not bad, 'non-finite replayed G updates: %s' % bad[:8]
     assert lg.keys() == le.keys() and lg
     for k in le:
         assert lg[k] == lg[k], k  # finite
