@@ -7,7 +7,16 @@ namespace iamd {
 // spade_norm.hip (k1)
 std::vector<at::Tensor> norm_stats(const at::Tensor& x, bool per_instance, double eps,
                                    const c10::optional<at::Tensor>& weight,
-                                   const c10::optional<at::Tensor>& bias, bool partial_only);
+                                   const c10::optional<at::Tensor>& bias, bool partial_only,
+                                   const c10::optional<at::Tensor>& running_mean,
+                                   const c10::optional<at::Tensor>& running_var,
+                                   const c10::optional<at::Tensor>& num_batches,
+                                   double momentum);
+std::vector<at::Tensor> norm_bwd_coeffs(const at::Tensor& S1, const at::Tensor& S2,
+                                        const at::Tensor& rstd,
+                                        const c10::optional<at::Tensor>& weight,
+                                        bool per_instance, double invM, bool need_dw,
+                                        bool need_db);
 at::Tensor norm_apply(const at::Tensor& x, const at::Tensor& scale, const at::Tensor& shift,
                       const c10::optional<at::Tensor>& gamma,
                       const c10::optional<at::Tensor>& beta, double slope);
@@ -182,7 +191,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "the taps of one stride-s phase; nb per-sample weights", py::arg("w"), py::arg("s") = 1,
         py::arg("qy") = 0, py::arg("qx") = 0, py::arg("nb") = 1);
   m.def("sn_scale_backward", &iamd::sn_scale_backward, "spectral-norm W/sigma backward (k5d)");
-  m.def("norm_stats", &iamd::norm_stats, "per-(group,channel) statistics (k1)");
+  m.def("norm_stats", &iamd::norm_stats, "per-(group,channel) statistics (k1)",
+        py::arg("x"), py::arg("per_instance"), py::arg("eps"), py::arg("weight"),
+        py::arg("bias"), py::arg("partial_only"), py::arg("running_mean") = py::none(),
+        py::arg("running_var") = py::none(), py::arg("num_batches") = py::none(),
+        py::arg("momentum") = 0.0);
+  m.def("norm_bwd_coeffs", &iamd::norm_bwd_coeffs, "k1 backward coefficients from the sums");
   m.def("norm_apply", &iamd::norm_apply, "norm + SPADE modulation + activation (k1 fwd)");
   m.def("norm_bwd_reduce", &iamd::norm_bwd_reduce, "k1 backward reduction");
   m.def("norm_bwd_apply", &iamd::norm_bwd_apply, "k1 backward dx");

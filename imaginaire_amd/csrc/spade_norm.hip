@@ -208,7 +208,9 @@ stats_finalize(const float* __restrict__ pcnt, const float* __restrict__ pmean,
                float eps, const float* __restrict__ weight,
                const float* __restrict__ bias, float* __restrict__ out_cnt,
                float* __restrict__ out_mean, float* __restrict__ out_var,
-               float* __restrict__ out_scale, float* __restrict__ out_shift) {
+               float* __restrict__ out_scale, float* __restrict__ out_shift,
+               float* __restrict__ out_rstd, float* __restrict__ run_mean,
+               float* __restrict__ run_var, int64_t* __restrict__ num_batches, float factor) {
   __shared__ float sh_n[kFinRows][64], sh_mean[kFinRows][64], sh_m2[kFinRows][64];
   const int lane = threadIdx.x, row = threadIdx.y;
   const int c = blockIdx.x * 64 + lane;
@@ -234,13 +236,57 @@ stats_finalize(const float* __restrict__ pcnt, const float* __restrict__ pmean,
   out_cnt[idx] = n_a;
   out_mean[idx] = mean_a;
   out_var[idx] = var;
+  const float rstd = rsqrtf(var + eps);
+  if (out_rstd != nullptr) out_rstd[idx] = rstd;
   if (out_scale != nullptr) {
-    const float rstd = rsqrtf(var + eps);
     const float a = weight ? weight[c] : 1.f;
     const float b = bias ? bias[c] : 0.f;
     out_scale[idx] = rstd * a;
     out_shift[idx] = b - mean_a * rstd * a;
   }
+  // running statistics (one group: batch norm), unbiased variance as torch's BatchNorm:
+  // r <- (1 - f) r + f x, in place — replaces ~9 one-element-per-channel PyTorch launches
+  if (run_mean != nullptr) {
+    const float unb = var * n_a / fmaxf(n_a - 1.f, 1.f);
+    run_mean[c] = (1.f - factor) * run_mean[c] + factor * mean_a;
+    run_var[c] = (1.f - factor) * run_var[c] + factor * unb;
+  }
+  if (num_batches != nullptr && idx == 0) num_batches[0] += 1;
+}
+
+// Backward coefficients of the k1 data gradient from the per-sample sums S1 = Σ g', S2 =
+// Σ g'·x̂ ([N, C] each) in one launch (PyTorch: 2 column sums, a stack, a multiply and two
+// divides with their copies per norm layer). Batch norm (per_instance 0): k1 = rstd·w, k2 =
+// ΣS1·invM, k3 = ΣS2·invM ([1, C]); instance norm: k1 = rstd·w, k2 = S1·invM, k3 = S2·invM
+// ([N, C], invM = 1/HW). dw = ΣS2, db = ΣS1 over the batch (affine gradients).
+__global__ void __launch_bounds__(256)
+norm_bwd_coeffs_kernel(const float* __restrict__ S1, const float* __restrict__ S2,
+                       const float* __restrict__ rstd, const float* __restrict__ w, int N, int C,
+                       int per_instance, float invM, float* __restrict__ k1,
+                       float* __restrict__ k2, float* __restrict__ k3, float* __restrict__ dw,
+                       float* __restrict__ db) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const float a = w ? w[c] : 1.f;
+  float s1 = 0.f, s2 = 0.f;
+  for (int n = 0; n < N; ++n) {
+    const float x1 = S1[(int64_t)n * C + c], x2 = S2[(int64_t)n * C + c];
+    s1 += x1;
+    s2 += x2;
+    if (per_instance) {
+      const int64_t o = (int64_t)n * C + c;
+      k1[o] = rstd[o] * a;
+      k2[o] = x1 * invM;
+      k3[o] = x2 * invM;
+    }
+  }
+  if (!per_instance) {
+    k1[c] = rstd[c] * a;
+    k2[c] = s1 * invM;
+    k3[c] = s2 * invM;
+  }
+  if (dw != nullptr) dw[c] = s2;
+  if (db != nullptr) db[c] = s1;
 }
 
 // ------------------------------------------------------------------------
@@ -620,9 +666,15 @@ int apply_grid(int64_t total_vec) {
 
 // Returns (count[G,C], mean[G,C], var[G,C], scale[G,C], shift[G,C]); scale/shift
 // include the per-channel affine (weight/bias may be undefined).
+// running_mean / running_var (fp32 [C], batch statistics only) are updated in place with
+// factor `momentum`, num_batches (int64 [1]) incremented; the 6th output is rstd [G, C].
 std::vector<at::Tensor> norm_stats(const at::Tensor& x, bool per_instance, double eps,
                                    const c10::optional<at::Tensor>& weight,
-                                   const c10::optional<at::Tensor>& bias, bool partial_only) {
+                                   const c10::optional<at::Tensor>& bias, bool partial_only,
+                                   const c10::optional<at::Tensor>& running_mean,
+                                   const c10::optional<at::Tensor>& running_var,
+                                   const c10::optional<at::Tensor>& num_batches,
+                                   double momentum) {
   IAMD_CHECK(x.is_cuda(), "norm_stats: x must be on the GPU");
   Geom g = geom_of(x);
   const int vec = pick_vec(g, x.element_size(), {});
@@ -658,9 +710,28 @@ std::vector<at::Tensor> norm_stats(const at::Tensor& x, bool per_instance, doubl
   auto cnt = at::empty({G, g.C}, fopt), mean = at::empty({G, g.C}, fopt),
        var = at::empty({G, g.C}, fopt);
   at::Tensor scale, shift;
+  auto rstd = at::empty({G, g.C}, fopt);
   if (!partial_only) {
     scale = at::empty({G, g.C}, fopt);
     shift = at::empty({G, g.C}, fopt);
+  }
+  float* rmp = nullptr;
+  float* rvp = nullptr;
+  int64_t* nbp = nullptr;
+  if (running_mean.has_value() && running_mean->defined()) {
+    IAMD_CHECK(!per_instance && running_var.has_value() && running_var->defined() &&
+                   running_mean->scalar_type() == at::kFloat &&
+                   running_var->scalar_type() == at::kFloat && running_mean->is_contiguous() &&
+                   running_var->is_contiguous() && running_mean->numel() == g.C &&
+                   running_var->numel() == g.C,
+               "norm_stats: running statistics must be contiguous fp32 [C] (batch norm)");
+    rmp = running_mean->data_ptr<float>();
+    rvp = running_var->data_ptr<float>();
+  }
+  if (num_batches.has_value() && num_batches->defined()) {
+    IAMD_CHECK(num_batches->scalar_type() == at::kLong && num_batches->numel() == 1,
+               "norm_stats: num_batches must be one int64");
+    nbp = num_batches->data_ptr<int64_t>();
   }
   const float* wp = nullptr;
   const float* bp = nullptr;
@@ -692,9 +763,40 @@ std::vector<at::Tensor> norm_stats(const at::Tensor& x, bool per_instance, doubl
                      stream(), mc, mm, m2p, fN, fP, g.C, (per_instance || RS > 1) ? 1 : 0,
                      (float)eps, wp, bp, cnt.data_ptr<float>(), mean.data_ptr<float>(),
                      var.data_ptr<float>(), partial_only ? nullptr : scale.data_ptr<float>(),
-                     partial_only ? nullptr : shift.data_ptr<float>());
+                     partial_only ? nullptr : shift.data_ptr<float>(), rstd.data_ptr<float>(),
+                     rmp, rvp, nbp, (float)momentum);
   IAMD_LAUNCH_CHECK();
-  return {cnt, mean, var, scale, shift};
+  return {cnt, mean, var, scale, shift, rstd};
+}
+
+// (k1, k2, k3, dweight, dbias) of the k1 backward from the per-sample sums (see kernel)
+std::vector<at::Tensor> norm_bwd_coeffs(const at::Tensor& S1, const at::Tensor& S2,
+                                        const at::Tensor& rstd,
+                                        const c10::optional<at::Tensor>& weight,
+                                        bool per_instance, double invM, bool need_dw,
+                                        bool need_db) {
+  IAMD_CHECK(S1.dim() == 2 && S1.sizes() == S2.sizes() && S1.scalar_type() == at::kFloat &&
+                 S2.scalar_type() == at::kFloat && S1.is_contiguous() && S2.is_contiguous() &&
+                 rstd.scalar_type() == at::kFloat && rstd.is_contiguous(),
+             "norm_bwd_coeffs: fp32 contiguous [N, C] sums and rstd expected");
+  const int N = (int)S1.size(0), C = (int)S1.size(1);
+  IAMD_CHECK(rstd.numel() == (per_instance ? (int64_t)N * C : (int64_t)C),
+             "norm_bwd_coeffs: rstd shape");
+  auto fopt = S1.options();
+  const int64_t R = per_instance ? N : 1;
+  auto k1 = at::empty({R, C}, fopt), k2 = at::empty({R, C}, fopt), k3 = at::empty({R, C}, fopt);
+  at::Tensor wf, dw, db;
+  if (weight.has_value() && weight->defined()) wf = weight->contiguous().to(at::kFloat);
+  if (need_dw) dw = at::empty({C}, fopt);
+  if (need_db) db = at::empty({C}, fopt);
+  hipLaunchKernelGGL(norm_bwd_coeffs_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, stream(),
+                     S1.data_ptr<float>(), S2.data_ptr<float>(), rstd.data_ptr<float>(),
+                     wf.defined() ? wf.data_ptr<float>() : nullptr, N, C, per_instance ? 1 : 0,
+                     (float)invM, k1.data_ptr<float>(), k2.data_ptr<float>(), k3.data_ptr<float>(),
+                     need_dw ? dw.data_ptr<float>() : nullptr,
+                     need_db ? db.data_ptr<float>() : nullptr);
+  IAMD_LAUNCH_CHECK();
+  return {k1, k2, k3, dw, db};
 }
 
 at::Tensor norm_apply(const at::Tensor& x, const at::Tensor& scale, const at::Tensor& shift,

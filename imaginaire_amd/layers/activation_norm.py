@@ -123,13 +123,23 @@ class _FusedNormBase(nn.Module):
             nn.init.ones_(self.weight)
             nn.init.zeros_(self.bias)
 
-    def _factor(self):
+    def _factor(self, defer_count=False):
+        """Running-average factor of this call. With ``defer_count`` (and a fixed momentum)
+        ``num_batches_tracked`` is NOT incremented here: the caller hands it to
+        :func:`fused_norm_act`, whose statistics kernel increments it."""
         if not (self.training and self.track_running_stats):
             return 0.0
+        if defer_count and self.momentum is not None:
+            return self.momentum
         self.num_batches_tracked.add_(1)
         if self.momentum is None:
             return 1.0 / float(self.num_batches_tracked.item())
         return self.momentum
+
+    def _deferred_count(self, use_batch):
+        return self.num_batches_tracked if (
+            use_batch and self.training and self.track_running_stats and
+            self.momentum is not None) else None
 
     def _effective_mode(self):
         return self.mode
@@ -150,8 +160,9 @@ class _FusedNormBase(nn.Module):
             x, self._effective_mode(), self.weight, self.bias, gamma=gamma, beta=beta, gb=gb,
             running_mean=self.running_mean if self.track_running_stats else None,
             running_var=self.running_var if self.track_running_stats else None,
-            training=use_batch, momentum=self._factor() if use_batch else 0.0, eps=self.eps,
-            slope=act_slope, process_group=self.process_group, deferred=deferred)
+            training=use_batch, momentum=self._factor(True) if use_batch else 0.0, eps=self.eps,
+            slope=act_slope, process_group=self.process_group, deferred=deferred,
+            num_batches=self._deferred_count(use_batch))
         if squeeze is not None:
             y = y.reshape(squeeze)
         return y

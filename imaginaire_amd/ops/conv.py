@@ -207,6 +207,22 @@ def _out_hw(H, W, k, stride, padding, dilation):
             (W + 2 * padding[1] - dilation[1] * (k[1] - 1) - 1) // stride[1] + 1)
 
 
+# > 0 inside utils.cuda_graph.graph_routing() (a graphed step's warm-up, its capture and
+# eager comparisons against it): global, not thread-local — the backward runs on autograd's
+# worker thread
+_GRAPH_ROUTING = [0]
+
+
+def _capturing():
+    """True while a hipGraph is being captured on the current stream, or inside a graphed
+    step's warm-up. MIOpen's backward solvers for small problems accumulate with atomics into
+    buffers zeroed by calls that stream capture does not record, so under replay they add onto
+    the previous replay's values (the pix2pixHD graph diverged to NaN in its 16 x 16 resblock
+    weight gradients, scripts/probe/graph_stash_probe.py): there every conv k10 / k11 can run
+    takes them, whatever its grid size."""
+    return _GRAPH_ROUTING[0] > 0 or torch.cuda.is_current_stream_capturing()
+
+
 def mfma_eligible(x, w, stride, padding, dilation, groups):
     """True if the k10 MFMA kernel runs this conv (see module docstring)."""
     if not (x.is_cuda and x.dim() == 4 and w.dim() == 4 and groups == 1 and _mfma_enabled()):
@@ -235,7 +251,8 @@ def mfma_eligible(x, w, stride, padding, dilation, groups):
     # MIOpen's immediate-mode solvers for them may split K with atomics
     # narrow outputs (flow / mask heads, FlowNet2's predict_flow on 1/64-scale maps): MIOpen
     # takes ~0.65 ms for a [2, 1056, 16, 32] -> 2-channel 3x3 conv; k10 splits K over the grid
-    return blocks >= _MFMA_MIN_BLOCKS or cout <= 8 or torch.are_deterministic_algorithms_enabled()
+    return blocks >= _MFMA_MIN_BLOCKS or cout <= 8 or \
+        torch.are_deterministic_algorithms_enabled() or _capturing()
 
 
 def _flip_t(w):
@@ -334,6 +351,7 @@ class _MfmaConv2d(torch.autograd.Function):
             # identity activation: the k2 kernel reads only dy (y stands in for the layout)
             dy, db = _ext.ext().bias_act_bwd(y if y is not None else dy, dy, slope)
         dx = dw = None
+        cap = _capturing()
         if need_x:
             kh, kw = wb.shape[2], wb.shape[3]
             pt = (dilation[0] * (kh - 1) - padding[0], dilation[1] * (kw - 1) - padding[1])
@@ -343,21 +361,21 @@ class _MfmaConv2d(torch.autograd.Function):
             # the dgrad GEMM has N = Cin (few tiles, K = taps x Cout for the SPADE γ/β convs):
             # k10 splits K over the grid's y dimension for those
             fl = 2.0 * dy.shape[0] * dy.shape[2] * dy.shape[3] * wb.numel()
-            if stride == (1, 1) and dilation == (1, 1) and pt[0] >= 0 and pt[1] >= 0 and \
-                    dblocks >= _MFMA_MIN_DGRAD_BLOCKS:
+            big = dblocks >= _MFMA_MIN_DGRAD_BLOCKS or cap
+            if stride == (1, 1) and dilation == (1, 1) and pt[0] >= 0 and pt[1] >= 0 and big:
                 # k10 v4 reads the forward weight tap-flipped and transposed in-kernel (no
                 # flipped weight copy); other shapes flip once inside and run the k10 routing
                 with _Logged('dgrad', 'k10', fl, _gemm_desc(dy, wb.transpose(0, 1), (1, 1), pt)):
                     dx = _ext.ext().conv2d_dgrad_mfma(dy, wb, padding[0], padding[1])
-            elif stride == (1, 1) and pt[0] >= 0 and pt[1] >= 0 and \
-                    dblocks >= _MFMA_MIN_DGRAD_BLOCKS:
+            elif stride == (1, 1) and pt[0] >= 0 and pt[1] >= 0 and big:
                 wt = _flip_t(wb)
                 with _Logged('dgrad', 'k10', fl, _gemm_desc(dy, wt, (1, 1), pt)):
                     dx = _ext.ext().conv2d_mfma(dy, wt, None, 1, 1, pt[0], pt[1],
                                                 dilation[0], dilation[1], 1.0)
             elif _STRIDED_DGRAD and stride[0] == stride[1] and 2 <= stride[0] <= 4 and \
-                    dilation == (1, 1) and dblocks >= _MFMA_MIN_DGRAD_BLOCKS * stride[0] ** 2 and \
-                    xb.shape[0] * xb.shape[2] * xb.shape[3] >= _STRIDED_DGRAD_MIN_PIX:
+                    dilation == (1, 1) and (cap or (
+                        dblocks >= _MFMA_MIN_DGRAD_BLOCKS * stride[0] ** 2 and
+                        xb.shape[0] * xb.shape[2] * xb.shape[3] >= _STRIDED_DGRAD_MIN_PIX)):
                 # large maps only: 1.3-1.6x MIOpen on the full-resolution PatchGAN layers, on par
                 # or slower below ~128K dx pixels (profiles/strided_dgrad_probe_mi355x.txt)
                 with _Logged('dgrad', 'k10s', fl, _gemm_desc(dy, wb, stride, padding)):
@@ -610,7 +628,7 @@ def _wgrad(dy, xb, wb, stride, padding, dilation, cout=-1, cin=-1, wdt=torch.flo
     mode = _MFMA_WGRAD
     fl = 2.0 * dy.shape[0] * dy.shape[2] * dy.shape[3] * wb.numel()
     desc = _gemm_desc(xb, wb, stride, padding)
-    if mode == '0':
+    if mode == '0' and not _capturing():
         with _Logged('wgrad', 'miopen', fl, desc):
             return miopen()
     variants = _k11_variants(dy, xb, wb, stride, dilation)
@@ -626,7 +644,7 @@ def _wgrad(dy, xb, wb, stride, padding, dilation, cout=-1, cin=-1, wdt=torch.flo
         _WGRAD_PENDING.setdefault(key, (dy.dtype, xb.dtype, wb.dtype))
         choice = 'k11'
     with _Logged('wgrad', choice, fl, desc):
-        if choice == 'miopen':
+        if choice == 'miopen' and not _capturing():
             return miopen()
         if choice == 'k11v2':
             return k11(2)

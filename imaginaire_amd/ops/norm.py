@@ -137,6 +137,16 @@ def prefetch_sync_stats(x, eps, group):
     x._iamd_bn_stats = (key, 'pending', work, allst, stacked)
 
 
+def _native_running(running_mean, running_var, cfg):
+    """The running statistics can be updated by the k1 finalize kernel (fp32, contiguous)."""
+    if running_mean is None:
+        return cfg.num_batches is None or cfg.num_batches.dtype == torch.int64
+    return (running_var is not None and running_mean.dtype == torch.float32 and
+            running_var.dtype == torch.float32 and running_mean.is_contiguous() and
+            running_var.is_contiguous() and
+            (cfg.num_batches is None or cfg.num_batches.dtype == torch.int64))
+
+
 def _update_running(running_mean, running_var, mean, var, count, factor):
     if running_mean is None:
         return
@@ -161,9 +171,11 @@ def _expand_mod(t, x):
 
 class _NormCfg:
     __slots__ = ('mode', 'training', 'momentum', 'eps', 'slope', 'group', 'use_batch_stats',
-                 'deferred')
+                 'deferred', 'num_batches')
 
-    def __init__(self, mode, training, momentum, eps, slope, group, deferred=None):
+    def __init__(self, mode, training, momentum, eps, slope, group, deferred=None,
+                 num_batches=None):
+        self.num_batches = num_batches
         self.mode = mode
         self.training = training
         self.momentum = momentum
@@ -248,6 +260,7 @@ class _FusedNormActFn(torch.autograd.Function):
         wf = weight.float() if weight is not None else None
         bf = bias.float() if bias is not None else None
         per_instance = cfg.mode == 'instance'
+        updated = False
         if cfg.mode == 'none':
             mean = x.new_zeros((1, C), dtype=torch.float32)
             var = x.new_ones((1, C), dtype=torch.float32)
@@ -265,13 +278,23 @@ class _FusedNormActFn(torch.autograd.Function):
             else:
                 if cached is not None:  # merged statistics of a prefetched exchange
                     count, mean, var = cached
-                    scale = None
+                    scale = rstd = None
                 else:
-                    count, mean, var, scale, shift = ext.norm_stats(x, per_instance, cfg.eps, wf,
-                                                                    bf, sync)
+                    # without a cross-rank merge the finalize kernel also updates the running
+                    # statistics and the batch counter in place
+                    fold = (not sync and cfg.training and not per_instance and
+                            _native_running(running_mean, running_var, cfg))
+                    count, mean, var, scale, shift, rstd = ext.norm_stats(
+                        x, per_instance, cfg.eps, wf, bf, sync,
+                        running_mean if fold else None, running_var if fold else None,
+                        cfg.num_batches if fold else None, float(cfg.momentum))
+                    if fold:
+                        updated = True
                     if sync:
                         count, mean, var = _merge_stats(count, mean, var, cfg.group)
-                rstd = torch.rsqrt(var + cfg.eps)
+                        rstd = None
+                if rstd is None:
+                    rstd = torch.rsqrt(var + cfg.eps)
                 if sync or scale is None:
                     a = wf.reshape(1, C) if wf is not None else 1.0
                     b = bf.reshape(1, C) if bf is not None else 0.0
@@ -279,7 +302,7 @@ class _FusedNormActFn(torch.autograd.Function):
                     shift = (b - mean * scale).contiguous()
                 if shareable:
                     x._iamd_bn_stats = (key, 'done', (count, mean, var, rstd, scale, shift))
-            if cfg.training and not per_instance:
+            if cfg.training and not per_instance and not updated:
                 _update_running(running_mean, running_var, mean, var, count, cfg.momentum)
         else:  # eval with running statistics
             mean = running_mean.float().reshape(1, C)
@@ -290,6 +313,8 @@ class _FusedNormActFn(torch.autograd.Function):
             scale = (rstd * a).contiguous()
             shift = (b - mean * scale).contiguous()
             count = None
+        if cfg.num_batches is not None and not updated:
+            cfg.num_batches.add_(1)
         out = ext.norm_apply(x, scale, shift, gamma_v, beta_v, cfg.slope)
         ctx.cfg = cfg
         ctx.has_gb = gb is not None
@@ -336,9 +361,25 @@ class _FusedNormActFn(torch.autograd.Function):
             dgamma = dgam_v.to(ctx.mod_dtypes[0])
             dbeta = dbet_v.to(ctx.mod_dtypes[1])
         N, HW = x.shape[0], x.shape[2] * x.shape[3]
-        dweight = S2.sum(0).to(weight.dtype) if weight is not None and ctx.needs_input_grad[1] else None
+        sync = cfg.mode == 'sync_batch' and sync_active(cfg.group)
+        need_dw = weight is not None and ctx.needs_input_grad[1]
+        need_db = ctx.needs_input_grad[2]
+        if cfg.use_batch_stats and cfg.mode != 'none' and not sync and \
+                S1.dtype == torch.float32 and S1.is_contiguous() and S2.is_contiguous():
+            # one launch for k1 / k2 / k3 and the affine gradients
+            inst = cfg.mode == 'instance'
+            k1, k2, k3, dw32, db32 = ext.norm_bwd_coeffs(
+                S1, S2, rstd.contiguous(), weight, inst, 1.0 / float(HW if inst else N * HW),
+                need_dw, need_db)
+            dweight = dw32.to(weight.dtype) if need_dw else None
+            dbias = db32.to(weight.dtype if weight is not None else torch.float32) \
+                if need_db else None
+            dx = ext.norm_bwd_apply(x, dout, scale, shift, mean, rstd, k1, k2, k3, gamma_v,
+                                    beta_v, cfg.slope) if ctx.needs_input_grad[0] else None
+            return dx, dweight, dbias, dgamma, dbeta, dgb, None, None, None
+        dweight = S2.sum(0).to(weight.dtype) if need_dw else None
         dbias = S1.sum(0).to(weight.dtype if weight is not None else torch.float32) \
-            if ctx.needs_input_grad[2] else None
+            if need_db else None
         if cfg.mode == 'none' or not cfg.use_batch_stats:
             # no batch statistics in the graph: dx = g * scale
             k1 = scale.contiguous()
@@ -351,7 +392,6 @@ class _FusedNormActFn(torch.autograd.Function):
             k3 = (S2 / HW).contiguous()
         else:
             s = torch.stack([S1.sum(0), S2.sum(0)], 0)
-            sync = cfg.mode == 'sync_batch' and sync_active(cfg.group)
             M = ctx.count.reshape(1, C) if sync else float(N * HW)
             k1 = (rstd * (weight.float().reshape(1, C) if weight is not None else 1.0)).contiguous()
             h = cfg.deferred
@@ -445,10 +485,11 @@ class _SyncStats(torch.autograd.Function):
 
 def fused_norm_act(x, mode='batch', weight=None, bias=None, gamma=None, beta=None, gb=None,
                    running_mean=None, running_var=None, training=True, momentum=0.1,
-                   eps=1e-5, slope=1.0, process_group=None, deferred=None):
+                   eps=1e-5, slope=1.0, process_group=None, deferred=None, num_batches=None):
     """``act((norm(x)·w + b)·(1+γ) + β)`` — see module docstring.
 
-    ``momentum`` is the already-resolved exponential-average factor.
+    ``momentum`` is the already-resolved exponential-average factor. ``num_batches`` (the
+    layer's ``num_batches_tracked``) is incremented when the running statistics are updated.
     ``gb`` is an alternative to (γ, β): one [N, 2C, H, W] tensor whose first C
     channels are γ and last C are β (output of a fused γ|β convolution).
     """
@@ -456,7 +497,8 @@ def fused_norm_act(x, mode='batch', weight=None, bias=None, gamma=None, beta=Non
         mode_eff = 'batch'
     else:
         mode_eff = mode
-    cfg = _NormCfg(mode_eff, training, momentum, eps, slope, process_group, deferred)
+    cfg = _NormCfg(mode_eff, training, momentum, eps, slope, process_group, deferred,
+                   num_batches)
     if gamma is not None and gamma.dim() == 2 and x.shape[2] * x.shape[3] == 1:
         gamma = gamma.reshape(x.shape[0], x.shape[1], 1, 1)
         beta = beta.reshape(x.shape[0], x.shape[1], 1, 1)
@@ -474,4 +516,6 @@ def fused_norm_act(x, mode='batch', weight=None, bias=None, gamma=None, beta=Non
             beta = beta.contiguous(memory_format=fmt)
         return _FusedNormActFn.apply(x, weight, bias, gamma, beta, gb, running_mean,
                                      running_var, cfg)
+    if num_batches is not None:
+        num_batches.add_(1)
     return _reference(x, mode_eff, weight, bias, gamma, beta, gb, running_mean, running_var, cfg)

@@ -50,8 +50,11 @@ def _static_copy(dst, src):
     if torch.is_tensor(dst):
         dst.copy_(src, non_blocking=True)
     elif isinstance(dst, dict):
-        for k in dst:
-            _static_copy(dst[k], src[k])
+        # the captured step may have added entries to its static batch (e.g. the SPADE
+        # trainer's style noise 'z'): those are outputs of the graph, not inputs
+        for k in src:
+            if k in dst:
+                _static_copy(dst[k], src[k])
     elif isinstance(dst, (list, tuple)):
         for d, s in zip(dst, src):
             _static_copy(d, s)
@@ -97,6 +100,27 @@ def _signature(x):
         return ('V', x)
     except TypeError:
         return ('V', repr(x))
+
+
+class graph_routing(object):
+    """Kernel routing of a graphed step, for its warm-up, its capture and any eager run compared
+    against its replay: every conv k10 / k11 can run takes them whatever its grid size
+    (ops/conv.py ``_capturing``), and the remaining MIOpen calls use deterministic solvers. The
+    small-problem MIOpen backward solvers picked otherwise accumulate with atomics into buffers
+    zeroed outside the captured stream, so a replay adds onto the previous replay's values.
+    Warm-up runs under it too, so the capture records the kernels the warm-up already ran."""
+
+    def __enter__(self):
+        from imaginaire_amd.ops import conv
+        self.prev = torch.backends.cudnn.deterministic
+        torch.backends.cudnn.deterministic = True
+        conv._GRAPH_ROUTING[0] += 1
+        return self
+
+    def __exit__(self, *exc):
+        from imaginaire_amd.ops import conv
+        conv._GRAPH_ROUTING[0] -= 1
+        torch.backends.cudnn.deterministic = self.prev
 
 
 class GraphedStep(object):
@@ -177,7 +201,7 @@ class GraphedStep(object):
             # remember the stream they were created on
             st = self._side_stream()
             st.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(st):
+            with torch.cuda.stream(st), graph_routing():
                 self.step_fn(data)
             torch.cuda.current_stream().wait_stream(st)
             ent['n_eager'] += 1
@@ -200,7 +224,7 @@ class GraphedStep(object):
             # its work events while a (seconds-long) step is being captured; under the default
             # global mode those calls from another thread are refused and abort the process
             with torch.cuda.graph(g, pool=self.pool, stream=st,
-                                  capture_error_mode='thread_local'):
+                                  capture_error_mode='thread_local'), graph_routing():
                 self.step_fn(ent['static'])
         except Exception as e:  # noqa: BLE001 - any capture failure: stay eager
             if os.environ.get('IMAGINAIRE_AMD_GRAPH_DEBUG'):

@@ -19,6 +19,8 @@ name = sys.argv[1] if len(sys.argv) > 1 else 'pix2pixHD'
 seq = int(sys.argv[2]) if len(sys.argv) > 2 else None
 from imaginaire_amd.utils.cuda_graph import make_trainer_step  # noqa: E402
 torch.cuda.set_device(0)
+if os.environ.get('IAMD_PROBE_DET') == '1':  # MIOpen: deterministic (non-atomic) solvers
+    torch.backends.cudnn.deterministic = True
 cfg, tr, batches = _build(name, seq)
 step, graphed = make_trainer_step(tr, warmup=2, enabled=True)
 for i in range(3):

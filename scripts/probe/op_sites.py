@@ -97,6 +97,15 @@ def record_sites(step_fn, ops=DEFAULT_OPS, top=60, out=sys.stdout):
     for (name, shape, dt, st), (n, b) in rows[:top]:
         print('%8.1f MB %4d  %-20s %-9s %-26s %s' % (b / 1e6, n, name, dt, str(shape)[:26], st),
               file=out)
+    # launch-count view: small ops cost a kernel each whatever their bytes
+    by_site = collections.defaultdict(lambda: [0, 0])
+    for (name, shape, dt, st), (n, b) in rows:
+        s = by_site[(name, dt, st)]
+        s[0] += n
+        s[1] += b
+    print('\nby call count (op, dtype, site; all shapes):', file=out)
+    for (name, dt, st), (n, b) in sorted(by_site.items(), key=lambda kv: -kv[1][0])[:top]:
+        print('%5d %9.1f MB  %-20s %-9s %s' % (n, b / 1e6, name, dt, st), file=out)
 
 
 if __name__ == '__main__':

@@ -89,7 +89,7 @@ def _losses(tr):
 @pytest.mark.parametrize('name,seq_len', [('munit', None), ('pix2pixHD', None),
                                           ('vid2vid_street', 3), ('fs_vid2vid_face', 2)])
 def test_family_graph_replay_matches_eager(name, seq_len):
-    from imaginaire_amd.utils.cuda_graph import make_trainer_step
+    from imaginaire_amd.utils.cuda_graph import graph_routing, make_trainer_step
     torch.cuda.set_device(0)
     cfg, tr, batches = _build(name, seq_len)
     assert getattr(tr, 'graph_capturable', False), name + ' is not marked capturable'
@@ -116,7 +116,8 @@ def test_family_graph_replay_matches_eager(name, seq_len):
     torch.cuda.synchronize()
     d = tr.start_of_iteration(_fresh(batches[1]), 3)
     torch.manual_seed(11)
-    graphed.step_fn(d)
+    with graph_routing():  # the kernels the capture recorded
+        graphed.step_fn(d)
     torch.cuda.synchronize()
     le = _losses(tr)
     de = [p.detach() - q for p, q in zip(gparams, p0)]

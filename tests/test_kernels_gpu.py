@@ -1196,3 +1196,30 @@ def test_conv2d_dgrad_mfma(case):
     assert got.shape == ref.shape
     scale = ref.abs().max().item()
     assert (got.float() - ref).abs().max().item() <= 1e-2 * scale
+
+
+@pytest.mark.parametrize('affine', [True, False])
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_batchnorm_running_stats_match_torch(affine, dtype):
+    """The k1 statistics kernel updates running_mean / running_var / num_batches_tracked in
+    place (one launch instead of ~10 per layer): three training calls and one eval call against
+    torch.nn.BatchNorm2d in fp32."""
+    from imaginaire_amd.layers.activation_norm import BatchNorm2d
+    torch.manual_seed(0)
+    C = 48
+    ours = BatchNorm2d(C, affine=affine).cuda()
+    ref = torch.nn.BatchNorm2d(C, affine=affine).cuda()
+    for i in range(3):
+        x = (torch.randn(3, C, 10, 14, device='cuda') * (1 + i) + 0.5 * i)
+        x = x.to(dtype).contiguous(memory_format=torch.channels_last)
+        y = ours.fused(x)
+        yr = ref(x.float())
+        tol = 3e-2 if dtype == torch.bfloat16 else 1e-4
+        assert torch.allclose(y.float(), yr, atol=tol, rtol=tol)
+    assert int(ours.num_batches_tracked) == int(ref.num_batches_tracked) == 3
+    assert torch.allclose(ours.running_mean, ref.running_mean, atol=1e-3, rtol=1e-3)
+    assert torch.allclose(ours.running_var, ref.running_var, atol=1e-3, rtol=1e-3)
+    ours.eval()
+    ref.eval()
+    x = torch.randn(2, C, 6, 6, device='cuda').contiguous(memory_format=torch.channels_last)
+    assert torch.allclose(ours.fused(x).float(), ref(x), atol=1e-4, rtol=1e-4)
