@@ -237,7 +237,8 @@ def mfma_eligible(x, w, stride, padding, dilation, groups):
     # up to 2x padding waste still runs k10 for the 32-channel full-resolution layers of the
     # video models (MIOpen's NHWC bf16 solvers reach only 35-150 TF/s on [2, 32, 512, 1024]
     # 1x1 / 3x3 convs, profiles/recipe_vid2vid512x1024_conv_log_mi355x.txt)
-    if cp * op * 3 > cin * cout * 4 and min(cin, cout) > 16 and cp * op > 2 * cin * cout:
+    if cp * op * 3 > cin * cout * 4 and min(cin, cout) > 16 and cp * op > 2 * cin * cout and \
+            not _capturing():  # (in a graph: padded MFMA work rather than MIOpen's backward)
         return False
     ho, wo = _out_hw(x.shape[2], x.shape[3], w.shape[2:], stride, padding, dilation)
     if ho <= 0 or wo <= 0 or w.shape[2] * w.shape[3] > 64:  # k10 tap masks are 64-bit

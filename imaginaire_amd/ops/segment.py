@@ -4,11 +4,55 @@ Reference generators/pix2pixHD.py:323-349 loops in Python over instance ids and 
 with ``.nonzero()`` (a host sync per instance). Here the (batch, instance-id) pairs are hashed
 to one key per pixel and SORTED (a static-shape device sort, no host sync — so the pooling
 also runs inside a captured hipGraph, where ``torch.unique``'s data-dependent output size
-cannot): run starts of the sorted keys give a dense segment id per pixel, per-segment channel
-sums and counts go into a pixel-count-sized table with ``index_add_``, and the means are
-gathered back.
+cannot). In sorted order every segment is a contiguous run: its sum is the difference of an
+fp64 running sum (cumsum) at the run's two ends and its count the run length, found with a
+cummax / reversed cummax of the run boundaries. The averaging operator is symmetric, so the
+backward is the same segment mean of the incoming gradient (an autograd Function: no
+``index_add_`` scatter in either direction). No atomics anywhere: the earlier ``index_add_``
+into a per-segment table serialised on the few large instances (~20 ms per pix2pixHD 512x1024
+iteration, profiles/recipe_pix2pixhd512x1024_kernels_mi355x.txt).
 """
 import torch
+
+
+def _runs(key):
+    """Sort order of ``key`` and, per sorted position, the first / last sorted position of its
+    run of equal keys."""
+    n = key.numel()
+    sk, perm = torch.sort(key)
+    pos = torch.arange(n, device=key.device)
+    first = torch.ones(n, dtype=torch.bool, device=key.device)
+    first[1:] = sk[1:] != sk[:-1]
+    last = torch.ones(n, dtype=torch.bool, device=key.device)
+    last[:-1] = first[1:]
+    zero = torch.zeros_like(pos)
+    s = torch.cummax(torch.where(first, pos, zero), 0)[0]
+    e = (n - 1) - torch.cummax(torch.where(last, n - 1 - pos, zero).flip(0), 0)[0].flip(0)
+    return perm, s, e
+
+
+def _segment_mean(x, perm, s, e):
+    """x [n, c] (pixel order) -> per-pixel mean over its run (same layout, fp32)."""
+    c = x.shape[1]
+    cs = torch.cumsum(x.index_select(0, perm).double(), 0)
+    cs = torch.cat([cs.new_zeros((1, c)), cs], 0)        # cs[i] = sum of the first i sorted rows
+    seg = cs.index_select(0, e + 1) - cs.index_select(0, s)
+    means = (seg / (e - s + 1).unsqueeze(1).double()).to(torch.float32)
+    out = torch.empty_like(means)
+    out[perm] = means                                     # back to pixel order (a permutation)
+    return out
+
+
+class _SegmentMean(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, perm, s, e):
+        ctx.save_for_backward(perm, s, e)
+        return _segment_mean(x, perm, s, e)
+
+    @staticmethod
+    def backward(ctx, g):
+        perm, s, e = ctx.saved_tensors
+        return _segment_mean(g.float(), perm, s, e), None, None, None
 
 
 def instance_mean(features, instance_map):
@@ -16,21 +60,10 @@ def instance_mean(features, instance_map):
     b, c, h, w = features.shape
     inst = instance_map.reshape(b, -1).long()
     key = (inst + (torch.arange(b, device=inst.device).view(b, 1) << 32)).reshape(-1)
-    n = key.numel()
-    sk, perm = torch.sort(key)
-    start = torch.ones_like(sk, dtype=torch.long)
-    start[1:] = (sk[1:] != sk[:-1]).long()
-    seg_sorted = torch.cumsum(start, 0) - 1          # dense segment id in sorted order
-    seg = torch.empty_like(seg_sorted)
-    seg[perm] = seg_sorted                           # segment id of every pixel
+    perm, s, e = _runs(key)
     feats = features.permute(0, 2, 3, 1).reshape(-1, c).float()
-    sums = torch.zeros(n, c, device=features.device, dtype=torch.float32)
-    sums.index_add_(0, seg, feats)
-    counts = torch.zeros(n, device=features.device, dtype=torch.float32)
-    counts.index_add_(0, seg, torch.ones_like(seg, dtype=torch.float32))
-    means = sums / counts.clamp_min(1).unsqueeze(1)
-    out = means.index_select(0, seg).reshape(b, h, w, c).permute(0, 3, 1, 2)
-    return out.to(features.dtype).contiguous()
+    out = _SegmentMean.apply(feats, perm, s, e)
+    return out.reshape(b, h, w, c).permute(0, 3, 1, 2).to(features.dtype).contiguous()
 
 
 def get_edges(t):

@@ -104,23 +104,21 @@ def _signature(x):
 
 class graph_routing(object):
     """Kernel routing of a graphed step, for its warm-up, its capture and any eager run compared
-    against its replay: every conv k10 / k11 can run takes them whatever its grid size
-    (ops/conv.py ``_capturing``), and the remaining MIOpen calls use deterministic solvers. The
-    small-problem MIOpen backward solvers picked otherwise accumulate with atomics into buffers
-    zeroed outside the captured stream, so a replay adds onto the previous replay's values.
-    Warm-up runs under it too, so the capture records the kernels the warm-up already ran."""
+    against its replay: every conv k10 / k11 can run takes them, whatever its grid size or
+    channel-padding waste (ops/conv.py ``_capturing``). The small-problem MIOpen backward
+    solvers accumulate with atomics into buffers zeroed outside the captured stream, so a replay
+    adds onto the previous replay's values (and MIOpen's deterministic mode is no way out: it
+    falls back to its naive direct kernels, ~11 s per MUNIT recipe iteration). Warm-up runs
+    under it too, so the capture records the kernels the warm-up already ran."""
 
     def __enter__(self):
         from imaginaire_amd.ops import conv
-        self.prev = torch.backends.cudnn.deterministic
-        torch.backends.cudnn.deterministic = True
         conv._GRAPH_ROUTING[0] += 1
         return self
 
     def __exit__(self, *exc):
         from imaginaire_amd.ops import conv
         conv._GRAPH_ROUTING[0] -= 1
-        torch.backends.cudnn.deterministic = self.prev
 
 
 class GraphedStep(object):

@@ -16,7 +16,7 @@ run() {  # name, timeout, args...
   if [ -n "$ONLY" ] && [[ " $ONLY " != *" $name "* ]]; then return 0; fi
   for rep in $(seq 1 "$REPS"); do
     local extra=""
-    [ "$rep" = 1 ] && extra="--conv-log"
+    [ "$rep" = 1 ] && [ -n "$CONVLOG" ] && extra="--conv-log"
     timeout -k 10 "$t" python scripts/bench_families.py "$@" --steps "$STEPS" --warmup 4 $extra $EXTRA \
       >> "$OUT/recipes.jsonl" 2> "$OUT/${name}_$rep.err"
     local rc=$?
@@ -31,7 +31,7 @@ run() {  # name, timeout, args...
     done
     (cd /tmp && TMPDIR=/tmp timeout -k 10 "$t" rocprofv3 --kernel-trace --stats --output-format csv \
       -d /tmp/iamd_rprof -o run -- python3 "$ROOT/scripts/bench_families.py" "${args[@]}" \
-      --steps 5 --warmup 4 > "$OUT/${name}_prof.log" 2>&1)
+      --steps 5 --warmup 4 $EXTRA > "$OUT/${name}_prof.log" 2>&1)
     local prc=$?
     echo "[r3rec] $name rocprof rc=$prc"
     [ $prc -eq 0 ] || exit $prc

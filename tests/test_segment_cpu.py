@@ -20,3 +20,17 @@ def test_instance_mean_matches_reference_loop():
     inst = (torch.randint(0, 6, (3, 1, 12, 10)) * 1000 + 26).float()
     inst[1] = 26.0  # one sample with a single instance
     torch.testing.assert_close(instance_mean(f, inst), _reference(f, inst), atol=1e-6, rtol=1e-5)
+
+
+def test_instance_mean_gradient_is_segment_mean():
+    """The averaging operator is symmetric: the backward (an autograd Function, no scatter)
+    must equal autograd through the reference per-instance loop."""
+    from imaginaire_amd.ops.segment import instance_mean
+    torch.manual_seed(1)
+    f = torch.randn(2, 3, 9, 13, requires_grad=True)
+    inst = torch.randint(0, 4, (2, 1, 9, 13)).float()
+    g = torch.randn(2, 3, 9, 13)
+    instance_mean(f, inst).backward(g)
+    f2 = f.detach().clone().requires_grad_(True)
+    _reference(f2, inst).backward(g)
+    torch.testing.assert_close(f.grad, f2.grad, atol=1e-6, rtol=1e-5)
