@@ -422,6 +422,18 @@ class MultiOutConv2dBlock(_MultiOutBaseConvBlock):
                          inplace_nonlinearity, apply_noise, order, 2)
 
 
+class NHWCConv2d(nn.Conv2d):
+    """``nn.Conv2d`` (same parameters and state-dict keys) that runs through the k10 / k11 conv
+    routing of :mod:`imaginaire_amd.ops.conv` instead of calling MIOpen directly — the bare
+    1x1 style heads of the MUNIT / FUNIT style encoders (reference generators/munit.py:
+    ``nn.Conv2d(num_filters, style_channels, 1, 1, 0)``); inside a captured graph MIOpen's
+    small-problem backward solvers must not run."""
+
+    def forward(self, x):
+        return nhwc_conv.conv2d(x, self.weight, self.bias, self.stride, self.padding,
+                                self.dilation, self.groups, self.padding_mode)
+
+
 class PartialConv2d(nn.Conv2d):
     """Partial convolution (Liu et al.; reference conv.py:927-1009).
 

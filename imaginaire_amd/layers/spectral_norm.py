@@ -118,9 +118,17 @@ def spectral_norm(module, name='weight', n_power_iterations=1, eps=1e-12, dim=No
 
 class _SNGroup:
     """Forward pre-hook of a network: one batched power iteration for all of
-    its (dim-0, single-iteration) SN layers."""
+    its (dim-0, single-iteration) SN layers.
 
-    def __init__(self, net):
+    ``sub=True``: the hook of a sub-module of a grouped network (an encoder / decoder / block
+    with >= 2 SN layers). It iterates its layers only when every one of them has already
+    consumed the network-level iteration — i.e. on a SECOND call of the sub-module within one
+    network forward (MUNIT / UNIT re-encode translated images; reference torch semantics: one
+    power iteration per layer call) — instead of each layer falling back to its own per-layer
+    iteration (~10 small PyTorch launches forward and ~6 backward per layer per call)."""
+
+    def __init__(self, net, sub=False):
+        self.sub = sub
         self.entries = self._collect(net)
 
     @staticmethod
@@ -139,6 +147,8 @@ class _SNGroup:
             self.entries = self._collect(net)  # SN removed/added since (e.g. EMA copy)
         if not self.entries:
             return
+        if self.sub and any(getattr(h, '_batched', None) is not None for _, h in self.entries):
+            return  # first call within this forward: the network-level iteration is pending
         w0 = getattr(self.entries[0][0], self.entries[0][1].name + '_orig')
         if not _ext.use_native(w0):
             return
@@ -166,11 +176,18 @@ class _SNGroup:
 
 
 def install_batched_spectral_norm(net):
-    """Register the batched SN pre-hook on ``net``; returns the number of layers covered."""
+    """Register the batched SN pre-hook on ``net`` (and the re-call hooks of its sub-modules
+    holding >= 2 SN layers); returns the number of layers covered."""
     group = _SNGroup(net)
     if group.entries:
         net.register_forward_pre_hook(group)
         net._iamd_sn_group = group
+        for m in net.modules():
+            if m is net or any(isinstance(h, _SNGroup) for h in m._forward_pre_hooks.values()):
+                continue
+            sub = _SNGroup(m, sub=True)
+            if len(sub.entries) >= 2:
+                m.register_forward_pre_hook(sub)
     return len(group.entries)
 
 

@@ -467,7 +467,9 @@ def per_sample_eligible(x, w, stride, groups):
     # weight-gradient kernels ran at a few TF/s on the fs-vid2vid hyper layers (4.5 ms per call,
     # profiles/recipe_fsvid2vid512_kernels_mi355x.txt), far below a 4x-padded MFMA tile
     cin = w.shape[2]
-    return x.shape[2] * x.shape[3] >= 256 and \
+    # (small maps go to MIOpen's grouped convolution eagerly, never inside a graph: its backward
+    # solvers accumulate with atomics into buffers the capture does not re-zero)
+    return (x.shape[2] * x.shape[3] >= 256 or _capturing()) and \
         x.numel() // x.shape[0] * _round_up(cin, 64) // max(cin, 1) * 2 < (1 << 30)
 
 

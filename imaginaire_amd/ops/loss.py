@@ -36,10 +36,19 @@ class _MultiL1(torch.autograd.Function):
         return tuple(out)
 
 
-def _native_ok(a, b):
-    return a.is_cuda and _ext.use_native(a) and a.dtype in (torch.bfloat16, torch.float32) and \
-        a.dtype == b.dtype and a.shape == b.shape and a.stride() == b.stride() and \
-        _ext.is_dense(a) and not b.requires_grad
+def _native_target(a, b):
+    """``b`` (detached) in ``a``'s dtype and memory layout for the k13 kernel, or None when the
+    pair stays on the PyTorch path. The targets of the feature-matching loss come from the real
+    branch of a discriminator that still tracks grad, and may differ in layout or dtype from the
+    fake features: re-laying them out is one pass, the fp32 ``l1_loss`` fallback was three
+    (fp32 copies of both operands + the difference; 1.4 GB per vid2vid recipe iteration)."""
+    if not (a.is_cuda and _ext.use_native(a) and a.dtype in (torch.bfloat16, torch.float32) and
+            a.shape == b.shape and _ext.is_dense(a) and b.is_cuda):
+        return None
+    b = b.detach()
+    if b.dtype == a.dtype and b.stride() == a.stride():
+        return b
+    return torch.empty_like(a).copy_(b)  # empty_like keeps a's (dense) strides
 
 
 def weighted_l1(as_, bs, weights):
@@ -47,12 +56,13 @@ def weighted_l1(as_, bs, weights):
     constants, like the detached targets of both callers)."""
     as_, bs, weights = list(as_), list(bs), [float(w) for w in weights]
     total = None
-    native = [i for i in range(len(as_)) if _native_ok(as_[i], bs[i])]
+    tg = [_native_target(a, b) for a, b in zip(as_, bs)]
+    native = [i for i in range(len(as_)) if tg[i] is not None]
     for s in range(0, len(native), _MAX_PAIRS):
         idx = native[s:s + _MAX_PAIRS]
         args = []
         for i in idx:
-            args += [as_[i], bs[i].detach()]
+            args += [as_[i], tg[i]]
         v = _MultiL1.apply([weights[i] for i in idx], *args)
         total = v if total is None else total + v
     for i in sorted(set(range(len(as_))) - set(native)):

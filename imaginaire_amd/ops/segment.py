@@ -4,10 +4,12 @@ Reference generators/pix2pixHD.py:323-349 loops in Python over instance ids and 
 with ``.nonzero()`` (a host sync per instance). Here the (batch, instance-id) pairs are hashed
 to one key per pixel and SORTED (a static-shape device sort, no host sync — so the pooling
 also runs inside a captured hipGraph, where ``torch.unique``'s data-dependent output size
-cannot). In sorted order every segment is a contiguous run: its sum is the difference of an
-fp64 running sum (cumsum) at the run's two ends and its count the run length, found with a
-cummax / reversed cummax of the run boundaries. The averaging operator is symmetric, so the
-backward is the same segment mean of the incoming gradient (an autograd Function: no
+cannot). In sorted order every segment is a contiguous run, located per position by two binary
+searches of its own key (``searchsorted`` left / right). Its sum is the difference of an fp64
+running sum at the run's two ends — ONE flat 1-D cumsum over the channel-major [C, n] copy
+(the device-wide scan; a cumsum along dim 0 of [n, C] ran as a near-serial outer-dim scan,
+~150 ms at 1 M pixels) — and its count the run length. The averaging operator is symmetric, so
+the backward is the same segment mean of the incoming gradient (an autograd Function: no
 ``index_add_`` scatter in either direction). No atomics anywhere: the earlier ``index_add_``
 into a per-segment table serialised on the few large instances (~20 ms per pix2pixHD 512x1024
 iteration, profiles/recipe_pix2pixhd512x1024_kernels_mi355x.txt).
@@ -18,26 +20,21 @@ import torch
 def _runs(key):
     """Sort order of ``key`` and, per sorted position, the first / last sorted position of its
     run of equal keys."""
-    n = key.numel()
     sk, perm = torch.sort(key)
-    pos = torch.arange(n, device=key.device)
-    first = torch.ones(n, dtype=torch.bool, device=key.device)
-    first[1:] = sk[1:] != sk[:-1]
-    last = torch.ones(n, dtype=torch.bool, device=key.device)
-    last[:-1] = first[1:]
-    zero = torch.zeros_like(pos)
-    s = torch.cummax(torch.where(first, pos, zero), 0)[0]
-    e = (n - 1) - torch.cummax(torch.where(last, n - 1 - pos, zero).flip(0), 0)[0].flip(0)
+    s = torch.searchsorted(sk, sk)
+    e = torch.searchsorted(sk, sk, right=True) - 1
     return perm, s, e
 
 
 def _segment_mean(x, perm, s, e):
     """x [n, c] (pixel order) -> per-pixel mean over its run (same layout, fp32)."""
-    c = x.shape[1]
-    cs = torch.cumsum(x.index_select(0, perm).double(), 0)
-    cs = torch.cat([cs.new_zeros((1, c)), cs], 0)        # cs[i] = sum of the first i sorted rows
-    seg = cs.index_select(0, e + 1) - cs.index_select(0, s)
-    means = (seg / (e - s + 1).unsqueeze(1).double()).to(torch.float32)
+    n, c = x.shape
+    xs = x.index_select(0, perm).double().t().contiguous()          # [c, n], sorted order
+    cs = torch.cumsum(xs.reshape(-1), 0)
+    cs = torch.cat([cs.new_zeros(1), cs])                # cs[j] = sum of the first j flat items
+    off = (torch.arange(c, device=x.device) * n).unsqueeze(1)      # channel row offsets
+    seg = cs[off + (e + 1).unsqueeze(0)] - cs[off + s.unsqueeze(0)]
+    means = (seg / (e - s + 1).unsqueeze(0).double()).to(torch.float32).t()
     out = torch.empty_like(means)
     out[perm] = means                                     # back to pixel order (a permutation)
     return out

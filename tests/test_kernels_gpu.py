@@ -269,6 +269,53 @@ def test_batched_spectral_norm_matches_torch(training):
         assert torch.allclose(b, br, atol=1e-5, rtol=1e-4), n
 
 
+def test_batched_spectral_norm_recalled_submodule_matches_torch():
+    """A sub-module called twice per network forward (MUNIT / UNIT re-encoding): its second
+    call runs ONE batched iteration for its SN layers (sub-module group hook), which must equal
+    torch's per-call power iteration — outputs, u / v buffers after two forwards, and grads."""
+    from torch import nn
+    from imaginaire_amd.layers import spectral_norm as snm
+    torch.manual_seed(7)
+
+    class Net(nn.Module):
+        def __init__(self, sn):
+            super().__init__()
+            self.enc = nn.Sequential(sn(nn.Conv2d(4, 16, 3, padding=1)), nn.ReLU(),
+                                     sn(nn.Conv2d(16, 4, 3, padding=1)))
+            self.head = sn(nn.Conv2d(4, 8, 1))
+
+        def forward(self, x):
+            return self.head(self.enc(self.enc(x)))  # enc called twice
+
+    ref = Net(torch.nn.utils.spectral_norm).cuda()
+    net = Net(snm.spectral_norm).cuda()
+    net.load_state_dict(ref.state_dict())
+    assert snm.install_batched_spectral_norm(net) == 3
+    assert any(isinstance(h, snm._SNGroup) and h.sub for h in net.enc._forward_pre_hooks.values())
+    calls = []
+    orig = snm._TorchSN.compute_weight
+    def counted(self, *a, **k):
+        if isinstance(self, snm.SpectralNorm):  # ours only (ref runs torch's class)
+            calls.append(1)
+        return orig(self, *a, **k)
+    snm._TorchSN.compute_weight = counted
+    try:
+        for _ in range(2):
+            x = torch.randn(2, 4, 8, 8, device='cuda')
+            y_ref, y = ref(x), net(x)
+            assert torch.allclose(y, y_ref, atol=1e-4, rtol=1e-4), (y - y_ref).abs().max()
+    finally:
+        snm._TorchSN.compute_weight = orig
+    assert not calls, 'a re-called layer fell back to its per-layer power iteration'
+    g = torch.randn_like(y)
+    y_ref.backward(g)
+    y.backward(g)
+    for (n, p), (_, pr) in zip(net.named_parameters(), ref.named_parameters()):
+        assert torch.allclose(p.grad, pr.grad, atol=1e-4, rtol=1e-3), n
+    for (n, b), (_, br) in zip(net.named_buffers(), ref.named_buffers()):
+        assert torch.allclose(b, br, atol=1e-5, rtol=1e-4), n
+
+
 @pytest.mark.gpu
 def test_batched_spectral_norm_large_layers():
     """Vectorised k5b / k5d paths on layers with several row splits and column tiles, aligned
