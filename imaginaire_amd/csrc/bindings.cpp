@@ -99,8 +99,9 @@ std::vector<at::Tensor> resample2d_backward(const at::Tensor& in1, const at::Ten
 // conv_mfma.hip (k10)
 at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                        int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
-                       double slope, int64_t nb);
-at::Tensor conv2d_dgrad_mfma(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int64_t pw);
+                       double slope, int64_t nb, int64_t ncv);
+at::Tensor conv2d_dgrad_mfma(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int64_t pw,
+                             int64_t ncv);
 at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t KH, int64_t KW,
                              int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh,
                              int64_t dw, int64_t out_cout, int64_t out_cin, bool out_bf16,
@@ -163,10 +164,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "all-gather into a flat rank-major tensor on the current stream, capturable");
   m.def("conv2d_mfma", &iamd::conv2d_mfma, "MFMA implicit-GEMM NHWC conv + bias + act (k10)",
         py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("sh"), py::arg("sw"), py::arg("ph"),
-        py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("slope"), py::arg("nb") = 1);
+        py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("slope"), py::arg("nb") = 1,
+        py::arg("ncv") = -1);
   m.def("conv2d_dgrad_mfma", &iamd::conv2d_dgrad_mfma,
         "stride-1 conv data gradient from the forward weight (k10 v4 transposed-weight path)",
-        py::arg("dy"), py::arg("w"), py::arg("ph"), py::arg("pw"));
+        py::arg("dy"), py::arg("w"), py::arg("ph"), py::arg("pw"), py::arg("ncv") = -1);
   m.def("conv2d_wgrad_mfma", &iamd::conv2d_wgrad_mfma, "MFMA conv weight gradient (k11)",
         py::arg("dy"), py::arg("x"), py::arg("KH"), py::arg("KW"), py::arg("sh"), py::arg("sw"),
         py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("out_cout") = -1,

@@ -67,6 +67,9 @@ struct ConvArgs {
   // blockIdx.z: operand / output / bias strides in elements between samples (v1 kernel only)
   int64_t xbs, wbs, ybs;
   int bbs, nz;
+  // channels stored per output pixel = row stride of y (<= Cout, a multiple of 8): the padded
+  // output channels of a Cout % 64 != 0 conv are never written, so no crop copy follows
+  int ldy;
 };
 
 // destination pixel (row of the NHWC output) of GEMM row m
@@ -286,9 +289,9 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_fwd_mfma(ConvA
   for (int p = 0; p < BM / kRowsPerPass; ++p) {
     const int rl = p * kRowsPerPass + rr;
     const int m = m0 + rl;
-    if (m < a.M) {
+    if (m < a.M && n0 + ch * 8 < a.ldy) {
       const uint4 v = *reinterpret_cast<const uint4*>(E + rl * kEpiStride + ch * 16);
-      *reinterpret_cast<uint4*>(yz + out_row(a, m) * a.Cout + n0 + ch * 8) = v;
+      *reinterpret_cast<uint4*>(yz + out_row(a, m) * a.ldy + n0 + ch * 8) = v;
     }
   }
 #endif  // __HIP_DEVICE_COMPILE__
@@ -482,9 +485,9 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v2(ConvArgs a) {
   for (int p = 0; p < BM / kRowsPerPass; ++p) {
     const int rl = p * kRowsPerPass + rr;
     const int m = m0 + rl;
-    if (m < a.M) {
+    if (m < a.M && n0 + ch * 8 < a.ldy) {
       const uint4 v = *reinterpret_cast<const uint4*>(E + rl * kEpiStride + ch * 16);
-      *reinterpret_cast<uint4*>(a.y + out_row(a, m) * a.Cout + n0 + ch * 8) = v;
+      *reinterpret_cast<uint4*>(a.y + out_row(a, m) * a.ldy + n0 + ch * 8) = v;
     }
   }
 #endif  // __HIP_DEVICE_COMPILE__
@@ -735,9 +738,9 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v3(ConvArgs a) {
     for (int p = 0; p < BM / 32; ++p) {
       const int rl = p * 32 + rr;
       const int m = m0 + rl;
-      if (m < a.M) {
+      if (m < a.M && n0 + half * 128 + ch * 8 < a.ldy) {
         const uint4 v = *reinterpret_cast<const uint4*>(E + rl * kEpiStride + ch * 16);
-        *reinterpret_cast<uint4*>(a.y + out_row(a, m) * a.Cout + n0 + half * 128 + ch * 8) = v;
+        *reinterpret_cast<uint4*>(a.y + out_row(a, m) * a.ldy + n0 + half * 128 + ch * 8) = v;
       }
     }
     __syncthreads();
@@ -995,9 +998,9 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v4(ConvArgs a) {
   for (int p = 0; p < BM / 32; ++p) {
     const int rl = p * 32 + rr;
     const int m = m0 + rl;
-    if (m < a.M) {
+    if (m < a.M && n0 + ch * 8 < a.ldy) {
       const uint4 v = *reinterpret_cast<const uint4*>(E + rl * kEpiStride + ch * 16);
-      *reinterpret_cast<uint4*>(a.y + out_row(a, m) * a.Cout + n0 + ch * 8) = v;
+      *reinterpret_cast<uint4*>(a.y + out_row(a, m) * a.ldy + n0 + ch * 8) = v;
     }
   }
 #endif  // __HIP_DEVICE_COMPILE__
@@ -1023,6 +1026,7 @@ conv_splitk_reduce(const float* __restrict__ part, const float* __restrict__ bia
       acc[4] += hi.x; acc[5] += hi.y; acc[6] += hi.z; acc[7] += hi.w;
     }
     const int c = (int)(e % C);
+    if (c >= map.ldy) continue;  // padded output channels are not stored
     const int zb = (int)(e / ((int64_t)map.M * C));  // sample of a batched launch
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -1030,7 +1034,7 @@ conv_splitk_reduce(const float* __restrict__ part, const float* __restrict__ bia
       acc[k] = t > 0.f ? t : t * slope;
     }
     const int64_t m = e / C - (int64_t)zb * map.M;
-    store_vec<__hip_bfloat16, 8>(y + zb * map.ybs + out_row(map, (int)m) * C + (e % C), acc);
+    store_vec<__hip_bfloat16, 8>(y + zb * map.ybs + out_row(map, (int)m) * map.ldy + c, acc);
   }
 }
 
@@ -1231,7 +1235,7 @@ void run_conv(ConvArgs& a, const at::Tensor& x) {
 // (sample-major), bias [nb * Cout]: y[b] = act(conv2d(x[b], w[b]) + bias[b]).
 at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                        int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
-                       double slope, int64_t nb) {
+                       double slope, int64_t nb, int64_t ncv) {
   IAMD_CHECK(x.is_cuda() && w.is_cuda(), "conv2d_mfma: CUDA tensors expected");
   IAMD_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16,
              "conv2d_mfma: bf16 operands expected");
@@ -1254,7 +1258,10 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
                  (int64_t)B * Ho * Wo * Cout < (1ll << 31),
              "conv2d_mfma: tensor too large for 32-bit buffer offsets");
   IAMD_CHECK(KH * KW <= 64, "conv2d_mfma: filters with more than 64 taps are not supported");
-  auto y = at::empty({B, Cout, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  if (ncv < 0) ncv = Cout;
+  IAMD_CHECK(ncv == Cout || (nb == 1 && ncv > 0 && ncv < Cout && ncv % 8 == 0),
+             "conv2d_mfma: stored channels must be Cout, or a multiple of 8 below it (nb == 1)");
+  auto y = at::empty({B, ncv, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   at::Tensor bf;
   if (bias.has_value() && bias->defined()) {
     IAMD_CHECK(bias->numel() == Cout * nb, "conv2d_mfma: bias size");
@@ -1271,6 +1278,7 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
   a.xbs = nb > 1 ? (int64_t)H * W * Cin : 0;
   a.wbs = nb > 1 ? (int64_t)Cout * KH * KW * Cin : 0;
   a.ybs = nb > 1 ? (int64_t)Ho * Wo * Cout : 0;
+  a.ldy = (int)ncv;
   a.bbs = nb > 1 ? Cout : 0;
   a.KH = KH;
   a.H = H; a.W = W; a.Cin = Cin; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
@@ -1292,7 +1300,8 @@ at::Tensor conv_weight_flip_t(const at::Tensor& w, int64_t s, int64_t qy, int64_
 // (channels-last): dx [B, Cin, H, W] = conv(dy, flip_t(w), padding (KH-1-ph, KW-1-pw)). On the v4
 // path the forward weight is read directly (tap-flipped, k-major, transposing LDS reads): no
 // flipped copy of the weight per backward; other shapes flip once and run the k10 routing.
-at::Tensor conv2d_dgrad_mfma(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int64_t pw) {
+at::Tensor conv2d_dgrad_mfma(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int64_t pw,
+                             int64_t ncv) {
   IAMD_CHECK(dy.is_cuda() && w.is_cuda() && dy.scalar_type() == at::kBFloat16 &&
                  w.scalar_type() == at::kBFloat16 && dy.dim() == 4 && w.dim() == 4,
              "conv2d_dgrad_mfma: 4-D bf16 CUDA tensors expected");
@@ -1318,9 +1327,12 @@ at::Tensor conv2d_dgrad_mfma(const at::Tensor& dy, const at::Tensor& w, int64_t 
                   std::getenv("IMAGINAIRE_AMD_DGRAD_FLIP") == nullptr;
   if (!ok) {
     const at::Tensor wt = conv_weight_flip_t(w, 1, 0, 0, 1);
-    return conv2d_mfma(dy, wt, c10::nullopt, 1, 1, tph, tpw, 1, 1, 1.0, 1);
+    return conv2d_mfma(dy, wt, c10::nullopt, 1, 1, tph, tpw, 1, 1, 1.0, 1, ncv);
   }
-  auto y = at::empty({B, N, a.Ho, a.Wo}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  if (ncv < 0) ncv = N;
+  IAMD_CHECK(ncv == N || (ncv > 0 && ncv < N && ncv % 8 == 0),
+             "conv2d_dgrad_mfma: stored channels must be Cin or a multiple of 8 below it");
+  auto y = at::empty({B, ncv, a.Ho, a.Wo}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   a.x = reinterpret_cast<const __hip_bfloat16*>(dy.data_ptr());
   a.w = reinterpret_cast<const __hip_bfloat16*>(w.data_ptr());
   a.bias = nullptr;
@@ -1329,6 +1341,7 @@ at::Tensor conv2d_dgrad_mfma(const at::Tensor& dy, const at::Tensor& w, int64_t 
   a.wbytes = (int)(w.numel() * 2);
   a.xbs = a.wbs = a.ybs = 0;
   a.bbs = 0;
+  a.ldy = (int)ncv;
   a.M = B * a.Ho * a.Wo;
   a.cpt = K / kBK;
   a.nk = KH * KW * a.cpt;

@@ -325,17 +325,19 @@ class _MfmaConv2d(torch.autograd.Function):
         xb = _pad_channels(x, cp, torch.bfloat16)
         wb = _pad_rows(_pad_channels(w, cp, torch.bfloat16), op)
         ho, wo = _out_hw(x.shape[2], x.shape[3], w.shape[2:], stride, padding, dilation)
+        # Cout % 8 == 0: k10 stores only the real output channels (no crop copy after it)
+        ncv = cout if (op != cout and cout % 8 == 0) else op
         with _Logged('fwd', 'k10', 2.0 * x.shape[0] * ho * wo * op * cp * w.shape[2] * w.shape[3],
                      _gemm_desc(xb, wb, stride, padding)):
             y = _ext.ext().conv2d_mfma(xb, wb, _pad_rows(bias, op), stride[0], stride[1],
                                        padding[0], padding[1], dilation[0], dilation[1],
-                                       float(slope))
+                                       float(slope), 1, ncv)
         ctx.conf = (stride, padding, dilation, float(slope), cin, cout, x.dtype, w.dtype,
                     None if bias is None else bias.dtype, x.shape[1])
         # the output is needed only for a fused activation's mask: with slope 1 it is not
         # saved, so in-place ops on the conv output stay legal (as after a plain F.conv2d)
         ctx.save_for_backward(xb, wb, y if slope != 1.0 else None)
-        if op == cout:
+        if y.shape[1] == cout:
             return y
         # a fresh tensor, not a view of y: callers apply in-place activations (nn.ReLU(
         # inplace=True)) to conv outputs, which autograd forbids on a custom Function's view
@@ -346,11 +348,14 @@ class _MfmaConv2d(torch.autograd.Function):
         xb, wb, y = ctx.saved_tensors
         stride, padding, dilation, slope, cin, cout, xdt, wdt, bdt, xc = ctx.conf
         need_x, need_w, need_b = ctx.needs_input_grad[:3]
-        dy = _pad_channels(dy, wb.shape[0], torch.bfloat16)
+        # the activation backward runs at the saved output's channel count (the real Cout when
+        # k10 stored only those, else the padded one), then dy is padded for the GEMMs
+        dy = _pad_channels(dy, y.shape[1] if y is not None else dy.shape[1], torch.bfloat16)
         db = None
         if slope != 1.0 or need_b:
             # identity activation: the k2 kernel reads only dy (y stands in for the layout)
             dy, db = _ext.ext().bias_act_bwd(y if y is not None else dy, dy, slope)
+        dy = _pad_channels(dy, wb.shape[0], torch.bfloat16)
         dx = dw = None
         cap = _capturing()
         if need_x:
@@ -363,16 +368,18 @@ class _MfmaConv2d(torch.autograd.Function):
             # k10 splits K over the grid's y dimension for those
             fl = 2.0 * dy.shape[0] * dy.shape[2] * dy.shape[3] * wb.numel()
             big = dblocks >= _MFMA_MIN_DGRAD_BLOCKS or cap
+            # dx keeps only the input's real channels when they are a multiple of 8
+            ncv = xc if (cp != xc and xc % 8 == 0) else cp
             if stride == (1, 1) and dilation == (1, 1) and pt[0] >= 0 and pt[1] >= 0 and big:
                 # k10 v4 reads the forward weight tap-flipped and transposed in-kernel (no
                 # flipped weight copy); other shapes flip once inside and run the k10 routing
                 with _Logged('dgrad', 'k10', fl, _gemm_desc(dy, wb.transpose(0, 1), (1, 1), pt)):
-                    dx = _ext.ext().conv2d_dgrad_mfma(dy, wb, padding[0], padding[1])
+                    dx = _ext.ext().conv2d_dgrad_mfma(dy, wb, padding[0], padding[1], ncv)
             elif stride == (1, 1) and pt[0] >= 0 and pt[1] >= 0 and big:
                 wt = _flip_t(wb)
                 with _Logged('dgrad', 'k10', fl, _gemm_desc(dy, wt, (1, 1), pt)):
                     dx = _ext.ext().conv2d_mfma(dy, wt, None, 1, 1, pt[0], pt[1],
-                                                dilation[0], dilation[1], 1.0)
+                                                dilation[0], dilation[1], 1.0, 1, ncv)
             elif _STRIDED_DGRAD and stride[0] == stride[1] and 2 <= stride[0] <= 4 and \
                     dilation == (1, 1) and (cap or (
                         dblocks >= _MFMA_MIN_DGRAD_BLOCKS * stride[0] ** 2 and

@@ -407,6 +407,11 @@ _CONV_CASES = [
     (2, 1026, 2, 4, 8, 3, 1, 1, 1),         # predict_flow on a 1/64 map: tiny grid, split K
     (1, 32, 128, 16, 24, 1, 1, 0, 1),       # 32-channel 1x1: Cin padded 32 -> 64 (2x waste)
     (1, 32, 64, 16, 24, 3, 2, 1, 1),        # 32-channel 3x3 s2
+    # Cout / Cin multiples of 8 below the 64 padding: k10 stores only the real channels (ldy)
+    (2, 64, 32, 16, 24, 3, 1, 1, 1),        # Cout 32 (of 64), v1 epilogue
+    (1, 48, 96, 12, 20, 3, 1, 1, 1),        # Cout 96 (of 128), dx 48 (of 64) via flip + k10
+    (1, 96, 128, 16, 64, 3, 1, 1, 1),       # dx 96 (of 128) on the v4 dgrad epilogue
+    (1, 128, 96, 16, 256, 5, 1, 2, 1),      # Cout 96 of 128: v4 forward with split-K reduce
 ]
 
 
