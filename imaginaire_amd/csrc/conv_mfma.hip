@@ -770,7 +770,12 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v3(ConvArgs a) {
 // (KH-1-ky, KW-1-kx). Its weight tile is staged k-major (64 rows of 128 n-channels, 256 B,
 // 16-byte chunks swizzled per row) and the B fragments are read with the transposing
 // ds_read_b64_tr_b16 (two 4-row reads per 8-deep fragment, as the k11 weight gradient does).
-template <int KW, bool HAS_BIAS, bool BT>
+// PF (fragment prefetch across the tap barrier): a tap step's second k-half fragments (kk = 1)
+// are read during the step and consumed by the NEXT step's first MFMAs, which issue right after
+// its barrier while that step's kk = 0 fragments are still in flight — without it every tap
+// step began with all 8 waves waiting on LDS reads (MFMA pipe busy 54-63%,
+// profiles/pmc_conv_v4_r3_mi355x.txt).
+template <int KW, bool HAS_BIAS, bool BT, bool PF>
 __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v4(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   constexpr int BM = 256, BN = 128;
@@ -886,62 +891,123 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v4(ConvArgs a) {
     const int s = p / SW;
     wrow[i] = s * L + (p - s * SW);
   }
-  auto tapstep = [&](int abuf, int kx) {
+  // fragments of k-half kk of tap kx (window buffer abuf)
+  auto load_frags = [&](int abuf, int kx, int kk, bf16x8 (&af)[4], bf16x8 (&bf)[4]) {
     const char* As = smem + abuf * kAbytes;
     const char* Bs = smem + kBoff + kx * kBbytes;
-    bf16x8 af[2][4], bfr[2][4];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = wrow[i] + kx;
-        af[kk][i] = *reinterpret_cast<const bf16x8*>(
-            As + row * kRowBytes + (((kk * 4 + fk) ^ (row & 7)) << 4));
-      }
-      if constexpr (BT) {
-        // lane (g, q, p): rows kk*32 + 8g + q (+4), 8-byte quarter p of a 16-column block
-        const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-        const int r0 = kk * 32 + g * 8 + q;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int cb = (wn * 64 + j * 16) >> 3;
-          auto baddr = [&](int row) {
-            return row * 256 + (((cb + (p >> 1)) ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4) +
-                   ((p & 1) << 3);
-          };
-          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t)(Bs + baddr(r0)));
-          const bf16x4 hi =
-              __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t)(Bs + baddr(r0 + 4)));
-          bfr[kk][j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-        }
-      } else {
-        const int coff = ((kk * 4 + fk) ^ fsw) << 4;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          bfr[kk][j] = *reinterpret_cast<const bf16x8*>(
-              Bs + (wn * 64 + j * 16 + frow) * kRowBytes + coff);
-      }
+    for (int i = 0; i < 4; ++i) {
+      const int row = wrow[i] + kx;
+      af[i] = *reinterpret_cast<const bf16x8*>(
+          As + row * kRowBytes + (((kk * 4 + fk) ^ (row & 7)) << 4));
     }
+    if constexpr (BT) {
+      // lane (g, q, p): rows kk*32 + 8g + q (+4), 8-byte quarter p of a 16-column block
+      const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+      const int r0 = kk * 32 + g * 8 + q;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int cb = (wn * 64 + j * 16) >> 3;
+        auto baddr = [&](int row) {
+          return row * 256 + (((cb + (p >> 1)) ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4) +
+                 ((p & 1) << 3);
+        };
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t)(Bs + baddr(r0)));
+        const bf16x4 hi =
+            __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t)(Bs + baddr(r0 + 4)));
+        bf[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+    } else {
+      const int coff = ((kk * 4 + fk) ^ fsw) << 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bf[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * 64 + j * 16 + frow) * kRowBytes +
+                                                 coff);
+    }
+  };
+  auto mma = [&](const bf16x8 (&af)[4], const bf16x8 (&bf)[4]) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0,
-                                                              0, 0);
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
+  };
+  // PF: the previous tap step's kk = 1 fragments (zero before the first step: +0 MFMAs)
+  bf16x8 pa[4], pb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    pa[i] = bf16x8{};
+    pb[i] = bf16x8{};
+  }
+  auto tapstep = [&](int abuf, int kx) {
+    if constexpr (PF) {
+      bf16x8 a0[4], b0[4];
+      load_frags(abuf, kx, 0, a0, b0);
+      mma(pa, pb);                      // previous step, kk = 1: no LDS wait after the barrier
+      load_frags(abuf, kx, 1, pa, pb);  // this step's kk = 1, consumed by the next step
+      mma(a0, b0);
+    } else {
+      const char* As = smem + abuf * kAbytes;
+      const char* Bs = smem + kBoff + kx * kBbytes;
+      bf16x8 af[2][4], bfr[2][4];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = wrow[i] + kx;
+          af[kk][i] = *reinterpret_cast<const bf16x8*>(
+              As + row * kRowBytes + (((kk * 4 + fk) ^ (row & 7)) << 4));
+        }
+        if constexpr (BT) {
+          // lane (g, q, p): rows kk*32 + 8g + q (+4), 8-byte quarter p of a 16-column block
+          const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+          const int r0 = kk * 32 + g * 8 + q;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int cb = (wn * 64 + j * 16) >> 3;
+            auto baddr = [&](int row) {
+              return row * 256 + (((cb + (p >> 1)) ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4) +
+                     ((p & 1) << 3);
+            };
+            const bf16x4 lo =
+                __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t)(Bs + baddr(r0)));
+            const bf16x4 hi =
+                __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t)(Bs + baddr(r0 + 4)));
+            bfr[kk][j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          }
+        } else {
+          const int coff = ((kk * 4 + fk) ^ fsw) << 4;
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            bfr[kk][j] = *reinterpret_cast<const bf16x8*>(
+                Bs + (wn * 64 + j * 16 + frow) * kRowBytes + coff);
+        }
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j],
+                                                                0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
   };
   // one outer step (window buffer abuf static): KW tap steps; tap step q stages the weights of
   // tap step q + 2 into its ring slot and, at kx == 0, the next outer step's window
   auto outer = [&](int o, int abuf) {
 #pragma unroll
     for (int kx = 0; kx < KW; ++kx) {
+      // (lgkmcnt(0): this wave's fragment reads of the previous step are in registers before
+      // any wave's DMA may overwrite their LDS slot / window)
       if (kx == 1)
-        asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // younger: window(o+1) 5 + weights 2
+        asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)" ::: "memory");  // younger: window 5 + weights 2
       else
-        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // younger: the next weights 2
+        asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");  // younger: the next weights 2
       __builtin_amdgcn_s_barrier();
       if (kx == 0) issueA(o + 1, nky, ncc, abuf ^ 1);
       if (kx + 2 < KW) issueB(o, cky, ccc, kx + 2, kx + 2);
@@ -961,6 +1027,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v4(ConvArgs a) {
     outer(o, 0);
     if (o + 1 < o1) outer(o + 1, 1);
   }
+  if constexpr (PF) mma(pa, pb);  // the last tap step's kk = 1
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();  // trailing (zero) prefetches landed and every wave is done reading
 
@@ -1073,10 +1140,16 @@ void run_v4(ConvArgs& a, const at::Tensor& x, bool bt) {
     a.part = part4.data_ptr<float>();
   }
   const dim3 grid4((unsigned)tiles4, (unsigned)S4, 1);
+  // IMAGINAIRE_AMD_V4_PF = 0: A/B switch back to the un-prefetched tap step
+  const char* pfe = std::getenv("IMAGINAIRE_AMD_V4_PF");
+  const bool pf = !(pfe != nullptr && pfe[0] == '0');
   auto launch = [&](auto kv, auto hbv, auto btv) {
     constexpr int K = decltype(kv)::value;
     constexpr bool HB = decltype(hbv)::value, BTV = decltype(btv)::value;
-    hipLaunchKernelGGL((conv_fwd_mfma_v4<K, HB, BTV>), grid4, dim3(512), 0, stream(), a);
+    if (pf && !BTV)  // (the BT kernels have no registers left for a second fragment set)
+      hipLaunchKernelGGL((conv_fwd_mfma_v4<K, HB, BTV, !BTV>), grid4, dim3(512), 0, stream(), a);
+    else
+      hipLaunchKernelGGL((conv_fwd_mfma_v4<K, HB, BTV, false>), grid4, dim3(512), 0, stream(), a);
   };
   auto by_bt = [&](auto kv, auto hbv) {
     if (bt) launch(kv, hbv, std::true_type());
