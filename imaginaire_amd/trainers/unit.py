@@ -3,6 +3,7 @@ recon + perceptual."""
 import torch
 from torch import nn
 
+from imaginaire_amd.losses.l1 import L1Loss
 from imaginaire_amd.losses import GANLoss, PerceptualLoss
 from imaginaire_amd.trainers.munit import Trainer as MUNITTrainer, _weights_from
 
@@ -10,8 +11,8 @@ from imaginaire_amd.trainers.munit import Trainer as MUNITTrainer, _weights_from
 class Trainer(MUNITTrainer):
     def _init_loss(self, cfg):
         self.criteria['gan'] = GANLoss(cfg.trainer.gan_mode)
-        self.criteria['image_recon'] = nn.L1Loss()
-        self.criteria['cycle_recon'] = nn.L1Loss()
+        self.criteria['image_recon'] = L1Loss()
+        self.criteria['cycle_recon'] = L1Loss()
         if getattr(cfg.trainer.loss_weight, 'perceptual', 0) > 0:
             self.criteria['perceptual'] = PerceptualLoss(
                 cfg=cfg, network=cfg.trainer.perceptual_mode,

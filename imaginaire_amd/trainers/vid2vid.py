@@ -22,6 +22,7 @@ import os
 import numpy as np
 import torch
 
+from imaginaire_amd.losses.l1 import L1Loss
 from imaginaire_amd.evaluation.fid import compute_fid
 from imaginaire_amd.losses import FeatureMatchingLoss, GANLoss, MaskedL1Loss, PerceptualLoss
 from imaginaire_amd.model_utils.fs_vid2vid import (concat_frames, detach, get_fg_mask,
@@ -86,7 +87,7 @@ class Trainer(BaseTrainer):
             cfg=cfg, network=pl.mode, layers=pl.layers, weights=pl.weights,
             num_scales=getattr(pl, 'num_scales', 1)), lw.perceptual)
         if getattr(lw, 'L1', 0) > 0:
-            self._assign_criteria('L1', torch.nn.L1Loss(), lw.L1)
+            self._assign_criteria('L1', L1Loss(), lw.L1)
         self.add_dis_cfg = getattr(cfg.dis, 'additional_discriminators', None)
         if self.add_dis_cfg is not None:
             for name in self.add_dis_cfg:

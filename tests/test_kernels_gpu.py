@@ -1275,3 +1275,23 @@ def test_batchnorm_running_stats_match_torch(affine, dtype):
     ref.eval()
     x = torch.randn(2, C, 6, 6, device='cuda').contiguous(memory_format=torch.channels_last)
     assert torch.allclose(ours.fused(x).float(), ref(x), atol=1e-4, rtol=1e-4)
+
+
+def test_l1loss_module_native_matches_torch():
+    """losses.L1Loss (k13 multi-tensor L1, bf16 read in place) == torch.nn.L1Loss in fp32, value
+    and input gradient; a target that needs a gradient keeps the PyTorch path (and gets one)."""
+    from imaginaire_amd.losses import L1Loss
+    torch.manual_seed(3)
+    a = torch.randn(4, 64, 9, 13, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last).requires_grad_(True)
+    b = torch.randn(4, 64, 9, 13, device='cuda').to(torch.bfloat16)  # other layout
+    v = L1Loss()(a, b)
+    ar = a.detach().float().requires_grad_(True)
+    vr = torch.nn.functional.l1_loss(ar, b.float())
+    assert abs(float(v) - float(vr)) <= 1e-4 * max(1.0, abs(float(vr)))
+    v.backward()
+    vr.backward()
+    assert torch.allclose(a.grad.float(), ar.grad, atol=1e-6, rtol=1e-2)
+    t = b.float().requires_grad_(True)
+    L1Loss()(a.detach().float(), t).backward()
+    assert t.grad is not None
