@@ -146,31 +146,59 @@ def _pad_channels(t, c, dtype=None):
     return out
 
 
+class _StackNHWC(torch.autograd.Function):
+    """Forward of :func:`stack_nhwc`; the backward hands every input the matching slice of the
+    padded gradient (a view: no clone of the whole padded gradient and no per-slice copies,
+    which autograd's CopySlices made — 2.2 GB per vid2vid recipe iteration for the 64-channel
+    discriminator inputs)."""
+
+    @staticmethod
+    def forward(ctx, dtype, align, widths, n, *ts):
+        first = ts[0]
+        c = sum(widths)
+        cp = _round_up(c, align)
+        out = torch.empty((sum(n), cp) + tuple(first.shape[2:]), dtype=dtype,
+                          device=first.device, memory_format=_CL)
+        i = o = 0
+        ctx.slices = []
+        for k in n:
+            ch = 0
+            for wd in widths:
+                out[o:o + k, ch:ch + wd] = ts[i]
+                ctx.slices.append((o, k, ch, wd, ts[i].dtype))
+                ch += wd
+                i += 1
+            o += k
+        if cp > c:
+            out[:, c:].zero_()
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        grads = []
+        for (o, k, ch, wd, dt), need in zip(ctx.slices, ctx.needs_input_grad[4:]):
+            grads.append(g[o:o + k, ch:ch + wd].to(dt) if need else None)
+        return (None, None, None, None) + tuple(grads)
+
+
 def stack_nhwc(rows, dtype=None, align=64):
     """``cat([cat(row, 1) for row in rows], 0)`` written ONCE into a channel-padded NHWC
     buffer (channels rounded up to ``align``, zero tail marked for the convs): the
     discriminator inputs label|image for real and fake, without the two channel concats, the
     batch concat, the fp32 -> bf16 cast and the conv's own zero-padding copy. ``dtype``
-    defaults to the autocast dtype (or the first tensor's)."""
+    defaults to the autocast dtype (or the first tensor's). Every row holds tensors of the
+    same channel widths."""
     first = rows[0][0]
     if dtype is None:
         dtype = torch.get_autocast_dtype('cuda') if (first.is_cuda and
                                                      torch.is_autocast_enabled('cuda')) \
             else first.dtype
-    c = sum(t.shape[1] for t in rows[0])
-    cp = _round_up(c, align)
+    widths = [t.shape[1] for t in rows[0]]
+    assert all([t.shape[1] for t in row] == widths for row in rows), 'stack_nhwc: row widths'
     n = [row[0].shape[0] for row in rows]
-    out = torch.empty((sum(n), cp) + tuple(first.shape[2:]), dtype=dtype, device=first.device,
-                      memory_format=_CL)
-    o = 0
-    for row, k in zip(rows, n):
-        ch = 0
-        for t in row:
-            out[o:o + k, ch:ch + t.shape[1]] = t
-            ch += t.shape[1]
-        o += k
-    if cp > c:
-        out[:, c:].zero_()
+    out = _StackNHWC.apply(dtype, align, widths, n, *[t for row in rows for t in row])
+    c = sum(widths)
+    if _round_up(c, align) > c:
         mark_zero_tail(out, c)
     return out
 
@@ -523,7 +551,8 @@ class _TapSplitConv2d(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             wzt = wz.view(cz, cp).t().contiguous().view(cp, cz, 1, 1)
-            dx = _ext.ext().conv2d_mfma(dz, wzt, None, 1, 1, 0, 0, 1, 1, 1.0, 1)
+            ncv = xc if (cp != xc and xc % 8 == 0) else cp  # only the real input channels
+            dx = _ext.ext().conv2d_mfma(dz, wzt, None, 1, 1, 0, 0, 1, 1, 1.0, 1, ncv)
             dx = (dx[:, :xc] if dx.shape[1] != xc else dx).to(xdt)
         if ctx.needs_input_grad[1]:
             g = _ext.ext().conv2d_wgrad_mfma(dz, xb, 1, 1, 1, 1, 0, 0, 1, 1, cout * kh * kw, cin,
