@@ -377,10 +377,11 @@ class _MfmaConv2d(torch.autograd.Function):
         stride, padding, dilation, slope, cin, cout, xdt, wdt, bdt, xc = ctx.conf
         need_x, need_w, need_b = ctx.needs_input_grad[:3]
         # the activation backward runs at the saved output's channel count (the real Cout when
-        # k10 stored only those, else the padded one), then dy is padded for the GEMMs
-        dy = _pad_channels(dy, y.shape[1] if y is not None else dy.shape[1], torch.bfloat16)
+        # k10 stored only those, else the padded one), then dy is padded for the GEMMs; without
+        # an activation / bias gradient that is ONE pad-cast pass from any dy layout
         db = None
         if slope != 1.0 or need_b:
+            dy = _pad_channels(dy, y.shape[1] if y is not None else dy.shape[1], torch.bfloat16)
             # identity activation: the k2 kernel reads only dy (y stands in for the layout)
             dy, db = _ext.ext().bias_act_bwd(y if y is not None else dy, dy, slope)
         dy = _pad_channels(dy, wb.shape[0], torch.bfloat16)
