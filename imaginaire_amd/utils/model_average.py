@@ -40,11 +40,13 @@ def _drop_sn_load_hooks(m):
 
 def _drop_sn_group_hooks(net):
     """The deep-copied EMA network has no SN layers left: drop the batched-SN
-    pre-hook it inherited from the source network."""
+    pre-hooks it inherited from the source network (the network-level one and the
+    re-call hooks of its sub-modules)."""
     from imaginaire_amd.layers.spectral_norm import _SNGroup
-    for k, h in list(net._forward_pre_hooks.items()):
-        if isinstance(h, _SNGroup):
-            del net._forward_pre_hooks[k]
+    for m in net.modules():
+        for k, h in list(m._forward_pre_hooks.items()):
+            if isinstance(h, _SNGroup):
+                del m._forward_pre_hooks[k]
 
 
 class ModelAverage(nn.Module):
