@@ -1369,6 +1369,16 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
 
 at::Tensor conv_weight_flip_t(const at::Tensor& w, int64_t s, int64_t qy, int64_t qx, int64_t nb);
 
+// The transposed-weight (BT) v4 data gradient saves the flipped weight copy (one small
+// flip_t pass per backward) but runs 10-35% slower than v4 on the flipped copy: its
+// k-major B tile is read with two ds_read_b64_tr_b16 per fragment and the KW = 5 build
+// spills (profiles/spade_step_conv_log_mi355x.txt vs the flipped route). Off by default;
+// IMAGINAIRE_AMD_DGRAD_BT=1 turns it on.
+static bool dgrad_bt_enabled() {
+  const char* e = std::getenv("IMAGINAIRE_AMD_DGRAD_BT");
+  return e != nullptr && e[0] == '1';
+}
+
 // Data gradient of a stride-1, undilated conv with forward weight w [Cout, Cin, KH, KW]
 // (channels-last): dx [B, Cin, H, W] = conv(dy, flip_t(w), padding (KH-1-ph, KW-1-pw)). On the v4
 // path the forward weight is read directly (tap-flipped, k-major, transposing LDS reads): no
@@ -1396,8 +1406,7 @@ at::Tensor conv2d_dgrad_mfma(const at::Tensor& dy, const at::Tensor& w, int64_t 
   a.nz = 1; a.omode = 0;
   const bool ok = K % kBK == 0 && a.Ho > 0 && a.Wo > 0 && v4_eligible(a) &&
                   (int64_t)B * H * W * K * 2 < kOobOffset && w.numel() * 2 < kOobOffset &&
-                  (int64_t)B * a.Ho * a.Wo * N < (1ll << 31) &&
-                  std::getenv("IMAGINAIRE_AMD_DGRAD_FLIP") == nullptr;
+                  (int64_t)B * a.Ho * a.Wo * N < (1ll << 31) && dgrad_bt_enabled();
   if (!ok) {
     const at::Tensor wt = conv_weight_flip_t(w, 1, 0, 0, 1);
     return conv2d_mfma(dy, wt, c10::nullopt, 1, 1, tph, tpw, 1, 1, 1.0, 1, ncv);

@@ -400,8 +400,9 @@ class _MfmaConv2d(torch.autograd.Function):
             # dx keeps only the input's real channels when they are a multiple of 8
             ncv = xc if (cp != xc and xc % 8 == 0) else cp
             if stride == (1, 1) and dilation == (1, 1) and pt[0] >= 0 and pt[1] >= 0 and big:
-                # k10 v4 reads the forward weight tap-flipped and transposed in-kernel (no
-                # flipped weight copy); other shapes flip once inside and run the k10 routing
+                # one flip_t pass of the weight, then the k10 routing (v4 for stride-1 3x3-5x5
+                # rows); IMAGINAIRE_AMD_DGRAD_BT=1 reads the forward weight transposed in-kernel
+                # instead (no copy, but a slower tile: csrc/conv_mfma.hip dgrad_bt_enabled)
                 with _Logged('dgrad', 'k10', fl, _gemm_desc(dy, wb.transpose(0, 1), (1, 1), pt)):
                     dx = _ext.ext().conv2d_dgrad_mfma(dy, wb, padding[0], padding[1], ncv)
             elif stride == (1, 1) and pt[0] >= 0 and pt[1] >= 0 and big:
