@@ -52,6 +52,10 @@ for net in (tr.net_G, tr.net_D):
             hooks.append(m.register_forward_hook(fwd_hook))
             hooks.append(m.register_full_backward_hook(bwd_hook))
 
+import contextlib  # noqa: E402
+from imaginaire_amd.utils.cuda_graph import graph_routing  # noqa: E402
+# IAMD_PROBE_ROUTING=1: the kernel routing of a graphed step (every conv on k10 / k11)
+routing = graph_routing if os.environ.get('IAMD_PROBE_ROUTING') == '1' else contextlib.nullcontext
 for trial in range(3):
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -60,7 +64,8 @@ for trial in range(3):
         junk.append(torch.full((sz // 4,), float('nan'), device='cuda'))
     del junk
     events.clear()
-    step(tr.start_of_iteration(_fresh(batches[1]), 10 + trial))
+    with routing():
+        step(tr.start_of_iteration(_fresh(batches[1]), 10 + trial))
     torch.cuda.synchronize()
     badp = [n for n, p in list(tr.net_G.named_parameters()) + list(tr.net_D.named_parameters())
             if p.grad is not None and not torch.isfinite(p.grad).all()]

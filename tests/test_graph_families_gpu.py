@@ -85,21 +85,31 @@ def _losses(tr):
     return out
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize('name,seq_len', [('munit', None), ('pix2pixHD', None),
-                                          ('vid2vid_street', 3), ('fs_vid2vid_face', 2)])
-def test_family_graph_replay_matches_eager(name, seq_len):
+def _case_worker(name, seq_len, q):
+    """Capture + replay vs eager for one family, in a fresh process (see the test)."""
+    import faulthandler
+    import sys
+    faulthandler.dump_traceback_later(170, exit=True, file=sys.__stderr__)
+    try:
+        q.put(('ok', _run_case(name, seq_len)))
+    except BaseException as e:  # noqa: BLE001 - reported to the parent
+        import traceback
+        q.put(('error', '%s: %s\n%s' % (type(e).__name__, e, traceback.format_exc())))
+
+
+def _run_case(name, seq_len):
     from imaginaire_amd.utils.cuda_graph import graph_routing, make_trainer_step
     torch.cuda.set_device(0)
     cfg, tr, batches = _build(name, seq_len)
-    assert getattr(tr, 'graph_capturable', False), name + ' is not marked capturable'
+    capturable = bool(getattr(tr, 'graph_capturable', False))
     step, graphed = make_trainer_step(tr, warmup=2, enabled=True)
-    assert graphed is not None
+    if graphed is None:
+        return {'capturable': capturable, 'graphed': False}
     for i in range(3):  # 2 eager warm-up iterations, then capture (+ first replay)
         torch.manual_seed(3)
         step(tr.start_of_iteration(_fresh(batches[i % 2]), i))
     torch.cuda.synchronize()
-    assert graphed.graph is not None and not graphed.failed, 'step was not captured'
+    captured = graphed.graph is not None and not graphed.failed
     state = _state(tr)
     saved = [t.detach().clone() for t in state]
     gparams = list(tr.net_G.parameters())
@@ -121,19 +131,46 @@ def test_family_graph_replay_matches_eager(name, seq_len):
     torch.cuda.synchronize()
     le = _losses(tr)
     de = [p.detach() - q for p, q in zip(gparams, p0)]
-    print(name, 'graph', lg, '\n', name, 'eager', le)
     names = [n for n, _ in tr.net_G.named_parameters()]
     bad = [n for n, x in zip(names, dg) if not torch.isfinite(x).all()]
-    assert not bad, 'non-finite replayed G updates: %s' % bad[:8]
+    num = sum(float((x - y).float().pow(2).sum()) for x, y in zip(dg, de))
+    den = sum(float(y.float().pow(2).sum()) for y in de)
+    return {'capturable': capturable, 'graphed': True, 'captured': captured, 'lg': lg,
+            'le': le, 'bad': bad[:8], 'num': num, 'den': den}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name,seq_len', [('munit', None), ('pix2pixHD', None),
+                                          ('vid2vid_street', 3), ('fs_vid2vid_face', 2)])
+def test_family_graph_replay_matches_eager(name, seq_len):
+    """Each case runs in a FRESH process (spawn): the comparison needs the eager run and the
+    replay to start from the same allocator history. In a process that had run other GPU tests
+    first, fs-vid2vid's eager iteration drifted from its replay by up to ~0.1 in the losses
+    while a fresh process gives bitwise-equal losses (open: scripts/probe/poison_probe.py with
+    IAMD_PROBE_ROUTING=1 looks for a kernel reading memory it never wrote)."""
+    import multiprocessing as mp
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    proc = ctx.Process(target=_case_worker, args=(name, seq_len, q))
+    proc.start()
+    try:
+        status, res = q.get(timeout=190)
+    finally:
+        proc.join(30)
+        if proc.is_alive():
+            proc.kill()
+    assert status == 'ok', res
+    assert res['capturable'], name + ' is not marked capturable'
+    assert res['graphed'] and res['captured'], 'step was not captured'
+    lg, le = res['lg'], res['le']
+    print(name, 'graph', lg, '\n', name, 'eager', le)
+    assert not res['bad'], 'non-finite replayed G updates: %s' % res['bad']
     assert lg.keys() == le.keys() and lg
     for k in le:
         assert lg[k] == lg[k], k  # finite
         # the G-side adversarial terms read D right after its Adam step, whose first updates are
-        # ~lr * sign(grad): bf16-level differences in near-zero D gradients (atomics in the
-        # flow-warp backward, kernel choices made by tests run earlier in the process) move them
-        # by up to ~0.05 while every other loss agrees to ~1e-3 (run alone: bitwise equal)
+        # ~lr * sign(grad): bf16-level differences in near-zero D gradients move them by up to
+        # ~0.05 while every other loss agrees to ~1e-3
         tol = 1e-1 if k.startswith('G/GAN') else 3e-2
         assert abs(lg[k] - le[k]) <= tol * max(1.0, abs(le[k])), (k, lg[k], le[k])
-    num = sum(float((x - y).float().pow(2).sum()) for x, y in zip(dg, de))
-    den = sum(float(y.float().pow(2).sum()) for y in de)
-    assert den > 0 and num <= 0.1 * den, (num, den)
+    assert res['den'] > 0 and res['num'] <= 0.1 * res['den'], (res['num'], res['den'])
