@@ -130,7 +130,7 @@ def prefetch_sync_stats(x, eps, group):
     key = _stats_key(x, eps, group, True)
     if getattr(x, '_iamd_bn_stats', (None,))[0] == key:
         return
-    count, mean, var, _, _ = _ext.ext().norm_stats(x, False, eps, None, None, True)
+    count, mean, var = _ext.ext().norm_stats(x, False, eps, None, None, True)[:3]
     stacked = torch.stack([count.reshape(-1), mean.reshape(-1), var.reshape(-1)], 0).contiguous()
     allst = stacked.new_empty((_world(group),) + tuple(stacked.shape))
     work = _gather_rows(allst, stacked, group, async_op=True)
