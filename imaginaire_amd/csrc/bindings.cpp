@@ -97,9 +97,13 @@ at::Tensor resample2d_forward(const at::Tensor& in1, const at::Tensor& flow, int
 std::vector<at::Tensor> resample2d_backward(const at::Tensor& in1, const at::Tensor& flow,
                                             const at::Tensor& dout, int64_t ks);
 // conv_mfma.hip (k10)
+at::Tensor channel_softmax_fwd(const at::Tensor& x);
+std::vector<at::Tensor> mt_conv_weight_flip_t(const std::vector<at::Tensor>& ws);
+at::Tensor channel_softmax_bwd(const at::Tensor& y, const at::Tensor& dy);
 at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                        int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
-                       double slope, int64_t nb, int64_t ncv);
+                       double slope, int64_t nb, int64_t ncv,
+                       const c10::optional<at::Tensor>& residual);
 at::Tensor conv2d_dgrad_mfma(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int64_t pw,
                              int64_t ncv);
 at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t KH, int64_t KW,
@@ -165,7 +169,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv2d_mfma", &iamd::conv2d_mfma, "MFMA implicit-GEMM NHWC conv + bias + act (k10)",
         py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("sh"), py::arg("sw"), py::arg("ph"),
         py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("slope"), py::arg("nb") = 1,
-        py::arg("ncv") = -1);
+        py::arg("ncv") = -1, py::arg("residual") = py::none());
   m.def("conv2d_dgrad_mfma", &iamd::conv2d_dgrad_mfma,
         "stride-1 conv data gradient from the forward weight (k10 v4 transposed-weight path)",
         py::arg("dy"), py::arg("w"), py::arg("ph"), py::arg("pw"), py::arg("ncv") = -1);
@@ -178,6 +182,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "whether the k11 v2 (one wave per SIMD) kernel can run this weight gradient",
         py::arg("dy"), py::arg("x"), py::arg("KH"), py::arg("KW"), py::arg("sh"), py::arg("sw"),
         py::arg("dh"), py::arg("dw"), py::arg("nb") = 1);
+  m.def("channel_softmax_fwd", &iamd::channel_softmax_fwd,
+        "softmax over the channels of a channels-last bf16 tensor (k15)");
+  m.def("channel_softmax_bwd", &iamd::channel_softmax_bwd, "k15 backward: y * (dy - sum(dy y))");
+  m.def("mt_conv_weight_flip_t", &iamd::mt_conv_weight_flip_t,
+        "flipped, transposed (dgrad) copies of many conv weights in one launch");
   m.def("conv_tap_sum", &iamd::conv_tap_sum, "tap-split conv: sum of per-tap partials (+bias)");
   m.def("conv_tap_gather", &iamd::conv_tap_gather, "tap-split conv backward: dy -> per-tap dZ");
   m.def("conv_phase_scatter", &iamd::conv_phase_scatter,

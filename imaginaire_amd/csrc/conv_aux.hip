@@ -21,6 +21,9 @@
 // (layers/conv.py:59-91); these kernels have no reference counterpart.
 #include "common.h"
 
+#include <mutex>
+#include <unordered_map>
+
 namespace iamd {
 namespace {
 
@@ -359,6 +362,148 @@ at::Tensor conv_weight_flip_t(const at::Tensor& w, int64_t s, int64_t qy, int64_
                      (int)s, (int)qy, (int)qx);
   IAMD_LAUNCH_CHECK();
   return wt;
+}
+
+namespace {
+
+// ---- multi-tensor plain flip (s = 1): every stride-1 conv weight of a network in one launch --
+// The data gradient of each stride-1 conv needs its flipped, transposed weight. Flipping in the
+// conv's backward costs one small launch per layer (~220 per SPADE step, 1.26 ms,
+// profiles/spade_step_latest_mi355x.txt); the spectral-norm group that produces every layer's
+// bf16 W / sigma in one launch (sn_power.hip k5c) flips them all right after it, in one more.
+struct FlipEntry {
+  int64_t src;  // element offset of the source weight from the base pointer (may be < 0)
+  int64_t dst;  // element offset in the flat output
+  int Cout, Cin, KH, KW, nci, nco;
+};
+
+__global__ void __launch_bounds__(kT)
+mt_flip_kernel(const FlipEntry* __restrict__ ents, const int* __restrict__ blocks,
+               const __hip_bfloat16* __restrict__ base, __hip_bfloat16* __restrict__ out) {
+  __shared__ __hip_bfloat16 tile[kTile * kLdsStride];
+  const FlipEntry e = ents[blocks[2 * blockIdx.x]];
+  int b = blocks[2 * blockIdx.x + 1];
+  const int KK = e.KH * e.KW;
+  const int tap = b % KK;
+  b /= KK;
+  const int cit = b % e.nci, cot = b / e.nci;
+  const int ci0 = cit * kTile, co0 = cot * kTile;
+  const int jy = tap / e.KW, jx = tap - jy * e.KW;
+  const int ftap = (e.KH - 1 - jy) * e.KW + (e.KW - 1 - jx);
+  const __hip_bfloat16* w = base + e.src;
+  __hip_bfloat16* wt = out + e.dst;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int q = tid + r * kT;
+    const int row = q >> 3, ch = q & 7;
+    const int co = co0 + row, ci = ci0 + ch * 8;
+    Pack<__hip_bfloat16, 8> v;
+    if (co < e.Cout && ci < e.Cin) {
+      v = *reinterpret_cast<const Pack<__hip_bfloat16, 8>*>(
+          w + ((int64_t)co * KK + ftap) * e.Cin + ci);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v.v[k] = __float2bfloat16(0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) tile[row * kLdsStride + ch * 8 + k] = v.v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int q = tid + r * kT;
+    const int row = q >> 3, ch = q & 7;
+    const int ci = ci0 + row, co = co0 + ch * 8;
+    if (ci >= e.Cin || co >= e.Cout) continue;
+    Pack<__hip_bfloat16, 8> v;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v.v[k] = tile[(ch * 8 + k) * kLdsStride + row];
+    *reinterpret_cast<Pack<__hip_bfloat16, 8>*>(wt + ((int64_t)ci * KK + tap) * e.Cout + co) = v;
+  }
+}
+
+struct FlipPlan {
+  at::Tensor ents, blocks;
+  int nblocks;
+  int64_t total;
+  std::vector<int64_t> offs;
+};
+std::mutex g_flip_mu;
+std::unordered_map<uint64_t, FlipPlan> g_flip_cache;
+
+}  // namespace
+
+// Plain flips wt[ci][kh][kw][co] = w[co][KH-1-kh][KW-1-kw][ci] of every weight in ``ws`` (bf16,
+// channels-last, channels multiples of 8) into ONE flat buffer, one launch. The launch plan is
+// cached on the weights' shapes and their offsets from ws[0] (the views of one flat buffer
+// keep them from call to call).
+std::vector<at::Tensor> mt_conv_weight_flip_t(const std::vector<at::Tensor>& ws) {
+  IAMD_CHECK(!ws.empty(), "mt_conv_weight_flip_t: empty list");
+  const char* base = reinterpret_cast<const char*>(ws[0].data_ptr());
+  uint64_t h = 0x9E3779B97F4A7C15ULL;
+  for (auto& w : ws) {
+    IAMD_CHECK(w.is_cuda() && w.dim() == 4 && w.scalar_type() == at::kBFloat16 &&
+                   w.is_contiguous(at::MemoryFormat::ChannelsLast) && w.size(0) % 8 == 0 &&
+                   w.size(1) % 8 == 0 && w.device() == ws[0].device(),
+               "mt_conv_weight_flip_t: channels-last bf16 weights with channels % 8 == 0");
+    const int64_t rel = reinterpret_cast<const char*>(w.data_ptr()) - base;
+    IAMD_CHECK(rel % 2 == 0, "mt_conv_weight_flip_t: misaligned weight");
+    for (int64_t v : {rel, w.size(0), w.size(1), w.size(2), w.size(3)})
+      h ^= (uint64_t)v + 0x9e3779b97f4a7c15ULL + (h << 6) + (h >> 2);
+  }
+  FlipPlan* pp;
+  {
+    std::lock_guard<std::mutex> lk(g_flip_mu);
+    auto it = g_flip_cache.find(h);
+    if (it == g_flip_cache.end()) {
+      FlipPlan p;
+      std::vector<FlipEntry> ents;
+      std::vector<int32_t> bm;
+      int64_t off = 0;
+      for (size_t i = 0; i < ws.size(); ++i) {
+        const auto& w = ws[i];
+        FlipEntry e;
+        e.src = (reinterpret_cast<const char*>(w.data_ptr()) - base) / 2;
+        e.dst = off;
+        e.Cout = (int)w.size(0); e.Cin = (int)w.size(1); e.KH = (int)w.size(2);
+        e.KW = (int)w.size(3);
+        e.nci = ceil_div(e.Cin, kTile);
+        e.nco = ceil_div(e.Cout, kTile);
+        ents.push_back(e);
+        p.offs.push_back(off);
+        const int nb = e.nci * e.nco * e.KH * e.KW;
+        for (int b = 0; b < nb; ++b) {
+          bm.push_back((int32_t)i);
+          bm.push_back(b);
+        }
+        off += (w.numel() + 7) / 8 * 8;
+      }
+      p.total = off;
+      p.ents = stage_to_device(ents.data(), ents.size() * sizeof(FlipEntry), ws[0].device());
+      p.blocks = stage_to_device(bm.data(), bm.size() * sizeof(int32_t), ws[0].device())
+                     .view(at::kInt);
+      p.nblocks = (int)(bm.size() / 2);
+      if (g_flip_cache.size() > 64) g_flip_cache.clear();
+      it = g_flip_cache.emplace(h, std::move(p)).first;
+    }
+    pp = &it->second;
+  }
+  auto flat = at::empty({pp->total}, ws[0].options());
+  hipLaunchKernelGGL(mt_flip_kernel, dim3(pp->nblocks), dim3(kT), 0, stream(),
+                     reinterpret_cast<const FlipEntry*>(pp->ents.data_ptr()),
+                     pp->blocks.data_ptr<int>(),
+                     reinterpret_cast<const __hip_bfloat16*>(ws[0].data_ptr()),
+                     reinterpret_cast<__hip_bfloat16*>(flat.data_ptr()));
+  IAMD_LAUNCH_CHECK();
+  std::vector<at::Tensor> out;
+  for (size_t i = 0; i < ws.size(); ++i) {
+    const auto& w = ws[i];
+    const int64_t co = w.size(0), ci = w.size(1), kh = w.size(2), kw = w.size(3);
+    // [Cin, Cout, KH, KW] channels-last: strides (KH*KW*Cout, 1, KW*Cout, Cout)
+    out.push_back(flat.as_strided({ci, co, kh, kw}, {kh * kw * co, 1, kw * co, co}, pp->offs[i]));
+  }
+  return out;
 }
 
 // part: fp32 [S * Cop * KK * Cip] -> [Cout, Cin, KH, KW] channels-last in `dtype`.

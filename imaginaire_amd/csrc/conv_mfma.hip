@@ -70,7 +70,35 @@ struct ConvArgs {
   // channels stored per output pixel = row stride of y (<= Cout, a multiple of 8): the padded
   // output channels of a Cout % 64 != 0 conv are never written, so no crop copy follows
   int ldy;
+  // residual added after the activation, same layout as y (nullptr: none): the shortcut of a
+  // residual block whose branch ends in this conv (reference layers/residual.py:150
+  // ``x_shortcut + dx``) lands in the epilogue instead of a separate full-tensor add
+  const __hip_bfloat16* res;
 };
+
+// y[off .. off + 8) = v (+ res[off .. off + 8) when the conv carries a residual), one 16-byte
+// store. The residual is added to the bf16-rounded conv output and rounded again: the same
+// two roundings as the unfused bf16 conv followed by a bf16 add.
+__device__ __forceinline__ void store_chunk(const ConvArgs& a, __hip_bfloat16* y, size_t off,
+                                            uint4 v) {
+  if (a.res) {
+    const uint4 r = *reinterpret_cast<const uint4*>(a.res + off);
+    const uint32_t* pv = reinterpret_cast<const uint32_t*>(&v);
+    const uint32_t* pr = reinterpret_cast<const uint32_t*>(&r);
+    uint4 o;
+    uint32_t* po = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float lo = __uint_as_float(pv[k] << 16) + __uint_as_float(pr[k] << 16);
+      const float hi = __uint_as_float(pv[k] & 0xffff0000u) + __uint_as_float(pr[k] & 0xffff0000u);
+      const __hip_bfloat16 blo = __float2bfloat16(lo), bhi = __float2bfloat16(hi);
+      po[k] = (uint32_t)(*reinterpret_cast<const uint16_t*>(&blo)) |
+              ((uint32_t)(*reinterpret_cast<const uint16_t*>(&bhi)) << 16);
+    }
+    v = o;
+  }
+  *reinterpret_cast<uint4*>(y + off) = v;
+}
 
 // destination pixel (row of the NHWC output) of GEMM row m
 __device__ __forceinline__ size_t out_row(const ConvArgs& a, int m) {
@@ -291,7 +319,7 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_fwd_mfma(ConvA
     const int m = m0 + rl;
     if (m < a.M && n0 + ch * 8 < a.ldy) {
       const uint4 v = *reinterpret_cast<const uint4*>(E + rl * kEpiStride + ch * 16);
-      *reinterpret_cast<uint4*>(yz + out_row(a, m) * a.ldy + n0 + ch * 8) = v;
+      store_chunk(a, yz, out_row(a, m) * a.ldy + n0 + ch * 8, v);
     }
   }
 #endif  // __HIP_DEVICE_COMPILE__
@@ -487,7 +515,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v2(ConvArgs a) {
     const int m = m0 + rl;
     if (m < a.M && n0 + ch * 8 < a.ldy) {
       const uint4 v = *reinterpret_cast<const uint4*>(E + rl * kEpiStride + ch * 16);
-      *reinterpret_cast<uint4*>(a.y + out_row(a, m) * a.ldy + n0 + ch * 8) = v;
+      store_chunk(a, a.y, out_row(a, m) * a.ldy + n0 + ch * 8, v);
     }
   }
 #endif  // __HIP_DEVICE_COMPILE__
@@ -740,7 +768,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v3(ConvArgs a) {
       const int m = m0 + rl;
       if (m < a.M && n0 + half * 128 + ch * 8 < a.ldy) {
         const uint4 v = *reinterpret_cast<const uint4*>(E + rl * kEpiStride + ch * 16);
-        *reinterpret_cast<uint4*>(a.y + out_row(a, m) * a.ldy + n0 + half * 128 + ch * 8) = v;
+        store_chunk(a, a.y, out_row(a, m) * a.ldy + n0 + half * 128 + ch * 8, v);
       }
     }
     __syncthreads();
@@ -1067,7 +1095,255 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v4(ConvArgs a) {
     const int m = m0 + rl;
     if (m < a.M && n0 + ch * 8 < a.ldy) {
       const uint4 v = *reinterpret_cast<const uint4*>(E + rl * kEpiStride + ch * 16);
-      *reinterpret_cast<uint4*>(a.y + out_row(a, m) * a.ldy + n0 + ch * 8) = v;
+      store_chunk(a, a.y, out_row(a, m) * a.ldy + n0 + ch * 8, v);
+    }
+  }
+#endif  // __HIP_DEVICE_COMPILE__
+}
+
+// ---- k10 v5: row-window implicit GEMM, 256 x 256 tile, 8 waves of 128 x 64 -----------------
+//
+// v4's 64 x 64 wave tile reads 512 LDS bytes per MFMA (A and B fragments) and, with the DMA
+// writes, keeps the LDS array ~80% busy against the MFMA pipe (MFMA busy 54-63%,
+// profiles/pmc_conv_v4_r3_mi355x.txt). Here each of the 8 waves (2 (M) x 4 (N)) owns a
+// 128 x 64 sub-tile of a 256-pixel x 256-channel block: 384 B per MFMA, and the window staged
+// per (filter row, channel block) is shared by twice the output channels.
+// LDS (144 KB): two 32 KB weight slots (tap t+1 staged during tap t: the 256-row tile is too
+// large for v4's KW-slot ring) at offset 0, then two 40 KB window buffers.
+// Window rows of output-row segment s start at row s * (SW + 8) (pitch padded to a multiple of
+// 8 rows), so a fragment row's swizzle key (row & 7) is (lane + kx) & 7 for every fragment:
+// per tap step two VGPR fragment bases, everything else is an ds_read immediate (FULLROW, one
+// 256-pixel segment per block) or one add per fragment (SW = 32..128).
+// DMA order per tap step: weights of the next tap, then (first tap of a filter row) the next
+// window, so the wait at tap 1 (vmcnt(5)) retires only the weights; other taps vmcnt(0).
+template <int KW, bool HAS_BIAS, bool FULLROW>
+__global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v5(ConvArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  constexpr int BM = 256, BN = 256;
+  constexpr int kArows = 320;                     // window rows per buffer: 5 DMA rounds of 64
+  constexpr int kAbytes = kArows * kRowBytes;     // 40 KB
+  constexpr int kBbytes = BN * kRowBytes;         // 32 KB per weight slot
+  constexpr int kAoff = 2 * kBbytes;              // windows after the two weight slots
+  constexpr int kEpi = BN * 2 + 16;               // epilogue row stride (bytes)
+  constexpr int kSmem = kAoff + 2 * kAbytes;
+  static_assert(BM * kEpi <= kSmem, "v5 epilogue staging exceeds LDS");
+  __shared__ __attribute__((aligned(16))) char smem[kSmem];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid / a.nNt, nt = bid - mt * a.nNt;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int HoWo = a.Ho * a.Wo;
+  const int SW = FULLROW ? BM : a.Wo;             // pixels per output-row segment
+  const int P = SW + 8;                           // LDS row pitch of a segment's window
+  const int R = BM / SW;
+
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__hip_bfloat16*>(a.x), 0, a.xbytes, kBufCfg);
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__hip_bfloat16*>(a.w), 0, a.wbytes, kBufCfg);
+
+  // ---- window DMA sources: round r of wave w moves LDS rows 64 r + 8 w + (lane >> 3) -------
+  // Rows outside the image columns or past a segment's SW + KW - 1 window rows get an offset
+  // past the tensor (any koff added keeps it past: koff < xbytes < 2^31), so the buffer unit
+  // returns zeros; the filter-row validity is a per-row bit mask (FULLROW: one output row per
+  // block, so the mask is wave-uniform and lives in an SGPR).
+  const int dr = lane >> 3;
+  const int csw = (lane & 7) ^ dr;                // row & 7 == dr for every staged row
+  const int rowbytes = a.W * a.Cin * 2;
+  int a_off[5];
+  uint32_t a_km[FULLROW ? 1 : 5];
+  if constexpr (FULLROW) {
+    const int b = m0 / HoWo, rr = m0 - b * HoWo;
+    const int oh = rr / a.Wo, ow0 = rr - oh * a.Wo;
+    const int ih0 = oh - a.ph;
+    uint32_t km = 0;
+    for (int ky = 0; ky < a.KH; ++ky) km |= (uint32_t)((unsigned)(ih0 + ky) < (unsigned)a.H) << ky;
+    a_km[0] = __builtin_amdgcn_readfirstlane(km);
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      const int j = r * 64 + wid * 8 + dr;
+      const int iw = ow0 - a.pw + j;
+      a_off[r] = (j < SW + KW - 1 && (unsigned)iw < (unsigned)a.W)
+                     ? (b * a.H + ih0) * rowbytes + (iw * a.Cin + csw * 8) * 2
+                     : kOobOffset;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      const int row = r * 64 + wid * 8 + dr;
+      const int s = row / P, j = row - s * P;
+      a_off[r] = kOobOffset;
+      a_km[r] = 0;
+      if (s < R && j < SW + KW - 1) {
+        const int m = m0 + s * SW;
+        const int b = m / HoWo, rr = m - b * HoWo;
+        const int oh = rr / a.Wo, ow0 = rr - oh * a.Wo;
+        const int ih0 = oh - a.ph, iw = ow0 - a.pw + j;
+        if ((unsigned)iw < (unsigned)a.W) {
+          a_off[r] = (b * a.H + ih0) * rowbytes + (iw * a.Cin + csw * 8) * 2;
+          for (int ky = 0; ky < a.KH; ++ky)
+            a_km[r] |= (uint32_t)((unsigned)(ih0 + ky) < (unsigned)a.H) << ky;
+        }
+      }
+    }
+  }
+  const int wrow_bytes = a.nk * kBK * 2;
+  int b_off[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) b_off[i] = (n0 + i * 64 + wid * 8 + dr) * wrow_bytes + csw * 16;
+
+  const int o0 = blockIdx.y * a.kps;
+  const int o1 = min(a.nk / KW, o0 + a.kps);
+  // (filter row, channel offset) of the outer step being computed and of the next one
+  int cky = o0 / a.cpt, ccc = (o0 - (o0 / a.cpt) * a.cpt) * kBK;
+  int nky = cky, ncc = ccc + kBK;
+  if (ncc == a.Cin) { ncc = 0; ++nky; }
+  auto issueA = [&](int o, int ky, int cc, int buf) {
+    const uint32_t live = o < o1;
+    const int koff = ky * rowbytes + cc * 2;
+    char* As = smem + kAoff + buf * kAbytes;
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      const uint32_t ok = live & (a_km[FULLROW ? 0 : r] >> (ky & 31));
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          xrs, (lds_ptr_t)(As + r * 8192 + wid * 1024), 16,
+          (ok & 1u) ? a_off[r] + koff : kOobOffset, 0, 0, 0);
+    }
+  };
+  auto issueB = [&](int o, int ky, int cc, int kx, int slot) {
+    const int soff = o < o1 ? ((ky * KW + kx) * a.Cin + cc) * 2 : kOobOffset;
+    char* Bs = smem + slot * kBbytes;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)(Bs + i * 8192 + wid * 1024), 16,
+                                               b_off[i], soff, 0, 0);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // A fragment i of this wave: output pixels p = wm*128 + i*16 + frow, window row p + 8 s(p)
+  // (16 | SW: a fragment never straddles two segments). Wave-uniform: SGPRs.
+  int arow[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int pb = wm * 128 + i * 16;
+    arow[i] = FULLROW ? 0 : 8 * (pb / SW) * kRowBytes;
+  }
+
+  auto tapstep = [&](int abuf, int kx, int slot) {
+    // The fragment addresses are recomputed per tap step from an opaque copy of the lane id:
+    // hoisted out of the loop they are 2 * KW * (8 + 1) loop-invariant registers, which spill
+    // (and a scratch reload's vmcnt wait drains the in-flight DMA).
+    int l = lane;
+    asm volatile("" : "+v"(l));
+    const int frow = l & 15, fk = l >> 4;
+    const int key = (frow + kx) & 7;
+    const int rb = (wm * 128 + frow) * kRowBytes;
+    const int ab0 = kAoff + rb + (((0 * 4 + fk) ^ key) << 4);
+    const int ab1 = kAoff + rb + (((1 * 4 + fk) ^ key) << 4);
+    const int brb = (wn * 64 + frow) * kRowBytes;
+    const int bb0 = brb + (((0 * 4 + fk) ^ (frow & 7)) << 4);
+    const int bb1 = brb + (((1 * 4 + fk) ^ (frow & 7)) << 4);
+    // (per k-half: 12 fragments = 48 VGPRs beside the 128 accumulator registers; hoisting
+    // both halves' reads spills at the 256-register budget of two waves per SIMD)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[8], bfr[4];
+      const int ab = kk ? ab1 : ab0;
+      const int bb = kk ? bb1 : bb0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(smem + bb + slot * kBbytes +
+                                                  j * 16 * kRowBytes);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(
+            smem + ab + arow[i] + abuf * kAbytes + (i * 16 + kx) * kRowBytes);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  };
+  // one outer step: KW tap steps; tap step kx stages the weights of the next tap (or of the
+  // next outer step's tap 0) into the other slot and, at kx == 0, the next outer step's window.
+  // ol = parity of (o - o0): slot of tap step (o, kx) = ((o - o0) * KW + kx) & 1
+  auto outer = [&](int o, int abuf, int ol) {
+#pragma unroll
+    for (int kx = 0; kx < KW; ++kx) {
+      if (kx == 1)
+        asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");  // younger: the window
+      else
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      const int slot = (ol * KW + kx) & 1;
+      if (kx + 1 < KW) issueB(o, cky, ccc, kx + 1, slot ^ 1);
+      else issueB(o + 1, nky, ncc, 0, slot ^ 1);
+      if (kx == 0) issueA(o + 1, nky, ncc, abuf ^ 1);
+      tapstep(abuf, kx, slot);
+    }
+    cky = nky;
+    ccc = ncc;
+    ncc += kBK;
+    if (ncc == a.Cin) { ncc = 0; ++nky; }
+  };
+  issueB(o0, cky, ccc, 0, 0);
+  issueA(o0, cky, ccc, 0);
+  for (int o = o0; o < o1; o += 2) {
+    outer(o, 0, 0);
+    if (o + 1 < o1) outer(o + 1, 1, 1);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // trailing (zero) prefetches landed and every wave is done reading
+
+  if (a.part) {
+    float* op = a.part + (size_t)blockIdx.y * a.M * a.Cout;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * 128 + i * 16 + (lane >> 4) * 4 + r;
+          if (m < a.M)
+            op[(size_t)m * a.Cout + n0 + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+        }
+    return;
+  }
+  char* E = smem;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int cl = wn * 64 + j * 16 + (lane & 15);
+    const float bv = HAS_BIAS ? a.bias[n0 + cl] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rl = wm * 128 + i * 16 + (lane >> 4) * 4 + r;
+        float v = acc[i][j][r] + bv;
+        v = v > 0.f ? v : v * a.slope;
+        *reinterpret_cast<__hip_bfloat16*>(E + rl * kEpi + cl * 2) = __float2bfloat16(v);
+      }
+  }
+  __syncthreads();
+  const int ch = tid & 31, rr = tid >> 5;  // 32 chunks per row, 16 rows per pass
+#pragma unroll 4
+  for (int p = 0; p < BM / 16; ++p) {
+    const int rl = p * 16 + rr;
+    const int m = m0 + rl;
+    if (m < a.M && n0 + ch * 8 < a.ldy) {
+      const uint4 v = *reinterpret_cast<const uint4*>(E + rl * kEpi + ch * 16);
+      store_chunk(a, a.y, out_row(a, m) * a.ldy + n0 + ch * 8, v);
     }
   }
 #endif  // __HIP_DEVICE_COMPILE__
@@ -1101,7 +1377,14 @@ conv_splitk_reduce(const float* __restrict__ part, const float* __restrict__ bia
       acc[k] = t > 0.f ? t : t * slope;
     }
     const int64_t m = e / C - (int64_t)zb * map.M;
-    store_vec<__hip_bfloat16, 8>(y + zb * map.ybs + out_row(map, (int)m) * map.ldy + c, acc);
+    const size_t off = (size_t)zb * map.ybs + out_row(map, (int)m) * map.ldy + c;
+    if (map.res) {  // (bf16 conv output + residual, as store_chunk)
+      float r[8];
+      load_vec<__hip_bfloat16, 8>(map.res + off, r);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] = __bfloat162float(__float2bfloat16(acc[k])) + r[k];
+    }
+    store_vec<__hip_bfloat16, 8>(y + off, acc);
   }
 }
 
@@ -1172,6 +1455,70 @@ void run_v4(ConvArgs& a, const at::Tensor& x, bool bt) {
   IAMD_LAUNCH_CHECK();
 }
 
+// v5 (row-window, 256 x 256): v4's geometry with Cout % 256 == 0, KW 3 or 5, and output rows
+// of >= 32 pixels (the padded segment pitch of 16-pixel rows does not fit the window buffer)
+bool v5_shape_ok(const ConvArgs& a) {
+  return v4_eligible(a) && a.Cout % 256 == 0 && (a.KW == 3 || a.KW == 5) &&
+         (a.Wo % 256 == 0 || a.Wo >= 32);
+}
+
+bool v5_eligible(const ConvArgs& a) {
+  static const int mode = [] {
+    // 0: A/B switch back to v4; 2: every eligible shape, whatever its grid
+    const char* e = std::getenv("IMAGINAIRE_AMD_CONV_V5");
+    return e == nullptr ? 1 : std::atoi(e);
+  }();
+  if (mode == 0 || !v5_shape_ok(a)) return false;
+  // grids below one 256 x 256 tile per CU split K and reduce; v4's 256 x 128 grid of the same
+  // conv is twice as wide: v5 measured 0.57-0.93x v4 on those (G up0 1024 @ 32x64, VGG 256 @
+  // 64x128) and 1.06-1.16x on every grid of >= 256 tiles (profiles/conv_v5_probe_mi355x.txt)
+  return mode == 2 || (int64_t)(a.M / 256) * (a.Cout / 256) >= 256;
+}
+
+void run_v5(ConvArgs& a, const at::Tensor& x) {
+  const int Cout = a.Cout, KW = a.KW;
+  a.nNt = Cout / 256;
+  const int64_t tiles = (int64_t)(a.M / 256) * a.nNt;
+  const int nout = a.nk / KW;
+  int S = 1;
+  if (tiles < 256 && nout >= 8) S = (int)std::min<int64_t>((256 + tiles - 1) / tiles, nout / 4);
+  if (const char* e = std::getenv("IMAGINAIRE_AMD_CONV_SPLITK")) S = std::max(1, std::atoi(e));
+  S = std::max(1, std::min(S, nout));
+  a.kps = ceil_div(nout, S);
+  S = ceil_div(nout, a.kps);
+  at::Tensor part;
+  a.part = nullptr;
+  if (S > 1) {
+    part = at::empty({(int64_t)S * a.M * Cout}, x.options().dtype(at::kFloat));
+    a.part = part.data_ptr<float>();
+  }
+  const dim3 grid((unsigned)tiles, (unsigned)S, 1);
+  const bool full = a.Wo % 256 == 0;
+  auto launch = [&](auto kv, auto hbv, auto fv) {
+    constexpr int K = decltype(kv)::value;
+    constexpr bool HB = decltype(hbv)::value, FR = decltype(fv)::value;
+    hipLaunchKernelGGL((conv_fwd_mfma_v5<K, HB, FR>), grid, dim3(512), 0, stream(), a);
+  };
+  auto by_full = [&](auto kv, auto hbv) {
+    if (full) launch(kv, hbv, std::true_type());
+    else launch(kv, hbv, std::false_type());
+  };
+  auto by_bias = [&](auto kv) {
+    if (a.bias) by_full(kv, std::true_type());
+    else by_full(kv, std::false_type());
+  };
+  if (KW == 5) by_bias(std::integral_constant<int, 5>());
+  else by_bias(std::integral_constant<int, 3>());
+  if (S > 1) {
+    IAMD_LAUNCH_CHECK();
+    const int64_t MC = (int64_t)a.M * Cout;
+    const int blocks = (int)std::min<int64_t>((MC / 8 + 255) / 256, 8192);
+    hipLaunchKernelGGL(conv_splitk_reduce, dim3(blocks), dim3(256), 0, stream(), a.part, a.bias,
+                       a.y, S, MC, Cout, a.slope, a);
+  }
+  IAMD_LAUNCH_CHECK();
+}
+
 // Kernel choice, split-K and launch for a filled-in ConvArgs (x supplies the tensor options of
 // the split-K slabs).
 void run_conv(ConvArgs& a, const at::Tensor& x) {
@@ -1198,6 +1545,10 @@ void run_conv(ConvArgs& a, const at::Tensor& x) {
     S = std::max(1, std::min(S, a.nk));
     return ceil_div(a.nk, ceil_div(a.nk, S));
   };
+  if ((ver == 0 && v5_eligible(a)) || (ver == 5 && v5_shape_ok(a))) {
+    run_v5(a, x);
+    return;
+  }
   if ((ver == 4 || ver == 0) && v4_eligible(a)) {
     // default: every eligible conv (1.02-1.52x v1 and 1.0-1.08x v3 on the SPADE-step shapes,
     // the N = 128 data gradients 1.36-1.52x: profiles/conv_v4_probe_mi355x.txt)
@@ -1308,7 +1659,8 @@ void run_conv(ConvArgs& a, const at::Tensor& x) {
 // (sample-major), bias [nb * Cout]: y[b] = act(conv2d(x[b], w[b]) + bias[b]).
 at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                        int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
-                       double slope, int64_t nb, int64_t ncv) {
+                       double slope, int64_t nb, int64_t ncv,
+                       const c10::optional<at::Tensor>& residual) {
   IAMD_CHECK(x.is_cuda() && w.is_cuda(), "conv2d_mfma: CUDA tensors expected");
   IAMD_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16,
              "conv2d_mfma: bf16 operands expected");
@@ -1362,6 +1714,16 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
   a.slope = (float)slope;
   a.omode = 0;
   a.oH = Ho; a.oW = Wo; a.osy = 1; a.osx = 1; a.ory = 0; a.orx = 0;
+  a.res = nullptr;
+  if (residual.has_value() && residual->defined()) {
+    const at::Tensor& r = *residual;
+    IAMD_CHECK(nb == 1 && r.is_cuda() && r.scalar_type() == at::kBFloat16 && r.dim() == 4 &&
+                   r.size(0) == B && r.size(1) == ncv && r.size(2) == Ho && r.size(3) == Wo &&
+                   r.is_contiguous(at::MemoryFormat::ChannelsLast),
+               "conv2d_mfma: the residual must be a packed channels-last bf16 tensor shaped "
+               "like the output (single-weight convs only)");
+    a.res = reinterpret_cast<const __hip_bfloat16*>(r.data_ptr());
+  }
   run_conv(a, x);
   return y;
 }
@@ -1409,7 +1771,7 @@ at::Tensor conv2d_dgrad_mfma(const at::Tensor& dy, const at::Tensor& w, int64_t 
                   (int64_t)B * a.Ho * a.Wo * N < (1ll << 31) && dgrad_bt_enabled();
   if (!ok) {
     const at::Tensor wt = conv_weight_flip_t(w, 1, 0, 0, 1);
-    return conv2d_mfma(dy, wt, c10::nullopt, 1, 1, tph, tpw, 1, 1, 1.0, 1, ncv);
+    return conv2d_mfma(dy, wt, c10::nullopt, 1, 1, tph, tpw, 1, 1, 1.0, 1, ncv, c10::nullopt);
   }
   if (ncv < 0) ncv = N;
   IAMD_CHECK(ncv == N || (ncv > 0 && ncv < N && ncv % 8 == 0),
@@ -1429,6 +1791,7 @@ at::Tensor conv2d_dgrad_mfma(const at::Tensor& dy, const at::Tensor& w, int64_t 
   a.nk = KH * KW * a.cpt;
   a.slope = 1.f;
   a.oH = a.Ho; a.oW = a.Wo; a.osy = 1; a.osx = 1; a.ory = 0; a.orx = 0;
+  a.res = nullptr;
   run_v4(a, dy, true);
   return y;
 }

@@ -11,6 +11,9 @@
 //     partials in a fixed order (deterministic, no atomics);
 //   * backward: ONE launch writes every dL/da_t = w_t / n_t * sign(a_t - b_t) * dL in the
 //     feature dtype.
+// The targets b may be fp32 where the inputs a are bf16 (the fp32 real frames of the vid2vid /
+// MUNIT reconstruction L1s): the difference is then taken in fp32 on the unrounded target, as
+// autocast's fp32 l1_loss does.
 // Up to kMaxT pairs per launch travel in the kernel arguments (no device table).
 //
 // k13b: multi-tensor GAN loss  L = sum_t w_t * mean(phi_t(x_t))  over every discriminator
@@ -30,10 +33,10 @@ constexpr int kMaxT = 16;
 constexpr int kThreads = 256;
 constexpr int64_t kChunk = 256 * 8 * 8;  // elements per block (8 x 16-byte loads per thread)
 
-template <typename T>
+template <typename T, typename TB = T>
 struct L1Args {
   const T* a[kMaxT];
-  const T* b[kMaxT];
+  const TB* b[kMaxT];
   T* g[kMaxT];
   int64_t n[kMaxT];
   float scale[kMaxT];   // w_t / n_t
@@ -41,8 +44,8 @@ struct L1Args {
   int nt;
 };
 
-template <typename T>
-__device__ __forceinline__ int find_tensor(const L1Args<T>& p, int bid) {
+template <typename P>
+__device__ __forceinline__ int find_tensor(const P& p, int bid) {
   int t = 0;
 #pragma unroll
   for (int k = 1; k < kMaxT; ++k)
@@ -50,15 +53,15 @@ __device__ __forceinline__ int find_tensor(const L1Args<T>& p, int bid) {
   return t;
 }
 
-template <typename T>
-__global__ void __launch_bounds__(kThreads) l1_partials(const L1Args<T> p, float* __restrict__ part) {
+template <typename T, typename TB>
+__global__ void __launch_bounds__(kThreads) l1_partials(const L1Args<T, TB> p, float* __restrict__ part) {
   __shared__ float sh[kThreads / 64];
   const int bid = blockIdx.x;
   const int t = find_tensor(p, bid);
   const int64_t c0 = (int64_t)(bid - p.start[t]) * kChunk;
   const int64_t c1 = min(p.n[t], c0 + kChunk);
   const T* __restrict__ a = p.a[t];
-  const T* __restrict__ b = p.b[t];
+  const TB* __restrict__ b = p.b[t];
   float acc = 0.f;
   const bool vec = (((uintptr_t)a | (uintptr_t)b) % 16 == 0);
   if (vec) {
@@ -66,15 +69,15 @@ __global__ void __launch_bounds__(kThreads) l1_partials(const L1Args<T> p, float
     for (; i + 7 < c1; i += kThreads * 8) {
       float va[8], vb[8];
       load_vec<T, 8>(a + i, va);
-      load_vec<T, 8>(b + i, vb);
+      load_vec<TB, 8>(b + i, vb);
 #pragma unroll
       for (int k = 0; k < 8; ++k) acc += fabsf(va[k] - vb[k]);
     }
     // tail of a tensor whose size is not a multiple of 8
     const int64_t tail = c0 + ((c1 - c0) / 8) * 8;
-    for (int64_t j = tail + threadIdx.x; j < c1; j += kThreads) acc += fabsf(to_f<T>(a[j]) - to_f<T>(b[j]));
+    for (int64_t j = tail + threadIdx.x; j < c1; j += kThreads) acc += fabsf(to_f<T>(a[j]) - to_f<TB>(b[j]));
   } else {
-    for (int64_t j = c0 + threadIdx.x; j < c1; j += kThreads) acc += fabsf(to_f<T>(a[j]) - to_f<T>(b[j]));
+    for (int64_t j = c0 + threadIdx.x; j < c1; j += kThreads) acc += fabsf(to_f<T>(a[j]) - to_f<TB>(b[j]));
   }
   acc = wave_sum(acc);
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
@@ -104,14 +107,14 @@ __global__ void __launch_bounds__(1024) sum_fixed(const float* __restrict__ part
   }
 }
 
-template <typename T>
-__global__ void __launch_bounds__(kThreads) l1_grad(const L1Args<T> p, const float* __restrict__ gout) {
+template <typename T, typename TB>
+__global__ void __launch_bounds__(kThreads) l1_grad(const L1Args<T, TB> p, const float* __restrict__ gout) {
   const int bid = blockIdx.x;
   const int t = find_tensor(p, bid);
   const int64_t c0 = (int64_t)(bid - p.start[t]) * kChunk;
   const int64_t c1 = min(p.n[t], c0 + kChunk);
   const T* __restrict__ a = p.a[t];
-  const T* __restrict__ b = p.b[t];
+  const TB* __restrict__ b = p.b[t];
   T* __restrict__ g = p.g[t];
   const float s = p.scale[t] * gout[0];
   auto sgn = [](float d) { return d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f); };
@@ -121,7 +124,7 @@ __global__ void __launch_bounds__(kThreads) l1_grad(const L1Args<T> p, const flo
     for (int64_t i = c0 + threadIdx.x * 8; i + 7 < c1; i += kThreads * 8) {
       float va[8], vb[8], o[8];
       load_vec<T, 8>(a + i, va);
-      load_vec<T, 8>(b + i, vb);
+      load_vec<TB, 8>(b + i, vb);
 #pragma unroll
       for (int k = 0; k < 8; ++k) o[k] = s * sgn(va[k] - vb[k]);
       store_vec<T, 8>(g + i, o);
@@ -129,7 +132,7 @@ __global__ void __launch_bounds__(kThreads) l1_grad(const L1Args<T> p, const flo
     j0 = c0 + ((c1 - c0) / 8) * 8;
   }
   for (int64_t j = j0 + threadIdx.x; j < c1; j += kThreads)
-    g[j] = from_f<T>(s * sgn(to_f<T>(a[j]) - to_f<T>(b[j])));
+    g[j] = from_f<T>(s * sgn(to_f<T>(a[j]) - to_f<TB>(b[j])));
 }
 
 template <typename T>
@@ -253,23 +256,24 @@ void check_gan(const std::vector<at::Tensor>& xs, const std::vector<int64_t>& ki
   }
 }
 
-template <typename T>
-L1Args<T> make_args(const std::vector<at::Tensor>& a, const std::vector<at::Tensor>& b,
-                    const std::vector<double>& w, int& nblocks) {
-  L1Args<T> p;
+template <typename T, typename TB>
+L1Args<T, TB> make_args(const std::vector<at::Tensor>& a, const std::vector<at::Tensor>& b,
+                        const std::vector<double>& w, int& nblocks) {
+  L1Args<T, TB> p;
   p.nt = (int)a.size();
   int blocks = 0;
   for (int t = 0; t < kMaxT; ++t) {
     p.start[t] = blocks;
     if (t < p.nt) {
       p.a[t] = reinterpret_cast<const T*>(a[t].data_ptr());
-      p.b[t] = reinterpret_cast<const T*>(b[t].data_ptr());
+      p.b[t] = reinterpret_cast<const TB*>(b[t].data_ptr());
       p.g[t] = nullptr;
       p.n[t] = a[t].numel();
       p.scale[t] = (float)(w[t] / (double)std::max<int64_t>(1, a[t].numel()));
       blocks += (int)((p.n[t] + kChunk - 1) / kChunk);
     } else {
-      p.a[t] = p.b[t] = nullptr;
+      p.a[t] = nullptr;
+      p.b[t] = nullptr;
       p.g[t] = nullptr;
       p.n[t] = 0;
       p.scale[t] = 0.f;
@@ -285,11 +289,13 @@ void check_pairs(const std::vector<at::Tensor>& a, const std::vector<at::Tensor>
   IAMD_CHECK(!a.empty() && a.size() == b.size() && a.size() == w.size(),
              "mt_l1_loss: list sizes differ");
   IAMD_CHECK((int)a.size() <= kMaxT, "mt_l1_loss: at most ", kMaxT, " pairs per call");
-  const auto dt = a[0].scalar_type();
+  const auto dt = a[0].scalar_type(), dtb = b[0].scalar_type();
   IAMD_CHECK(dt == at::kBFloat16 || dt == at::kFloat, "mt_l1_loss: bf16 or fp32 tensors");
+  IAMD_CHECK(dtb == dt || dtb == at::kFloat, "mt_l1_loss: targets of the inputs' dtype or fp32");
   for (size_t t = 0; t < a.size(); ++t) {
-    IAMD_CHECK(a[t].is_cuda() && a[t].scalar_type() == dt && b[t].scalar_type() == dt,
-               "mt_l1_loss: CUDA tensors of one dtype expected");
+    IAMD_CHECK(a[t].is_cuda() && b[t].is_cuda() && a[t].scalar_type() == dt &&
+                   b[t].scalar_type() == dtb,
+               "mt_l1_loss: CUDA tensors, one input dtype and one target dtype expected");
     IAMD_CHECK(a[t].sizes() == b[t].sizes() && a[t].strides() == b[t].strides() &&
                    a[t].is_non_overlapping_and_dense(),
                "mt_l1_loss: pair ", t, " must be dense tensors of identical layout");
@@ -303,17 +309,20 @@ at::Tensor mt_l1_loss(const std::vector<at::Tensor>& a, const std::vector<at::Te
   check_pairs(a, b, w);
   auto out = at::empty({}, a[0].options().dtype(at::kFloat));
   int nb = 0;
-  auto launch = [&](auto tag) {
+  auto launch = [&](auto tag, auto tagb) {
     using T = decltype(tag);
-    auto p = make_args<T>(a, b, w, nb);
+    using TB = decltype(tagb);
+    auto p = make_args<T, TB>(a, b, w, nb);
     auto part = at::empty({std::max(nb, 1)}, a[0].options().dtype(at::kFloat));
     if (nb > 0)
-      hipLaunchKernelGGL((l1_partials<T>), dim3(nb), dim3(kThreads), 0, stream(), p,
+      hipLaunchKernelGGL((l1_partials<T, TB>), dim3(nb), dim3(kThreads), 0, stream(), p,
                          part.data_ptr<float>());
     hipLaunchKernelGGL(sum_fixed, dim3(1), dim3(1024), 0, stream(), part.data_ptr<float>(), nb,
                        out.data_ptr<float>());
   };
-  if (a[0].scalar_type() == at::kBFloat16) launch(__hip_bfloat16()); else launch(float());
+  if (a[0].scalar_type() == at::kFloat) launch(float(), float());
+  else if (b[0].scalar_type() == at::kFloat) launch(__hip_bfloat16(), float());
+  else launch(__hip_bfloat16(), __hip_bfloat16());
   IAMD_LAUNCH_CHECK();
   return out;
 }
@@ -327,15 +336,18 @@ std::vector<at::Tensor> mt_l1_loss_backward(const std::vector<at::Tensor>& a,
   std::vector<at::Tensor> grads;
   for (auto& t : a) grads.push_back(at::empty_like(t));
   int nb = 0;
-  auto launch = [&](auto tag) {
+  auto launch = [&](auto tag, auto tagb) {
     using T = decltype(tag);
-    auto p = make_args<T>(a, b, w, nb);
+    using TB = decltype(tagb);
+    auto p = make_args<T, TB>(a, b, w, nb);
     for (size_t t = 0; t < a.size(); ++t) p.g[t] = reinterpret_cast<T*>(grads[t].data_ptr());
     if (nb > 0)
-      hipLaunchKernelGGL((l1_grad<T>), dim3(nb), dim3(kThreads), 0, stream(), p,
+      hipLaunchKernelGGL((l1_grad<T, TB>), dim3(nb), dim3(kThreads), 0, stream(), p,
                          g32.data_ptr<float>());
   };
-  if (a[0].scalar_type() == at::kBFloat16) launch(__hip_bfloat16()); else launch(float());
+  if (a[0].scalar_type() == at::kFloat) launch(float(), float());
+  else if (b[0].scalar_type() == at::kFloat) launch(__hip_bfloat16(), float());
+  else launch(__hip_bfloat16(), __hip_bfloat16());
   IAMD_LAUNCH_CHECK();
   return grads;
 }

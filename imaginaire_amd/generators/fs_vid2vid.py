@@ -30,6 +30,7 @@ from torch import nn
 
 from imaginaire_amd.layers import (Conv2dBlock, HyperConv2dBlock, HyperRes2dBlock, LinearBlock,
                                    Res2dBlock)
+from imaginaire_amd.ops.few_shot import softmax_pool
 from imaginaire_amd.model_utils.fs_vid2vid import (extract_valid_pose_labels, pick_image,
                                                    resample)
 from imaginaire_amd.utils.data import (get_paired_input_image_channel_number,
@@ -377,10 +378,15 @@ class WeightGenerator(nn.Module):
             if self.mul_ref_label:
                 x_label = getattr(self, 'ref_label_down_%d' % i)(x_label)
             if k > 1 and i == self.num_downsample_atn - 1:
-                x, atn, atn_vis = self.attention_module(x, label, ref_label)
+                # one fused attention for the image (and label) features: no B x KHW x HW
+                # matrix, the per-frame attention mass as a side output
+                feats = [x, x_label] if self.mul_ref_label else [x]
+                outs, atn_full = self.attention_module.fused(feats, label, ref_label)
+                x = outs[0]
                 if self.mul_ref_label:
-                    x_label, _, _ = self.attention_module(x_label, None, None, atn)
-                atn_sum = atn.reshape(label.shape[0], k, -1).sum(2)
+                    x_label = outs[1]
+                atn_vis = atn_full[-1:, 0:1]
+                atn_sum = atn_full.reshape(label.shape[0], k, -1).float().sum(2)
                 ref_idx = torch.argmax(atn_sum, dim=1)
         encoded_image_ref = [x]
         if self.mul_ref_label:
@@ -393,15 +399,9 @@ class WeightGenerator(nn.Module):
         if self.mul_ref_label:
             encoded_ref = []
             for conv, conv_label in zip(encoded_image_ref, encoded_ref_label):
-                b, c, h, w = conv.size()
-                if conv_label.is_cuda and conv_label.dtype == torch.bfloat16:
-                    with torch.autocast('cuda', enabled=False):  # bf16 I/O, fp32 accumulation
-                        conv_label = torch.softmax(conv_label, dim=1)
-                else:
-                    conv_label = torch.softmax(conv_label, dim=1)
-                # Σ_hw conv[b, c, hw] * softmax(label)[b, c', hw] as one batched GEMM
-                prod = torch.bmm(conv.reshape(b, c, h * w),
-                                 conv_label.reshape(b, c, h * w).transpose(1, 2))
+                # Σ_hw conv[b, c, hw] * softmax_c'(label)[b, c', hw]: k15 channel softmax +
+                # per-sample k11 MFMA GEMM (ops/few_shot.py)
+                prod = softmax_pool(conv, conv_label)
                 encoded_ref.append(prod.unsqueeze(-1))
         else:
             encoded_ref = encoded_image_ref
@@ -543,6 +543,48 @@ class AttentionModule(nn.Module):
         out = torch.bmm(feats, attention).reshape(b, c, h, w)
         atn_vis = attention.reshape(b, k, h * w, h * w).sum(2).reshape(b, k, h, w)
         return out, attention, atn_vis[-1:, 0:1]
+
+    def fused(self, features, label, ref_label):
+        """The attention of :meth:`forward` applied to every tensor of ``features`` (each
+        [B*K, C_i, H, W]) without materialising the B x KHW x HW attention matrix: one fused
+        scaled-dot-product attention (scale 1, softmax over the K*HW reference positions) whose
+        values are the features' channels plus K frame-indicator channels, so the same call
+        also returns, per query position, the attention mass on each reference frame (the
+        reference's ``attention.reshape(b, k, hw, hw).sum(2)``). Returns (outputs, atn_vis
+        [B, K, H, W])."""
+        import torch.nn.functional as F
+        bk, c, h, w = features[0].shape
+        k = self.initial_few_shot_K
+        b = bk // k
+        hw = h * w
+        atn_key = self.attention_encode(ref_label, 'atn_key')
+        atn_query = self.attention_encode(label, 'atn_query')
+        ck = atn_key.shape[1]
+        q = atn_query.reshape(b, ck, hw).transpose(1, 2)                       # [b, hw, ck]
+        key = atn_key.reshape(b, k, ck, hw).permute(0, 1, 3, 2).reshape(b, k * hw, ck)
+        vals = [f.reshape(b, k, f.shape[1], hw).permute(0, 1, 3, 2).reshape(b, k * hw, -1)
+                for f in features]
+        ind = torch.eye(k, device=q.device, dtype=vals[0].dtype).repeat_interleave(hw, 0)
+        vals.append(ind.unsqueeze(0).expand(b, -1, -1))
+        v = torch.cat(vals, 2)
+        # one head dim for q, k and v (zero columns change no dot product)
+        d = max(ck, v.shape[2])
+        d = (d + 7) // 8 * 8
+        q = F.pad(q, (0, d - ck))
+        key = F.pad(key, (0, d - ck))
+        v = F.pad(v, (0, d - v.shape[2]))
+        dt = torch.get_autocast_dtype('cuda') if q.is_cuda and torch.is_autocast_enabled('cuda') \
+            else q.dtype
+        with torch.autocast('cuda', enabled=False):
+            o = F.scaled_dot_product_attention(q.unsqueeze(1).to(dt), key.unsqueeze(1).to(dt),
+                                               v.unsqueeze(1).to(dt), scale=1.0).squeeze(1)
+        outs, off = [], 0
+        for f in features:
+            cf = f.shape[1]
+            outs.append(o[:, :, off:off + cf].transpose(1, 2).reshape(b, cf, h, w))
+            off += cf
+        atn_vis = o[:, :, off:off + k].transpose(1, 2).reshape(b, k, h, w)
+        return outs, atn_vis
 
     def attention_encode(self, img, net_name):
         x = getattr(self, net_name + '_first')(img)

@@ -95,7 +95,9 @@ class _BaseConvBlock(nn.Module):
         self.conditional = getattr(conv_layer, 'conditional', False) or \
             getattr(activation_norm_layer, 'conditional', False)
 
-    def forward(self, x, *cond_inputs, **kw_cond_inputs):
+    def forward(self, x, *cond_inputs, residual=None, **kw_cond_inputs):
+        """``residual``: added to the block's output (a residual block's shortcut). When the
+        block ends in a plain 2-D conv it lands in the k10 epilogue (ops/conv.py ``conv2d``)."""
         keys = list(self.layers.keys())
         i = 0
         n = len(keys)
@@ -124,14 +126,19 @@ class _BaseConvBlock(nn.Module):
                         i += 2
                         continue
             if name == 'conv' and _is_plain_conv2d(layer) and x.is_cuda:
+                last = i + 1 == n
                 x = nhwc_conv.conv2d(x, _plain_conv_weight(layer), layer.bias, layer.stride,
                                      layer.padding, layer.dilation, layer.groups,
-                                     layer.padding_mode)
+                                     layer.padding_mode, residual=residual if last else None)
+                if last:
+                    residual = None
             elif getattr(layer, 'conditional', False):
                 x = layer(x, *cond_inputs, **kw_cond_inputs)
             else:
                 x = layer(x)
             i += 1
+        if residual is not None:
+            x = x + residual
         return x
 
     def _get_conv_layer(self, in_channels, out_channels, kernel_size, stride, padding,

@@ -13,7 +13,7 @@ from imaginaire_amd.ops.resize import Upsample as NearestUpsample
 from torch.utils.checkpoint import checkpoint
 
 from .conv import (Conv1dBlock, Conv2dBlock, Conv3dBlock, HyperConv2dBlock, LinearBlock,
-                   MultiOutConv2dBlock, PartialConv2dBlock, PartialConv3dBlock)
+                   MultiOutConv2dBlock, PartialConv2dBlock, PartialConv3dBlock, _BaseConvBlock)
 
 
 class _BaseResBlock(nn.Module):
@@ -81,7 +81,29 @@ class _BaseResBlock(nn.Module):
         dx = self.conv_block_1(dx, *cond_inputs, **kw_cond_inputs)
         return dx
 
+    def _fused_shortcut_ok(self):
+        """The shortcut can be added inside conv_block_1 (its epilogue when it ends in a conv):
+        a plain conv block, and no noise layer in conv_block_1 / conv_block_s, whose random
+        draws would change order (the reference computes the branch before the shortcut)."""
+        ok = getattr(self, '_fuse_ok', None)
+        if ok is None:
+            ok = type(self.conv_block_1).forward is _BaseConvBlock.forward and \
+                'noise' not in self.conv_block_1.layers and \
+                not (self.learn_shortcut and 'noise' in getattr(self.conv_block_s, 'layers', {}))
+            self._fuse_ok = ok
+        return ok
+
     def forward(self, x, *cond_inputs, do_checkpoint=False, **kw_cond_inputs):
+        if not do_checkpoint and self._fused_shortcut_ok():
+            # x_shortcut + dx with the add in the epilogue of the branch's last conv (k10) when
+            # the branch ends in one (pre-activation 'NACNAC' blocks of SPADE / FUNIT / the
+            # residual discriminators): one full-tensor pass fewer per block
+            dx = self.conv_block_0(x, *cond_inputs, **kw_cond_inputs)
+            if self.learn_shortcut:
+                x_shortcut = self.conv_block_s(x, *cond_inputs, **kw_cond_inputs)
+            else:
+                x_shortcut = x
+            return self.conv_block_1(dx, *cond_inputs, residual=x_shortcut, **kw_cond_inputs)
         if do_checkpoint:
             dx = checkpoint(self.conv_blocks, x, *cond_inputs, use_reentrant=False,
                             **kw_cond_inputs)

@@ -292,6 +292,46 @@ def _flip_t(w):
     return w.flip(2, 3).transpose(0, 1).contiguous(memory_format=_CL)
 
 
+# flipped, transposed copies of conv weights for the stride-1 data gradient, made for many
+# layers in one launch (``register_dgrad_weights``: the spectral-norm group right after its
+# bf16 W / sigma launch) or cached for frozen weights (VGG in the perceptual loss):
+# data_ptr -> (weight, flipped). The entry holds the weight itself, so its storage cannot be
+# reused by another tensor while the entry lives.
+_WFLIP = {}
+_WFLIP_FROZEN = {}
+
+
+def register_dgrad_weights(weights, flipped, old_keys=()):
+    """Record ``flipped[i]`` as the dgrad weight of ``weights[i]``; drops ``old_keys`` first.
+    Returns the keys registered."""
+    for k in old_keys:
+        _WFLIP.pop(k, None)
+    keys = []
+    for w, f in zip(weights, flipped):
+        k = w.data_ptr()
+        _WFLIP[k] = (w, f)
+        keys.append(k)
+    return keys
+
+
+def _dgrad_weight(wb):
+    """The pre-flipped dgrad weight of ``wb`` (k10 bf16 weight), or None."""
+    ent = _WFLIP.get(wb.data_ptr())
+    if ent is not None and ent[0].shape == wb.shape and ent[0].stride() == wb.stride() and \
+            ent[0].dtype == wb.dtype:
+        return ent[1]
+    if isinstance(wb, torch.nn.Parameter) and not wb.requires_grad and \
+            wb.shape[0] % 8 == 0 and wb.shape[1] % 8 == 0:
+        key = (wb.data_ptr(), wb._version, tuple(wb.shape))
+        ent = _WFLIP_FROZEN.get(key)
+        if ent is None:
+            if len(_WFLIP_FROZEN) > 256:
+                _WFLIP_FROZEN.clear()
+            ent = _WFLIP_FROZEN[key] = (wb, _ext.ext().conv_weight_flip_t(wb, 1, 0, 0, 1))
+        return ent[1]
+    return None
+
+
 def _pad_rows(t, n):
     """Zero-pad dim 0 of a weight / bias to ``n`` rows."""
     if t is None or t.shape[0] == n:
@@ -347,7 +387,7 @@ class _MfmaConv2d(torch.autograd.Function):
     counts are zero-padded to multiples of 64 (input) / 64 (output) around the kernels."""
 
     @staticmethod
-    def forward(ctx, x, w, bias, stride, padding, dilation, slope):
+    def forward(ctx, x, w, bias, stride, padding, dilation, slope, res=None):
         cout, cin = w.shape[0], w.shape[1]
         cp, op = _round_up(cin, 64), _out_pad(cout)
         xb = _pad_channels(x, cp, torch.bfloat16)
@@ -355,13 +395,16 @@ class _MfmaConv2d(torch.autograd.Function):
         ho, wo = _out_hw(x.shape[2], x.shape[3], w.shape[2:], stride, padding, dilation)
         # Cout % 8 == 0: k10 stores only the real output channels (no crop copy after it)
         ncv = cout if (op != cout and cout % 8 == 0) else op
+        ctx.res_dtype = None if res is None else res.dtype
         with _Logged('fwd', 'k10', 2.0 * x.shape[0] * ho * wo * op * cp * w.shape[2] * w.shape[3],
                      _gemm_desc(xb, wb, stride, padding)):
             y = _ext.ext().conv2d_mfma(xb, wb, _pad_rows(bias, op), stride[0], stride[1],
                                        padding[0], padding[1], dilation[0], dilation[1],
-                                       float(slope), 1, ncv)
+                                       float(slope), 1, ncv, res)
         ctx.conf = (stride, padding, dilation, float(slope), cin, cout, x.dtype, w.dtype,
                     None if bias is None else bias.dtype, x.shape[1])
+        ctx.wflip = _dgrad_weight(wb) if (stride == (1, 1) and dilation == (1, 1) and
+                                          ctx.needs_input_grad[0]) else None
         # the output is needed only for a fused activation's mask: with slope 1 it is not
         # saved, so in-place ops on the conv output stay legal (as after a plain F.conv2d)
         ctx.save_for_backward(xb, wb, y if slope != 1.0 else None)
@@ -373,6 +416,7 @@ class _MfmaConv2d(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        dy_in = dy  # the residual's gradient (added after the activation: identity)
         xb, wb, y = ctx.saved_tensors
         stride, padding, dilation, slope, cin, cout, xdt, wdt, bdt, xc = ctx.conf
         need_x, need_w, need_b = ctx.needs_input_grad[:3]
@@ -400,11 +444,16 @@ class _MfmaConv2d(torch.autograd.Function):
             # dx keeps only the input's real channels when they are a multiple of 8
             ncv = xc if (cp != xc and xc % 8 == 0) else cp
             if stride == (1, 1) and dilation == (1, 1) and pt[0] >= 0 and pt[1] >= 0 and big:
-                # one flip_t pass of the weight, then the k10 routing (v4 for stride-1 3x3-5x5
-                # rows); IMAGINAIRE_AMD_DGRAD_BT=1 reads the forward weight transposed in-kernel
-                # instead (no copy, but a slower tile: csrc/conv_mfma.hip dgrad_bt_enabled)
+                # the flipped weight (made for the whole network in one launch, or cached for a
+                # frozen weight), else one flip_t pass of it here; then the k10 routing (v4 / v5
+                # for stride-1 3x3-5x5 rows). IMAGINAIRE_AMD_DGRAD_BT=1 reads the forward weight
+                # transposed in-kernel instead (csrc/conv_mfma.hip dgrad_bt_enabled)
                 with _Logged('dgrad', 'k10', fl, _gemm_desc(dy, wb.transpose(0, 1), (1, 1), pt)):
-                    dx = _ext.ext().conv2d_dgrad_mfma(dy, wb, padding[0], padding[1], ncv)
+                    if ctx.wflip is not None:
+                        dx = _ext.ext().conv2d_mfma(dy, ctx.wflip, None, 1, 1, pt[0], pt[1], 1,
+                                                    1, 1.0, 1, ncv)
+                    else:
+                        dx = _ext.ext().conv2d_dgrad_mfma(dy, wb, padding[0], padding[1], ncv)
             elif stride == (1, 1) and pt[0] >= 0 and pt[1] >= 0 and big:
                 wt = _flip_t(wb)
                 with _Logged('dgrad', 'k10', fl, _gemm_desc(dy, wt, (1, 1), pt)):
@@ -433,7 +482,10 @@ class _MfmaConv2d(torch.autograd.Function):
             dw = dw.to(wdt)
         if db is not None:
             db = db[:cout].to(bdt) if need_b else None
-        return dx, dw, db, None, None, None, None
+        dres = None
+        if ctx.res_dtype is not None and ctx.needs_input_grad[7]:
+            dres = dy_in if dy_in.dtype == ctx.res_dtype else dy_in.to(ctx.res_dtype)
+        return dx, dw, db, None, None, None, None, dres
 
 
 class _MfmaConvPerSample(torch.autograd.Function):
@@ -698,35 +750,81 @@ def routing_table():
             'deconv': {repr(k): v for k, v in _DECONV_CHOICE.items()}}
 
 
+def _pending_union():
+    """Every rank's pending tuning keys, agreed: [(kind, key, dtypes)] sorted by repr, the same
+    list on every rank. World size 1: the local keys. At world > 1 one fixed-size count
+    all-reduce runs on EVERY call (a rank with nothing pending must still take part, or the
+    ranks with new keys would wait in a collective it never joins), then the key lists are
+    all-gathered only when some rank has one. A rank may miss keys a peer saw (per-rank shapes:
+    the fs-vid2vid hand crops, ragged batches): the weight-gradient candidates are timed from the
+    key's shapes alone, so every rank times the union."""
+    import torch.distributed as dist
+    local = [('w', k, v) for k, v in _WGRAD_PENDING.items()] + \
+        [('d', k, None) for k in _DECONV_PENDING]
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+        return sorted(local, key=lambda e: repr(e[:2]))
+    dev = 'cpu' if dist.get_backend() == 'gloo' else torch.device('cuda',
+                                                                  torch.cuda.current_device())
+    n = torch.tensor([len(local)], dtype=torch.int64, device=dev)
+    dist.all_reduce(n, op=dist.ReduceOp.MAX)
+    if int(n.item()) == 0:
+        return []
+    gathered = [None] * dist.get_world_size()
+    dist.all_gather_object(gathered, [(kind, k, v) for kind, k, v in local])
+    union = {}
+    for lst in gathered:
+        for kind, k, v in lst:
+            union.setdefault((kind, k), v)
+    return sorted([(kind, k, v) for (kind, k), v in union.items()], key=lambda e: repr(e[:2]))
+
+
 def tune_pending():
-    """Resolve the per-shape kernel choices first seen since the last call (wgrad k11 vs MIOpen
-    under ``IMAGINAIRE_AMD_MFMA_WGRAD=auto``; FlowNet2 deconv k10 phases vs MIOpen): time each
-    candidate on scratch tensors of the recorded shapes and agree across ranks. Call it at the
-    same iteration on every rank, outside any forward / backward and outside graph capture."""
-    if not (_WGRAD_PENDING or _DECONV_PENDING) or torch.cuda.is_current_stream_capturing():
+    """Resolve the per-shape kernel choices first seen since the last call (wgrad k11 variants /
+    k11 vs MIOpen; FlowNet2 deconv k10 phases vs MIOpen): time each candidate on scratch tensors
+    of the recorded shapes and agree across ranks (:func:`_pending_union`, :func:`_agree`). Call
+    it at the same iteration on every rank, outside any forward / backward and outside graph
+    capture (every rank skips it while capturing)."""
+    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        return 0
+    import torch.distributed as dist
+    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    if not multi and not (_WGRAD_PENDING or _DECONV_PENDING):
+        return 0
+    entries = _pending_union()
+    if not entries:
         return 0
     times = {}
     dev = torch.device('cuda', torch.cuda.current_device())
     cl = torch.channels_last
-    for key, (dyt, xt, wt) in sorted(_WGRAD_PENDING.items(), key=lambda kv: repr(kv[0])):
-        dys, xs, ws, stride, padding, dilation, cout, cin, wdt = key
-        dy = torch.randn(dys, device=dev).to(dyt).contiguous(memory_format=cl)
-        xb = torch.randn(xs, device=dev).to(xt).contiguous(memory_format=cl)
-        wb = torch.randn(ws, device=dev).to(wt).contiguous(memory_format=cl)
-        k11, miopen = _wgrad_fns(dy, xb, wb, stride, padding, dilation, cout, cin, wdt)
-        cand = {}
-        if _MFMA_WGRAD != '1':
-            cand['miopen'] = _time_ms(miopen)
-        if len(_k11_variants(dy, xb, wb, stride, dilation)) > 1:
-            cand['k11'] = _time_ms(lambda: k11(1))
-            cand['k11v2'] = _time_ms(lambda: k11(2))
+    for kind, key, dts in entries:
+        if kind == 'w':
+            dyt, xt, wt = dts
+            dys, xs, ws, stride, padding, dilation, cout, cin, wdt = key
+            dy = torch.randn(dys, device=dev).to(dyt).contiguous(memory_format=cl)
+            xb = torch.randn(xs, device=dev).to(xt).contiguous(memory_format=cl)
+            wb = torch.randn(ws, device=dev).to(wt).contiguous(memory_format=cl)
+            k11, miopen = _wgrad_fns(dy, xb, wb, stride, padding, dilation, cout, cin, wdt)
+            cand = {}
+            if _MFMA_WGRAD != '1':
+                cand['miopen'] = _time_ms(miopen)
+            if len(_k11_variants(dy, xb, wb, stride, dilation)) > 1:
+                cand['k11'] = _time_ms(lambda: k11(1))
+                cand['k11v2'] = _time_ms(lambda: k11(2))
+            else:
+                cand['k11'] = _time_ms(k11)
+            times[('w',) + key] = cand
         else:
-            cand['k11'] = _time_ms(k11)
-        times[('w',) + key] = cand
-    for key, fns in sorted(_DECONV_PENDING.items(), key=lambda kv: repr(kv[0])):
-        times[('d',) + key] = {name: _time_ms(fn) for name, fn in fns().items()}
+            # a deconv key names its weight, which only the ranks that saw it hold: those time
+            # it, the others report 0 and the vote below averages over the ranks that timed
+            fns = _DECONV_PENDING.get(key)
+            cand = {'k10s': 0.0, 'miopen': 0.0, '#': 0.0}
+            if fns is not None:
+                cand = {name: _time_ms(fn) for name, fn in fns().items()}
+                cand['#'] = 1.0
+            times[('d',) + key] = cand
     times = _agree(times)
     for k, t in times.items():
+        t = {c: v for c, v in t.items() if c != '#'}
         choice = min(t, key=t.get)
         if k[0] == 'w':
             _WGRAD_CHOICE[k[1:]] = choice
@@ -786,8 +884,32 @@ def pad(x, pad_lrtb, mode):
     return F.pad(x, pad_lrtb, mode=mode)
 
 
+def _residual_fusible(res, x, weight, stride, padding, dilation):
+    """The k10 epilogue can add ``res`` (a bf16 packed-NHWC tensor shaped like the conv output,
+    whose channels k10 stores directly)."""
+    if res is None or not (torch.is_tensor(res) and res.is_cuda and res.dtype == torch.bfloat16
+                           and res.dim() == 4 and res.is_contiguous(memory_format=_CL)):
+        return False
+    cout = weight.shape[0]
+    op = _out_pad(cout)
+    ncv = cout if (op != cout and cout % 8 == 0) else op
+    ho, wo = _out_hw(x.shape[2], x.shape[3], weight.shape[2:], stride, padding, dilation)
+    return ncv == cout and tuple(res.shape) == (x.shape[0], cout, ho, wo)
+
+
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1,
-           padding_mode='zeros'):
+           padding_mode='zeros', residual=None):
+    """``F.conv2d`` (+ ``residual``, added to the output: on the k10 path inside its epilogue,
+    otherwise as a separate add)."""
+    if residual is not None:
+        st, pd, dl = _pair(stride), _pair(padding), _pair(dilation)
+        if groups == 1 and padding_mode in ('zeros', None) and x.is_cuda and x.dim() == 4:
+            w = _match_channels(x, weight)
+            if not tapsplit_eligible(x, w, st, pd, dl, groups) and \
+                    mfma_eligible(x, w, st, pd, dl, groups) and \
+                    _residual_fusible(residual, x, w, st, pd, dl):
+                return _MfmaConv2d.apply(x, w, bias, st, pd, dl, 1.0, residual)
+        return conv2d(x, weight, bias, stride, padding, dilation, groups, padding_mode) + residual
     if groups == 1:
         weight = _match_channels(x, weight)
     if padding_mode != 'zeros' and padding_mode is not None:
@@ -823,7 +945,9 @@ _DECONV_FORCE = os.environ.get('IMAGINAIRE_AMD_DECONV')  # 'k10s' / 'miopen': sk
 def deconv_eligible(x, weight, stride, padding, output_padding, groups, dilation):
     """The phase-convolution path of :func:`conv_transpose2d`: inference (no autograd graph),
     bf16, square stride 2-4, no dilation / output padding / groups, >= 16 channels each side
-    and an output map that is not tiny."""
+    and an output map that is not tiny — inside a captured graph (``_capturing``) any channel
+    count and map size (MIOpen's backward-data solvers never run in a graph: their workspace
+    zeroing is not captured)."""
     if not (x.is_cuda and x.dim() == 4 and weight.dim() == 4 and groups == 1 and
             _STRIDED_DGRAD and _mfma_enabled() and _ext.use_native(x)):
         return False
@@ -835,12 +959,13 @@ def deconv_eligible(x, weight, stride, padding, output_padding, groups, dilation
     if _compute_dtype(x, weight) != torch.bfloat16:
         return False
     cin, cout, kh, kw = weight.shape
-    if min(cin, cout) < 16 or kh < s[0] or kw < s[1] or not (
+    cap = _capturing()
+    if (min(cin, cout) < 16 and not cap) or kh < s[0] or kw < s[1] or not (
             0 <= padding[0] < kh and 0 <= padding[1] < kw):
         return False
     ho = (x.shape[2] - 1) * s[0] - 2 * padding[0] + kh
     wo = (x.shape[3] - 1) * s[1] - 2 * padding[1] + kw
-    return ho > 0 and wo > 0 and x.shape[0] * ho * wo >= _DECONV_MIN_PIX
+    return ho > 0 and wo > 0 and (cap or x.shape[0] * ho * wo >= _DECONV_MIN_PIX)
 
 
 def _deconv_phase_weights(weight, s, padding, cp, op):
@@ -898,7 +1023,7 @@ def conv_transpose2d(x, weight, bias=None, stride=1, padding=0, output_padding=0
         # times both at a rank-uniform point and agrees the choice across ranks (a per-rank
         # choice could give ranks different ground-truth flow at bf16 rounding level).
         key = (tuple(x.shape), tuple(weight.shape), st, pd)
-        choice = _DECONV_FORCE or _DECONV_CHOICE.get(key)
+        choice = 'k10s' if _capturing() else (_DECONV_FORCE or _DECONV_CHOICE.get(key))
         if choice is None:
             if key not in _DECONV_PENDING:
                 shapes = (tuple(x.shape), x.dtype, weight.detach(), bias, st, pd)

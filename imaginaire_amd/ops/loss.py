@@ -37,18 +37,21 @@ class _MultiL1(torch.autograd.Function):
 
 
 def _native_target(a, b):
-    """``b`` (detached) in ``a``'s dtype and memory layout for the k13 kernel, or None when the
-    pair stays on the PyTorch path. The targets of the feature-matching loss come from the real
-    branch of a discriminator that still tracks grad, and may differ in layout or dtype from the
-    fake features: re-laying them out is one pass, the fp32 ``l1_loss`` fallback was three
-    (fp32 copies of both operands + the difference; 1.4 GB per vid2vid recipe iteration)."""
+    """``b`` (detached) in ``a``'s memory layout for the k13 kernel, or None when the pair stays
+    on the PyTorch path. The targets of the feature-matching loss come from the real branch of a
+    discriminator that still tracks grad, and may differ in layout or dtype from the fake
+    features: re-laying them out is one pass, the fp32 ``l1_loss`` fallback was three (fp32
+    copies of both operands + the difference; 1.4 GB per vid2vid recipe iteration). An fp32
+    target of a bf16 input stays fp32 (the kernel reads it unrounded, as autocast's fp32
+    ``l1_loss`` does); other dtypes are cast to ``a``'s."""
     if not (a.is_cuda and _ext.use_native(a) and a.dtype in (torch.bfloat16, torch.float32) and
             a.shape == b.shape and _ext.is_dense(a) and b.is_cuda):
         return None
     b = b.detach()
-    if b.dtype == a.dtype and b.stride() == a.stride():
+    dt = torch.float32 if b.dtype == torch.float32 else a.dtype
+    if b.dtype == dt and b.stride() == a.stride():
         return b
-    return torch.empty_like(a).copy_(b)  # empty_like keeps a's (dense) strides
+    return torch.empty_like(a, dtype=dt).copy_(b)  # empty_like keeps a's (dense) strides
 
 
 def weighted_l1(as_, bs, weights):
@@ -58,8 +61,12 @@ def weighted_l1(as_, bs, weights):
     total = None
     tg = [_native_target(a, b) for a, b in zip(as_, bs)]
     native = [i for i in range(len(as_)) if tg[i] is not None]
-    for s in range(0, len(native), _MAX_PAIRS):
-        idx = native[s:s + _MAX_PAIRS]
+    # one launch per (input dtype, target dtype) class, at most _MAX_PAIRS pairs each
+    groups = {}
+    for i in native:
+        groups.setdefault((as_[i].dtype, tg[i].dtype), []).append(i)
+    chunks = [g[s:s + _MAX_PAIRS] for g in groups.values() for s in range(0, len(g), _MAX_PAIRS)]
+    for idx in chunks:
         args = []
         for i in idx:
             args += [as_[i], tg[i]]

@@ -228,6 +228,10 @@ class _SyncBwdJoin(torch.autograd.Function):
         DeferredSyncBwd.completed += 1
         dx = _ext.ext().norm_bwd_apply(x, dout, scale, shift, mean, rstd, k1, k2, k3,
                                        gamma_v, beta_v, slope)
+        # g is the norm's stride-0 zero placeholder plus whatever other consumers of x' sent
+        # back: add it unless it is exactly that placeholder (no extra pass in the usual case)
+        if g is not None and not (g.dim() == dx.dim() and all(st == 0 for st in g.stride())):
+            dx = dx + g
         return dx, None
 
 

@@ -8,7 +8,10 @@ poll, which is what makes a step holding collectives capturable into a hipGraph 
 capture those become graph dependencies.
 
 Enabled by ``IMAGINAIRE_AMD_NATIVE_COMM``: ``1`` always (RCCL groups), ``0`` never, ``auto``
-(default) when the step is graph-captured with collectives (``IMAGINAIRE_AMD_GRAPH=force``).
+(default) whenever hipGraph capture is not switched off (``IMAGINAIRE_AMD_GRAPH`` != ``0``):
+multi-rank training steps are captured by default (utils/cuda_graph.py). A new communicator is
+checked once with a rank-sum all-reduce; if that fails on any rank (agreed over the torch
+group), every rank falls back to the torch.distributed collectives together.
 """
 import os
 
@@ -23,7 +26,7 @@ _COMMS = {}
 def native_comm_wanted():
     mode = os.environ.get('IMAGINAIRE_AMD_NATIVE_COMM', 'auto')
     if mode == 'auto':
-        return os.environ.get('IMAGINAIRE_AMD_GRAPH', '1') == 'force'
+        return os.environ.get('IMAGINAIRE_AMD_GRAPH', '1') != '0'
     return mode == '1'
 
 
@@ -90,6 +93,28 @@ class NativeComm(object):
         return _Pending(ev)
 
 
+def _verified(group):
+    """A new :class:`NativeComm` of ``group`` after a rank-sum all-reduce check, or None on
+    every rank if it failed on any (the outcome is agreed over the torch group, so all ranks
+    take the same collective path)."""
+    comm, ok = None, 1
+    try:
+        comm = NativeComm(group)
+        t = torch.full((4,), float(comm.rank + 1), device='cuda')
+        comm.all_reduce(t, 'sum')
+        want = comm.world * (comm.world + 1) / 2.0
+        ok = int(bool(torch.all(t == want).item()))
+    except RuntimeError:
+        ok = 0
+    flag = torch.tensor([ok], dtype=torch.int32, device='cuda')
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    if int(flag.item()) == 1:
+        return comm
+    if dist.get_rank() == 0:
+        print('[rccl] native communicator check failed; using torch.distributed collectives')
+    return None
+
+
 def native_comm_for(group=None):
     """The cached :class:`NativeComm` of ``group`` when native collectives are wanted and
     possible (RCCL backend, HIP extension loaded), else None."""
@@ -98,7 +123,6 @@ def native_comm_for(group=None):
     if dist.get_backend(group) != 'nccl' or not _ext.available():
         return None
     key = id(group) if group is not None else None
-    c = _COMMS.get(key)
-    if c is None:
-        c = _COMMS[key] = NativeComm(group)
-    return c
+    if key not in _COMMS:
+        _COMMS[key] = _verified(group)
+    return _COMMS[key]

@@ -42,6 +42,12 @@ def amp_dtype_of(cfg, device):
 
 
 class BaseTrainer(object):
+    # True when every rank runs the same sequence of network calls each iteration (no
+    # data-dependent sub-networks): DDP then uses its rank-local unused-parameter mask (no host
+    # sync per backward) and the multi-rank step can be captured into a hipGraph
+    # (utils/trainer.py _find_unused_mode, utils/cuda_graph.py graph_supported)
+    rank_uniform_control_flow = False
+
     def __init__(self, cfg, net_G, net_D, opt_G, opt_D, sch_G, sch_D, train_data_loader,
                  val_data_loader):
         super().__init__()

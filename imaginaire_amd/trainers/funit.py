@@ -16,6 +16,8 @@ from imaginaire_amd.utils.distributed import is_master
 
 
 class Trainer(BaseTrainer):
+    rank_uniform_control_flow = True
+
     def _init_loss(self, cfg):
         self.criteria['gan'] = GANLoss(cfg.trainer.gan_mode)
         self.criteria['image_recon'] = L1Loss()

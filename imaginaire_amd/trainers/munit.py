@@ -28,6 +28,7 @@ class Trainer(BaseTrainer):
     # the D / G update (GP and consistency regularisation included) replays from a hipGraph
     # (tests/test_graph_families_gpu.py)
     graph_capturable = True
+    rank_uniform_control_flow = True
 
     def __init__(self, cfg, net_G, net_D, opt_G, opt_D, sch_G, sch_D, train_data_loader,
                  val_data_loader):

@@ -26,6 +26,7 @@ class Trainer(BaseTrainer):
     # the D -> G -> EMA iteration is device-only with fixed shapes: hipGraph-capturable
     # (utils/cuda_graph.py)
     graph_capturable = True
+    rank_uniform_control_flow = True
 
     def __init__(self, cfg, net_G, net_D, opt_G, opt_D, sch_G, sch_D, train_data_loader,
                  val_data_loader):

@@ -15,9 +15,17 @@ iteration is captured ONCE into a hipGraph (``torch.cuda.graph``) and replayed:
 * device tables that the multi-tensor kernels build on first use are uploaded after the
   capture (``flush_deferred_uploads``), never as copy nodes inside the graph.
 
-Single-process only by default: with ``world_size > 1`` the step contains RCCL
-collectives (DDP buckets, SyncBN) and host-side bucket bookkeeping, so the trainer keeps
-the eager path there (``IMAGINAIRE_AMD_GRAPH=force`` overrides).
+Multi-rank steps are captured too (the default since round 4), with their collectives: the
+DDP bucket all-reduces and sync-BN exchanges run on the native RCCL communicator
+(parallel/rccl.py: no torch Work objects for the watchdog to poll) and DDP uses its rank-local
+unused-parameter mask (no host sync in ``finish()``), which holds for the trainers that declare
+``rank_uniform_control_flow``. The others (the vid2vid family: data-dependent hand
+discriminator) keep the eager step at world > 1. Capture is rank-local (nothing executes while
+recording), so the ranks agree on its outcome afterwards: one all-reduce of a success flag and a
+batch-signature hash; if any rank failed, every rank runs eagerly. Both paths run the same
+kernels: the eager step also runs under :class:`graph_routing`. Batch structures must be
+rank-uniform (every rank captures / replays the same graph at the same iteration), as a
+``DistributedSampler`` with ``drop_last`` and the synthetic sources give.
 """
 import os
 import time
@@ -42,8 +50,55 @@ def graph_supported(trainer):
     if getattr(trainer.cfg.trainer, 'skip_nonfinite_steps', False):
         return False  # host-side decision per step
     if get_world_size() > 1 and mode != 'force':
-        return False
+        return multirank_capturable(trainer)
     return True
+
+
+def _capturable_wrapper(net):
+    """A network wrapper whose collectives can be recorded: the single-process wrapper, or the
+    bucketed DDP on the native RCCL communicator with the rank-local unused mask."""
+    from imaginaire_amd.parallel.ddp import DistributedDataParallel
+    if net is None:
+        return True
+    mod = getattr(net, 'module', None)
+    if isinstance(net, torch.nn.parallel.DistributedDataParallel):
+        return False
+    if isinstance(net, DistributedDataParallel):
+        return (not net._force) or (net.find_unused == 'local' and net._native is not None)
+    if mod is not None and mod is not net and isinstance(mod, torch.nn.Module) and \
+            isinstance(mod, (DistributedDataParallel, torch.nn.parallel.DistributedDataParallel)):
+        return _capturable_wrapper(mod)
+    return True
+
+
+def multirank_capturable(trainer):
+    """True when a world > 1 step of ``trainer`` can be captured: rank-uniform control flow and
+    every network wrapper on the native communicator with the local unused mask."""
+    if not getattr(trainer, 'rank_uniform_control_flow', False):
+        return False
+    return _capturable_wrapper(getattr(trainer, 'net_G', None)) and \
+        _capturable_wrapper(getattr(trainer, 'net_D', None))
+
+
+def _signature_hash(sig):
+    import hashlib
+    return int(hashlib.sha1(repr(sig).encode()).hexdigest()[:12], 16)
+
+
+def agree_capture(ok, sig_hash, group=None):
+    """Agree on a capture outcome across ranks: True only if every rank captured (``ok``) the
+    same batch structure (``sig_hash``). One all-reduce of [min ok, min hash, -max hash]
+    through the default group; world size 1: ``ok``."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return bool(ok)
+    dev = torch.device('cpu') if dist.get_backend(group) == 'gloo' else \
+        torch.device('cuda', torch.cuda.current_device())
+    h = float(sig_hash % (1 << 40))  # exact in float64
+    t = torch.tensor([1.0 if ok else 0.0, h, -h], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    t = t.cpu().tolist()
+    return t[0] == 1.0 and t[1] == -t[2]
 
 
 def _static_copy(dst, src):
@@ -127,8 +182,9 @@ class GraphedStep(object):
 
     One graph per batch structure (shapes / dtypes of the inputs): a new structure — the
     video trainers' growing sequence length, a ragged last batch — gets its own warm-up and
-    capture; the graphs share one memory pool. ``step_fn`` must be the steady-state
-    iteration for a given structure: no host synchronisation.
+    capture, and its own memory pool: graphs replayed in any order (A, B, A) never rewrite
+    each other's outputs (the trainers' loss dicts and images point into them). ``step_fn``
+    must be the steady-state iteration for a given structure: no host synchronisation.
     ``pre_replay`` / ``post_replay`` are host hooks run around every replay.
     """
 
@@ -148,7 +204,6 @@ class GraphedStep(object):
         self.failed = False
         self.capture_s = None
         self.stream = None
-        self.pool = None
         self._last = None
 
     # the most recently used entry (tests and bench scripts read .graph / .static)
@@ -184,7 +239,8 @@ class GraphedStep(object):
         if ent is None:
             if len(self.entries) >= self.MAX_GRAPHS:
                 return self.step_fn(data)  # structure churn: stay eager for new ones
-            ent = self.entries[sig] = {'graph': None, 'static': None, 'n_eager': 0}
+            ent = self.entries[sig] = {'graph': None, 'static': None, 'n_eager': 0,
+                                       'sig': sig, 'pool': None}
         self._last = ent
         if ent['graph'] is not None:
             _static_copy(ent['static'], data)
@@ -214,22 +270,31 @@ class GraphedStep(object):
         ent['static'] = _clone(data)
         saved = self.save_host() if self.save_host else None
         g = torch.cuda.CUDAGraph()
+        err = None
         try:
             st = self._side_stream()
-            if self.pool is None:
-                self.pool = torch.cuda.graph_pool_handle()
+            if ent['pool'] is None:
+                ent['pool'] = torch.cuda.graph_pool_handle()
             # thread-local capture mode: the RCCL process group's watchdog thread keeps polling
             # its work events while a (seconds-long) step is being captured; under the default
             # global mode those calls from another thread are refused and abort the process
-            with torch.cuda.graph(g, pool=self.pool, stream=st,
+            with torch.cuda.graph(g, pool=ent['pool'], stream=st,
                                   capture_error_mode='thread_local'), graph_routing():
                 self.step_fn(ent['static'])
         except Exception as e:  # noqa: BLE001 - any capture failure: stay eager
             if os.environ.get('IMAGINAIRE_AMD_GRAPH_DEBUG'):
                 raise
+            err = e
+        # every rank captured, or every rank runs eagerly (a rank replaying collectives its
+        # peers issue eagerly would still match them, but one that failed mid-capture must not
+        # leave the others replaying a graph it never recorded)
+        if not agree_capture(err is None, _signature_hash(ent['sig'])) and err is None:
+            err = RuntimeError('capture failed or differed on another rank')
+        if err is not None:
             print('[graph] capture of {} failed ({}: {}); running eagerly'.format(
-                self.name, type(e).__name__, str(e).splitlines()[0][:200]))
+                self.name, type(err).__name__, str(err).splitlines()[0][:200]))
             self.failed = True
+            g = None
             ent['static'] = None
             if self.restore_host:
                 self.restore_host(saved)
@@ -266,10 +331,13 @@ def make_trainer_step(trainer, warmup=None, enabled=True, force=False):
     from imaginaire_amd.ops.conv import tune_pending
 
     def step(data):
-        for _ in range(cfg.trainer.dis_step):
-            trainer.dis_update(data)
-        for _ in range(cfg.trainer.gen_step):
-            trainer.gen_update(data)
+        # the eager step routes its convs as the captured one does (graph_routing): multi-rank
+        # eager fallbacks and graph warm-ups run the same kernels as the replay
+        with graph_routing():
+            for _ in range(cfg.trainer.dis_step):
+                trainer.dis_update(data)
+            for _ in range(cfg.trainer.gen_step):
+                trainer.gen_update(data)
         # per-shape kernel choices first seen in this iteration are timed and agreed across
         # ranks here, between iterations (every rank runs the same iterations), never inside a
         # backward; no-op once every shape is known and during graph capture

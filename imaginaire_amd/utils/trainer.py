@@ -111,6 +111,22 @@ def _calculate_model_size(model):
     return sum(p.numel() for p in model.parameters() if p.requires_grad)
 
 
+def _find_unused_mode(cfg):
+    """DDP unused-parameter mode: ``trainer.ddp_find_unused`` when set, else 'local' for the
+    trainers whose iteration runs the same networks on every rank
+    (``Trainer.rank_uniform_control_flow``: SPADE, pix2pixHD, MUNIT, UNIT, FUNIT, COCO-FUNIT; no
+    host sync per backward, capturable) and 'global' for the rest (the vid2vid family's hand
+    discriminator runs only on batches with hand pixels)."""
+    mode = getattr(cfg.trainer, 'ddp_find_unused', None)
+    if mode in ('local', 'global'):
+        return mode
+    try:
+        cls = import_module(cfg.trainer.type).Trainer
+    except (ImportError, AttributeError):
+        return 'global'
+    return 'local' if getattr(cls, 'rank_uniform_control_flow', False) else 'global'
+
+
 def _wrap_model(cfg, model):
     # IMAGINAIRE_AMD_FORCE_DIST=1: the distributed wrappers (bucketed DDP, SyncBN exchanges)
     # also on a one-rank process group, e.g. to capture and test the collective path on one GPU
@@ -130,8 +146,7 @@ def _wrap_model(cfg, model):
                                        overlap=(ddp != 'apex'),
                                        broadcast_buffers=getattr(cfg.trainer,
                                                                  'ddp_broadcast_buffers', False),
-                                       find_unused=getattr(cfg.trainer, 'ddp_find_unused',
-                                                           'global'))
+                                       find_unused=_find_unused_mode(cfg))
     return WrappedModel(model)
 
 

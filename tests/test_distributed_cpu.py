@@ -256,3 +256,71 @@ def test_kernel_choice_agreed_across_ranks():
     assert res[0][1] == res[1][1]
     assert res[0][1][('w', (1, 2))] == 'miopen'  # 1+4 > 2+2
     assert res[0][1][('d', (3,))] == 'k10s'      # 5+1 = 6 == 3+3 -> min picks first (k10s)
+
+
+def _capture_agree_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from imaginaire_amd.utils.cuda_graph import agree_capture
+    out = {
+        'both_ok': agree_capture(True, 1234),
+        'one_failed': agree_capture(rank == 0, 1234),     # rank 1's capture raised
+        'sig_differs': agree_capture(True, 1234 + rank),  # ranks captured different batches
+        'none_ok': agree_capture(False, 7),
+    }
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_capture_outcome_agreed_across_ranks():
+    """Multi-rank hipGraph capture (utils/cuda_graph.py): every rank keeps its graph only if
+    every rank captured the same batch structure; one failed or different capture sends all
+    ranks to the eager step together."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_capture_agree_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda t: t[0])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for _, r in res:
+        assert r == {'both_ok': True, 'one_failed': False, 'sig_differs': False,
+                     'none_ok': False}, r
+
+
+def _pending_union_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from imaginaire_amd.ops import conv
+    # iteration 1: nothing pending anywhere -> both ranks still run the count exchange
+    first = conv._pending_union()
+    # iteration 2: only rank 1 saw a new weight-gradient shape (e.g. a per-rank hand crop)
+    if rank == 1:
+        key = ((2, 64, 8, 8), (2, 64, 8, 8), (64, 64, 3, 3), (1, 1), (1, 1), (1, 1), 64, 64,
+               torch.bfloat16)
+        conv._WGRAD_PENDING[key] = (torch.bfloat16, torch.bfloat16, torch.bfloat16)
+    second = conv._pending_union()
+    q.put((rank, first, [(k, key[0]) for k, key, _ in second]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_tune_pending_union_when_one_rank_has_keys():
+    """a rank with no pending kernel-choice keys must not skip the exchange a rank
+    with new keys enters; both ranks see the same union (and would time the same shapes)."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pending_union_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda t: t[0])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert res[0][1] == [] and res[1][1] == []
+    assert res[0][2] == res[1][2] == [('w', (2, 64, 8, 8))]

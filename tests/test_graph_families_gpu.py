@@ -85,16 +85,17 @@ def _losses(tr):
     return out
 
 
-def _case_worker(name, seq_len, q):
-    """Capture + replay vs eager for one family, in a fresh process (see the test)."""
+def _cases_worker(cases, q):
+    """Capture + replay vs eager for every family, all in ONE process (see the test)."""
     import faulthandler
     import sys
-    faulthandler.dump_traceback_later(170, exit=True, file=sys.__stderr__)
-    try:
-        q.put(('ok', _run_case(name, seq_len)))
-    except BaseException as e:  # noqa: BLE001 - reported to the parent
-        import traceback
-        q.put(('error', '%s: %s\n%s' % (type(e).__name__, e, traceback.format_exc())))
+    faulthandler.dump_traceback_later(170 * len(cases), exit=True, file=sys.__stderr__)
+    for name, seq_len in cases:
+        try:
+            q.put((name, 'ok', _run_case(name, seq_len)))
+        except BaseException as e:  # noqa: BLE001 - reported to the parent
+            import traceback
+            q.put((name, 'error', '%s: %s\n%s' % (type(e).__name__, e, traceback.format_exc())))
 
 
 def _run_case(name, seq_len):
@@ -139,26 +140,40 @@ def _run_case(name, seq_len):
             'le': le, 'bad': bad[:8], 'num': num, 'den': den}
 
 
+_CASES = [('munit', None), ('pix2pixHD', None), ('vid2vid_street', 3), ('fs_vid2vid_face', 2)]
+_RESULTS = {}
+
+
+def _results():
+    """Run every family case once, sequentially in one spawned process that shares its
+    allocator history across them (the setting in which round 3 saw fs-vid2vid's eager
+    iteration drift from its replay: FlowNet2's 2 -> 2 flow upsamplers ran MIOpen backward-data
+    solvers inside the graph, whose workspace zeroing the capture does not record; they now run
+    k10 phase convolutions)."""
+    if not _RESULTS:
+        import multiprocessing as mp
+        ctx = mp.get_context('spawn')
+        q = ctx.Queue()
+        proc = ctx.Process(target=_cases_worker, args=(_CASES, q))
+        proc.start()
+        try:
+            for _ in _CASES:
+                name, status, res = q.get(timeout=190)
+                _RESULTS[name] = (status, res)
+        finally:
+            proc.join(30)
+            if proc.is_alive():
+                proc.kill()
+    return _RESULTS
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize('name,seq_len', [('munit', None), ('pix2pixHD', None),
-                                          ('vid2vid_street', 3), ('fs_vid2vid_face', 2)])
+@pytest.mark.parametrize('name,seq_len', _CASES)
 def test_family_graph_replay_matches_eager(name, seq_len):
-    """Each case runs in a FRESH process (spawn): the comparison needs the eager run and the
-    replay to start from the same allocator history. In a process that had run other GPU tests
-    first, fs-vid2vid's eager iteration drifted from its replay by up to ~0.1 in the losses
-    while a fresh process gives bitwise-equal losses (open: scripts/probe/poison_probe.py with
-    IAMD_PROBE_ROUTING=1 looks for a kernel reading memory it never wrote)."""
-    import multiprocessing as mp
-    ctx = mp.get_context('spawn')
-    q = ctx.Queue()
-    proc = ctx.Process(target=_case_worker, args=(name, seq_len, q))
-    proc.start()
-    try:
-        status, res = q.get(timeout=190)
-    finally:
-        proc.join(30)
-        if proc.is_alive():
-            proc.kill()
+    """The replayed iteration equals the eager one from the same state: losses to 1e-3 and the
+    G update to 1e-2 relative L2 (every kernel on both paths is deterministic and routed
+    alike, so the two runs differ only where a kernel's reduction order differs)."""
+    status, res = _results()[name]
     assert status == 'ok', res
     assert res['capturable'], name + ' is not marked capturable'
     assert res['graphed'] and res['captured'], 'step was not captured'
@@ -168,9 +183,5 @@ def test_family_graph_replay_matches_eager(name, seq_len):
     assert lg.keys() == le.keys() and lg
     for k in le:
         assert lg[k] == lg[k], k  # finite
-        # the G-side adversarial terms read D right after its Adam step, whose first updates are
-        # ~lr * sign(grad): bf16-level differences in near-zero D gradients move them by up to
-        # ~0.05 while every other loss agrees to ~1e-3
-        tol = 1e-1 if k.startswith('G/GAN') else 3e-2
-        assert abs(lg[k] - le[k]) <= tol * max(1.0, abs(le[k])), (k, lg[k], le[k])
-    assert res['den'] > 0 and res['num'] <= 0.1 * res['den'], (res['num'], res['den'])
+        assert abs(lg[k] - le[k]) <= 1e-3 * max(1.0, abs(le[k])), (k, lg[k], le[k])
+    assert res['den'] > 0 and res['num'] <= 1e-4 * res['den'], (res['num'], res['den'])

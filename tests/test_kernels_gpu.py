@@ -1223,6 +1223,45 @@ def test_conv2d_mfma_v4_row_window(case):
 
 
 @pytest.mark.parametrize('case', [
+    # B, Cin, Cout, H, W, k, pad, ncv — k10 v5 (256 x 256 tile, 8 waves of 128 x 64)
+    (2, 128, 256, 8, 256, 5, 2, None),    # FULLROW: one 256-pixel segment per tile
+    (1, 128, 512, 6, 512, 3, 1, None),    # FULLROW, two tiles per row, two N tiles
+    (2, 192, 256, 8, 128, 5, 2, None),    # two 128-pixel rows per tile, 3 channel blocks
+    (1, 256, 256, 16, 64, 3, 1, None),    # four 64-pixel rows per tile
+    (2, 128, 256, 16, 32, 5, 2, None),    # eight 32-pixel rows per tile (window 320 rows)
+    (1, 1024, 256, 8, 32, 3, 1, None),    # split-K over filter rows (64 channel blocks)
+    (1, 128, 256, 12, 260, 5, 0, None),   # no padding: Wo = 256
+    (2, 128, 512, 8, 256, 5, 2, 264),     # stores 264 of 512 channels (ldy < Cout)
+])
+def test_conv2d_mfma_v5_tile(case):
+    """k10 v5 vs fp32 F.conv2d with bias and leaky-ReLU, and vs the v4 kernel."""
+    import os
+    from imaginaire_amd.ops import _ext
+    B, cin, cout, H, W, k, p, ncv = case
+    torch.manual_seed(18)
+    x = torch.randn(B, cin, H, W, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    w = (torch.randn(cout, cin, k, k, device='cuda') / (cin * k * k) ** 0.5).to(
+        torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    bias = torch.randn(cout, device='cuda')
+    ref = F.leaky_relu(F.conv2d(x.float(), w.float(), bias, 1, p), 0.2)
+    n = ncv if ncv is not None else -1
+    try:
+        os.environ['IMAGINAIRE_AMD_CONV_V'] = '5'
+        y5 = _ext.ext().conv2d_mfma(x, w, bias, 1, 1, p, p, 1, 1, 0.2, 1, n)
+        os.environ['IMAGINAIRE_AMD_CONV_V'] = '4'
+        y4 = _ext.ext().conv2d_mfma(x, w, bias, 1, 1, p, p, 1, 1, 0.2, 1, n)
+    finally:
+        os.environ.pop('IMAGINAIRE_AMD_CONV_V')
+    if ncv is not None:
+        ref = ref[:, :ncv]
+    assert y5.shape == ref.shape
+    scale = ref.abs().max().item()
+    assert (y5.float() - ref).abs().max().item() <= 1e-2 * scale
+    assert (y5.float() - y4.float()).abs().max().item() <= 1e-2 * scale
+
+
+@pytest.mark.parametrize('case', [
     # B, Cin, Cout, H, W, k, pad: the stride-1 data gradient from the forward weight
     (2, 128, 1024, 16, 256, 5, 2),   # SPADE gamma|beta dgrad: v4 transposed-weight path
     (1, 128, 512, 8, 64, 5, 2),      # four output rows per tile
@@ -1295,3 +1334,185 @@ def test_l1loss_module_native_matches_torch():
     t = b.float().requires_grad_(True)
     L1Loss()(a.detach().float(), t).backward()
     assert t.grad is not None
+
+
+def test_l1loss_fp32_target_stays_fp32():
+    """A bf16 input against an fp32 target (the vid2vid / MUNIT real frames) is compared in
+    fp32 on the unrounded target, as autocast's fp32 l1_loss does: values and the
+    input gradient match torch.nn.functional.l1_loss on (input.float(), target) exactly where
+    the bf16-rounded target would differ."""
+    from imaginaire_amd.losses import L1Loss
+    from imaginaire_amd.ops.loss import weighted_l1
+    torch.manual_seed(4)
+    a = torch.randn(2, 3, 64, 96, device='cuda').to(torch.bfloat16).requires_grad_(True)
+    # targets within one bf16 ulp of the inputs: rounding them to bf16 changes most signs
+    b = a.detach().float() + torch.randn(2, 3, 64, 96, device='cuda') * 1e-3
+    v = L1Loss()(a, b)
+    ar = a.detach().float().requires_grad_(True)
+    vr = torch.nn.functional.l1_loss(ar, b)
+    assert abs(float(v) - float(vr)) <= 1e-5 * max(1e-3, abs(float(vr)))
+    v.backward()
+    vr.backward()
+    assert torch.equal(a.grad.float().sign(), ar.grad.sign())
+    # mixed pair classes in one weighted_l1 call: one launch per (input, target) dtype class
+    c = torch.randn(2, 64, 8, 8, device='cuda').to(torch.bfloat16)
+    d = torch.randn(2, 64, 8, 8, device='cuda').to(torch.bfloat16)
+    tot = weighted_l1([a.detach(), c], [b, d], [1.0, 0.5])
+    ref = torch.nn.functional.l1_loss(a.detach().float(), b) + \
+        0.5 * torch.nn.functional.l1_loss(c.float(), d.float())
+    assert abs(float(tot) - float(ref)) <= 1e-5 * abs(float(ref))
+
+
+@pytest.mark.parametrize('case', [
+    # B, Cin, Cout, H, W, k, stride, pad — the routing classes the residual epilogue rides on
+    (2, 128, 256, 8, 256, 3, 1, 1),    # v5
+    (2, 128, 128, 8, 64, 3, 1, 1),     # v4
+    (2, 64, 128, 16, 32, 4, 2, 1),     # v1 (stride 2)
+    (1, 1024, 256, 8, 32, 3, 1, 1),    # v5 + split-K reduce
+    (2, 64, 96, 8, 16, 3, 1, 1),       # Cout 96: stored channels below the 128 padding
+])
+def test_conv2d_residual_epilogue(case):
+    """ops.conv.conv2d(..., residual=r) adds the shortcut inside the k10 epilogue (or split-K
+    reduce): value vs fp32 conv + r, and the gradients of x, w, b and r (r's is dy)."""
+    from imaginaire_amd.ops import conv as nhwc_conv
+    B, cin, cout, H, W, k, s, p = case
+    torch.manual_seed(19)
+    cl = torch.channels_last
+    x = torch.randn(B, cin, H, W, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=cl).requires_grad_(True)
+    w = (torch.randn(cout, cin, k, k, device='cuda') / (cin * k * k) ** 0.5).requires_grad_(True)
+    b = torch.randn(cout, device='cuda').requires_grad_(True)
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    r = torch.randn(B, cout, Ho, Wo, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=cl).requires_grad_(True)
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        y = nhwc_conv.conv2d(x, w, b, s, p, residual=r)
+    assert y.dtype == torch.bfloat16 and y.shape == (B, cout, Ho, Wo)
+    xr, wr, br, rr = [t.detach().float().requires_grad_(True) for t in (x, w, b, r)]
+    yr = F.conv2d(xr, wr, br, s, p) + rr
+    scale = yr.abs().max().item()
+    assert (y.float() - yr).abs().max().item() <= 1.5e-2 * scale
+    g = torch.randn_like(yr)
+    y.backward(g.to(torch.bfloat16))
+    yr.backward(g)
+    for got, ref, name in ((x.grad, xr.grad, 'x'), (w.grad, wr.grad, 'w'), (b.grad, br.grad, 'b'),
+                           (r.grad, rr.grad, 'r')):
+        e = (got.float() - ref).abs().max() / ref.abs().max()
+        assert e < 2e-2, (name, float(e))
+
+
+@pytest.mark.parametrize('c', [16, 32, 64, 128, 512, 1024, 4096])
+def test_channel_softmax_k15(c):
+    """k15 channel softmax (bf16 channels-last) vs fp32 torch.softmax(dim=1), forward and
+    backward."""
+    from imaginaire_amd.ops.few_shot import channel_softmax
+    torch.manual_seed(20)
+    x = (torch.randn(3, c, 9, 7, device='cuda') * 3).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last).requires_grad_(True)
+    y = channel_softmax(x)
+    xr = x.detach().float().requires_grad_(True)
+    yr = torch.softmax(xr, 1)
+    assert y.dtype == torch.bfloat16
+    assert (y.float() - yr).abs().max().item() <= 8e-3 * yr.abs().max().item()
+    g = torch.randn_like(yr)
+    y.backward(g.to(torch.bfloat16))
+    yr.backward(g)
+    e = (x.grad.float() - xr.grad).abs().max() / xr.grad.abs().max()
+    assert e < 2e-2, float(e)
+
+
+@pytest.mark.parametrize('shape', [(3, 32, 64, 128, 128), (2, 256, 256, 32, 32),
+                                   (3, 1024, 1024, 16, 16)])
+def test_softmax_pool_k15_k11(shape):
+    """Few-shot reference pooling, K = 1 (the faceForensics recipe): k15 softmax + per-sample
+    k11 GEMM (+ k10 backward) vs fp32 softmax + bmm, values and both input gradients."""
+    from imaginaire_amd.ops.few_shot import softmax_pool
+    B, c, c2, H, W = shape
+    torch.manual_seed(21)
+    cl = torch.channels_last
+    a = torch.randn(B, c, H, W, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=cl).requires_grad_(True)
+    s = torch.randn(B, c2, H, W, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=cl).requires_grad_(True)
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        p = softmax_pool(a, s)
+    ar, sr = a.detach().float().requires_grad_(True), s.detach().float().requires_grad_(True)
+    pr = torch.bmm(ar.reshape(B, c, H * W),
+                   torch.softmax(sr, 1).reshape(B, c2, H * W).transpose(1, 2))
+    assert p.shape == pr.shape
+    assert (p.float() - pr).abs().max().item() <= 1.5e-2 * pr.abs().max().item()
+    g = torch.randn_like(pr)
+    p.backward(g.to(p.dtype))
+    pr.backward(g)
+    for got, ref, n in ((a.grad, ar.grad, 'a'), (s.grad, sr.grad, 's')):
+        e = (got.float() - ref).abs().max() / ref.abs().max()
+        assert e < 3e-2, (n, float(e))
+
+
+def test_fused_few_shot_attention_k2_gpu():
+    """Few-shot attention, K = 2: the fused scaled-dot-product path (no B x KHW x HW matrix,
+    per-frame attention mass as value channels) under bf16 autocast vs the fp32 reference
+    formulation (energy, softmax over KHW, bmm, column sums), values and input gradients."""
+    import types
+    from imaginaire_amd.generators.fs_vid2vid import AttentionModule
+    from imaginaire_amd.layers import Conv2dBlock
+    torch.manual_seed(22)
+    k, b, c, h, w = 2, 2, 64, 16, 16
+    atn_cfg = types.SimpleNamespace(num_downsamples=1)
+    data_cfg = types.SimpleNamespace(initial_few_shot_K=k, num_input_channels=3)
+
+    def block(cin, cout, stride=1):
+        return Conv2dBlock(cin, cout, 3, stride, 1, nonlinearity='leakyrelu')
+    m = AttentionModule(atn_cfg, data_cfg, block, [32, c]).cuda()
+    cl = torch.channels_last
+    label = torch.randn(b, 3, 2 * h, 2 * w, device='cuda').contiguous(memory_format=cl)
+    ref_label = torch.randn(b * k, 3, 2 * h, 2 * w, device='cuda').contiguous(memory_format=cl)
+    x = torch.randn(b * k, c, h, w, device='cuda').requires_grad_(True)
+    out, atn, _ = m(x, label, ref_label)  # fp32 reference
+    vis_ref = atn.reshape(b, k, h * w, h * w).sum(2).reshape(b, k, h, w)
+    x2 = x.detach().clone().requires_grad_(True)
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        outs, vis = m.fused([x2], label, ref_label)
+    scale = out.abs().max().item()
+    assert (outs[0].float() - out).abs().max().item() <= 3e-2 * scale
+    assert (vis.float() - vis_ref).abs().max().item() <= 3e-2
+    g = torch.randn_like(out)
+    (gx,) = torch.autograd.grad((out * g).sum(), [x])
+    (gx2,) = torch.autograd.grad((outs[0].float() * g).sum(), [x2])
+    assert (gx2.float() - gx).abs().max() / gx.abs().max() < 5e-2
+
+
+def test_mt_conv_weight_flip_t_matches_single():
+    """The one-launch multi-tensor flip (views of one flat buffer and separate tensors) equals
+    conv_weight_flip_t per weight, bitwise; and a conv whose weight was registered with its
+    flip (the spectral-norm group path) gets the same data gradient as one flipping itself."""
+    from imaginaire_amd.ops import _ext
+    from imaginaire_amd.ops import conv as nhwc_conv
+    X = _ext.ext()
+    torch.manual_seed(23)
+    cl = torch.channels_last
+    shapes = [(128, 64, 3, 3), (64, 192, 5, 5), (256, 128, 1, 1), (72, 136, 3, 3)]
+    flat = torch.randn(sum(a * b * c * d for a, b, c, d in shapes) + 64, device='cuda').to(
+        torch.bfloat16)
+    ws, off = [], 0
+    for co, ci, kh, kw in shapes:
+        ws.append(flat[off:off + co * ci * kh * kw].view(co, kh, kw, ci).permute(0, 3, 1, 2))
+        off += co * ci * kh * kw
+    got = X.mt_conv_weight_flip_t(ws)
+    for w, g in zip(ws, got):
+        assert g.is_contiguous(memory_format=cl)
+        assert torch.equal(g, X.conv_weight_flip_t(w, 1, 0, 0, 1))
+    # registered flip vs the conv's own flip: same dx
+    x = torch.randn(2, 64, 16, 64, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=cl).requires_grad_(True)
+    w = ws[0].detach().clone().contiguous(memory_format=cl).requires_grad_(True)
+    g = torch.randn(2, 128, 16, 64, device='cuda').to(torch.bfloat16)
+    y = nhwc_conv.conv2d(x, w, None, 1, 1)
+    (dx0,) = torch.autograd.grad(y, [x], g)
+    keys = nhwc_conv.register_dgrad_weights([w], X.mt_conv_weight_flip_t([w.detach()]))
+    try:
+        y = nhwc_conv.conv2d(x, w, None, 1, 1)
+        (dx1,) = torch.autograd.grad(y, [x], g)
+    finally:
+        nhwc_conv.register_dgrad_weights([], [], keys)
+    assert torch.equal(dx0, dx1)

@@ -146,3 +146,19 @@ def test_vid2vid_iteration_hip_bf16_matches_eager_fp32(tmp_path):
     # sequence length 2: the flow network, previous-frame warping (k9) and the temporal
     # discriminator are active
     _compare(tmp_path, 'vid2vid_street.yaml', seq_len=2)
+
+
+def test_pix2pixhd_iteration_hip_bf16_matches_eager_fp32(tmp_path):
+    # 512-wide images with instance maps: the atomic-free instance-wise feature pooling
+    # (ops/segment.py), reflect padding kernels and the multi-scale PatchGAN
+    _compare(tmp_path, 'pix2pixHD.yaml',
+             overrides=[('data.train.augmentations.resize_h_w', '256, 512')])
+
+
+@pytest.mark.parametrize('k', [1, 2])
+def test_fs_vid2vid_iteration_hip_bf16_matches_eager_fp32(tmp_path, k):
+    # K = 1: the label-weighted reference pooling (k15 channel softmax + per-sample k11 GEMM);
+    # K = 2: plus the fused few-shot attention; hyper (per-sample) SPADE convs, FlowNet2 flow
+    # loss and the warped-reference path at sequence length 2
+    _compare(tmp_path, 'fs_vid2vid_face.yaml', seq_len=2,
+             overrides=[('data.initial_few_shot_K', k)])
