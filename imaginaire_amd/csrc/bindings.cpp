@@ -98,6 +98,8 @@ std::vector<at::Tensor> resample2d_backward(const at::Tensor& in1, const at::Ten
                                             const at::Tensor& dout, int64_t ks);
 // conv_mfma.hip (k10)
 at::Tensor channel_softmax_fwd(const at::Tensor& x);
+at::Tensor conv2d_dgrad_strided(const at::Tensor& dy, const at::Tensor& w, int64_t s, int64_t ph,
+                                int64_t pw, int64_t H, int64_t W, int64_t ncv);
 std::vector<at::Tensor> mt_conv_weight_flip_t(const std::vector<at::Tensor>& ws);
 at::Tensor channel_softmax_bwd(const at::Tensor& y, const at::Tensor& dy);
 at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
@@ -187,6 +189,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("channel_softmax_bwd", &iamd::channel_softmax_bwd, "k15 backward: y * (dy - sum(dy y))");
   m.def("mt_conv_weight_flip_t", &iamd::mt_conv_weight_flip_t,
         "flipped, transposed (dgrad) copies of many conv weights in one launch");
+  m.def("conv2d_dgrad_strided", &iamd::conv2d_dgrad_strided,
+        "strided-conv data gradient: all s*s phase convs in one k10 launch, stored in place",
+        py::arg("dy"), py::arg("w"), py::arg("s"), py::arg("ph"), py::arg("pw"), py::arg("H"),
+        py::arg("W"), py::arg("ncv") = -1);
   m.def("conv_tap_sum", &iamd::conv_tap_sum, "tap-split conv: sum of per-tap partials (+bias)");
   m.def("conv_tap_gather", &iamd::conv_tap_gather, "tap-split conv backward: dy -> per-tap dZ");
   m.def("conv_phase_scatter", &iamd::conv_phase_scatter,

@@ -114,8 +114,10 @@ __device__ __forceinline__ size_t out_row(const ConvArgs& a, int m) {
 // VAR (main-loop schedule experiment, IMAGINAIRE_AMD_CONV_VAR): 0 = per-32-k fragment reads
 // then MFMAs; 1 = same with s_setprio(1) around the MFMA cluster; 2 = all 64-k fragments read
 // up front, then 32 back-to-back MFMAs under s_setprio(1).
+// The v1 body: tile bid (already XCD-remapped) of split `split` of sample zb (of nz).
 template <int BM, int BN, bool HAS_BIAS, int VAR>
-__global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_fwd_mfma(ConvArgs a) {
+__device__ __forceinline__ void conv_v1_impl(const ConvArgs& a, int bid, int split, int zb,
+                                             int nz) {
   // The buffer-resource builtins have no host form; the host pass only needs the launch stub.
 #if defined(__HIP_DEVICE_COMPILE__)
   constexpr int kThreads = BM * 2;
@@ -131,7 +133,6 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_fwd_mfma(ConvA
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // SGPR: the DMA's LDS base (M0)
   const int wm = wid >> 1, wn = wid & 1;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int mt = bid / a.nNt, nt = bid - mt * a.nNt;
   const int m0 = mt * BM, n0 = nt * BN;
 
@@ -139,7 +140,6 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_fwd_mfma(ConvA
   // Buffer-resource loads straight into LDS: the per-lane 32-bit byte offset selects the
   // pixel row, the wave-uniform parts (tap, channel block, k-step) ride in SGPRs, and an
   // out-of-range offset (padding pixels, M tail) returns zeros from the buffer unit itself.
-  const int zb = blockIdx.z;  // sample of a batched (per-sample weight) launch
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<__hip_bfloat16*>(a.x + (size_t)zb * a.xbs), 0, a.xbytes, kBufCfg);
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
@@ -174,7 +174,7 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_fwd_mfma(ConvA
 
   // scalar (tap, channel block) cursor of the next k-step to stage, advanced incrementally
   // (a division per k-step costs ~2 SALU per MFMA: profiles/pmc_conv_r2_mi355x.txt)
-  const int ks0 = blockIdx.y * a.kps;
+  const int ks0 = split * a.kps;
   const int ks1 = min(a.nk, ks0 + a.kps);
   int cky, ckx, cc, ctap;
   {
@@ -277,7 +277,7 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_fwd_mfma(ConvA
   }
 
   if (a.part) {  // split-K: raw fp32 partials [S][nz][M][Cout], bias/act/bf16 in the reduce
-    float* o = a.part + ((size_t)blockIdx.y * gridDim.z + zb) * a.M * a.Cout;
+    float* o = a.part + ((size_t)split * nz + zb) * a.M * a.Cout;
 #pragma unroll
     for (int j = 0; j < NI; ++j)
 #pragma unroll
@@ -323,6 +323,27 @@ __global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_fwd_mfma(ConvA
     }
   }
 #endif  // __HIP_DEVICE_COMPILE__
+}
+
+template <int BM, int BN, bool HAS_BIAS, int VAR>
+__global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_fwd_mfma(ConvArgs a) {
+  conv_v1_impl<BM, BN, HAS_BIAS, VAR>(a, xcd_remap(blockIdx.x, gridDim.x), blockIdx.y,
+                                      blockIdx.z, gridDim.z);
+}
+
+// Up to four independent convs in one launch (blockIdx.z = conv): the s*s phase convolutions
+// of a strided data gradient, each storing straight into its parity sub-grid of dx (omode).
+struct ConvPhases {
+  ConvArgs a[4];
+  int tiles[4];
+};
+
+template <int BM, int BN>
+__global__ __launch_bounds__(BM * 2, BM == 128 ? 2 : 1) void conv_fwd_mfma_phases(ConvPhases p) {
+  const int z = blockIdx.z;
+  const int tiles = p.tiles[z];
+  if ((int)blockIdx.x >= tiles) return;
+  conv_v1_impl<BM, BN, false, 2>(p.a[z], xcd_remap(blockIdx.x, tiles), 0, 0, 1);
 }
 
 // ---- k10 v2: 256 x 128 tile, 8 waves, 3-stage LDS ring with one stage in flight across
@@ -1794,6 +1815,103 @@ at::Tensor conv2d_dgrad_mfma(const at::Tensor& dy, const at::Tensor& w, int64_t 
   a.res = nullptr;
   run_v4(a, dy, true);
   return y;
+}
+
+
+// Data gradient of a stride-s conv (s = 2..4, undilated; w [Cout, Cin, KH, KW] channels-last
+// bf16) as its s*s phase convolutions in ONE k10 launch (blockIdx.z = phase), each phase
+// storing straight into its parity sub-grid of dx: input row i = s q + r receives
+// sum_j dy[q + c - j] w[k0 + s j] (k0 = (r + p) mod s, c = (r + p - k0) / s), i.e. a J-tap
+// correlation of dy with the flipped phase sub-kernel at padding J - 1 - c (negative where the
+// phase starts inside dy). Replaces per phase one launch + one scatter pass
+// (ops/conv.py _strided_dgrad). ncv: channels of dx stored (<= Cin, multiple of 8).
+at::Tensor conv2d_dgrad_strided(const at::Tensor& dy, const at::Tensor& w, int64_t s, int64_t ph,
+                                int64_t pw, int64_t H, int64_t W, int64_t ncv) {
+  IAMD_CHECK(dy.is_cuda() && w.is_cuda() && dy.scalar_type() == at::kBFloat16 &&
+                 w.scalar_type() == at::kBFloat16 && dy.dim() == 4 && w.dim() == 4,
+             "conv2d_dgrad_strided: 4-D bf16 CUDA tensors expected");
+  IAMD_CHECK(dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                 w.is_contiguous(at::MemoryFormat::ChannelsLast),
+             "conv2d_dgrad_strided: packed channels-last operands expected");
+  const int B = (int)dy.size(0), K = (int)dy.size(1), Ho = (int)dy.size(2), Wo = (int)dy.size(3);
+  const int N = (int)w.size(1), KH = (int)w.size(2), KW = (int)w.size(3);
+  IAMD_CHECK(w.size(0) == K, "conv2d_dgrad_strided: dy channels != weight rows");
+  IAMD_CHECK(s >= 2 && s <= 4 && K % kBK == 0 && N % 64 == 0 && KH >= s && KW >= s &&
+                 ph >= 0 && pw >= 0 && ph < KH && pw < KW,
+             "conv2d_dgrad_strided: unsupported geometry");
+  IAMD_CHECK(Ho == (H + 2 * ph - KH) / s + 1 && Wo == (W + 2 * pw - KW) / s + 1,
+             "conv2d_dgrad_strided: dy size does not match the conv geometry");
+  IAMD_CHECK((int64_t)B * Ho * Wo * K * 2 < kOobOffset && (int64_t)B * H * W * N < (1ll << 31),
+             "conv2d_dgrad_strided: tensors too large for 32-bit offsets");
+  if (ncv < 0) ncv = N;
+  IAMD_CHECK(ncv == N || (ncv > 0 && ncv < N && ncv % 8 == 0),
+             "conv2d_dgrad_strided: stored channels must be Cin or a multiple of 8 below it");
+  auto dx = at::empty({B, ncv, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  std::vector<ConvArgs> phases;
+  std::vector<at::Tensor> keep;
+  bool zero_fill = false;
+  const bool bn128 = N % 128 == 0;
+  const int BN = bn128 ? 128 : 64;
+  for (int ry = 0; ry < s; ++ry) {
+    for (int rx = 0; rx < s; ++rx) {
+      const int ky0 = (int)((ry + ph) % s), kx0 = (int)((rx + pw) % s);
+      const int jy = (int)((KH - ky0 + s - 1) / s), jx = (int)((KW - kx0 + s - 1) / s);
+      const int qy = (int)((H - ry + s - 1) / s), qx = (int)((W - rx + s - 1) / s);
+      if (jy <= 0 || jx <= 0 || qy <= 0 || qx <= 0) {
+        zero_fill = zero_fill || (qy > 0 && qx > 0);
+        continue;
+      }
+      const int cy = (int)((ry + ph - ky0) / s), cx = (int)((rx + pw - kx0) / s);
+      at::Tensor wt = conv_weight_flip_t(w, s, ky0, kx0, 1);  // [N, K, jy, jx]
+      keep.push_back(wt);
+      ConvArgs a;
+      a.x = reinterpret_cast<const __hip_bfloat16*>(dy.data_ptr());
+      a.w = reinterpret_cast<const __hip_bfloat16*>(wt.data_ptr());
+      a.bias = nullptr;
+      a.y = reinterpret_cast<__hip_bfloat16*>(dx.data_ptr());
+      a.res = nullptr;
+      a.xbytes = (int)(dy.numel() * 2);
+      a.wbytes = (int)(wt.numel() * 2);
+      a.H = Ho; a.W = Wo; a.Cin = K; a.Cout = N;
+      a.KH = jy; a.KW = jx; a.sh = a.sw = a.dh = a.dw = 1;
+      a.ph = jy - 1 - cy; a.pw = jx - 1 - cx;  // (may be negative: the phase starts inside dy)
+      a.Ho = qy; a.Wo = qx;
+      a.M = B * qy * qx;
+      a.cpt = K / kBK;
+      a.nk = jy * jx * a.cpt;
+      a.kps = a.nk;
+      a.nNt = N / BN;
+      a.part = nullptr;
+      a.slope = 1.f;
+      a.omode = 1; a.oH = (int)H; a.oW = (int)W; a.osy = (int)s; a.osx = (int)s;
+      a.ory = ry; a.orx = rx;
+      a.xbs = a.wbs = a.ybs = 0; a.bbs = 0; a.nz = 1;
+      a.ldy = (int)ncv;
+      phases.push_back(a);
+    }
+  }
+  if (zero_fill) dx.zero_();
+  // up to four phases per launch (the ConvPhases kernel argument; s = 3, 4 take several)
+  for (size_t p0 = 0; p0 < phases.size(); p0 += 4) {
+    ConvPhases P;
+    int np = 0, maxtiles = 0;
+    for (size_t i = p0; i < phases.size() && np < 4; ++i, ++np) {
+      P.a[np] = phases[i];
+      P.tiles[np] = ceil_div(P.a[np].M, 128) * P.a[np].nNt;
+      maxtiles = std::max(maxtiles, P.tiles[np]);
+    }
+    for (int i = np; i < 4; ++i) {
+      P.a[i] = phases[p0];
+      P.tiles[i] = 0;
+    }
+    const dim3 grid((unsigned)maxtiles, 1, (unsigned)np);
+    if (bn128)
+      hipLaunchKernelGGL((conv_fwd_mfma_phases<128, 128>), grid, dim3(256), 0, stream(), P);
+    else
+      hipLaunchKernelGGL((conv_fwd_mfma_phases<128, 64>), grid, dim3(256), 0, stream(), P);
+    IAMD_LAUNCH_CHECK();
+  }
+  return dx;  // (the phase weights are freed on this stream, after the kernel)
 }
 
 }  // namespace iamd

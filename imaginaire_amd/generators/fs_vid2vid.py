@@ -21,6 +21,7 @@ the reference-frame attention softmaxes its bf16 energy in place (no fp32 copy).
 (fs_vid2vid.py:903 vs 906) is fixed so K > 1 works.
 """
 import copy
+import os
 from functools import partial
 
 import numpy as np
@@ -37,6 +38,10 @@ from imaginaire_amd.utils.data import (get_paired_input_image_channel_number,
                                        get_paired_input_label_channel_number)
 from imaginaire_amd.utils.distributed import master_only_print as print
 from imaginaire_amd.utils.init_weight import weights_init
+
+# IMAGINAIRE_AMD_FUSED_ATTN=0: the reference formulation of the few-shot attention (energy
+# matrix, softmax over K*HW, bmm) instead of the fused scaled-dot-product path
+_FUSED_ATTN = os.environ.get('IMAGINAIRE_AMD_FUSED_ATTN', '1') == '1'
 from imaginaire_amd.utils.misc import get_and_setattr, get_nested_attr
 from imaginaire_amd.ops.resize import interpolate, Upsample
 
@@ -377,7 +382,13 @@ class WeightGenerator(nn.Module):
             x = getattr(self, 'ref_img_down_%d' % i)(x)
             if self.mul_ref_label:
                 x_label = getattr(self, 'ref_label_down_%d' % i)(x_label)
-            if k > 1 and i == self.num_downsample_atn - 1:
+            if k > 1 and i == self.num_downsample_atn - 1 and not _FUSED_ATTN:
+                x, atn, atn_vis = self.attention_module(x, label, ref_label)
+                if self.mul_ref_label:
+                    x_label, _, _ = self.attention_module(x_label, None, None, atn)
+                atn_sum = atn.reshape(label.shape[0], k, -1).sum(2)
+                ref_idx = torch.argmax(atn_sum, dim=1)
+            elif k > 1 and i == self.num_downsample_atn - 1:
                 # one fused attention for the image (and label) features: no B x KHW x HW
                 # matrix, the per-frame attention mass as a side output
                 feats = [x, x_label] if self.mul_ref_label else [x]

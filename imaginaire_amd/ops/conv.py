@@ -346,7 +346,10 @@ _STRIDED_DGRAD = os.environ.get('IMAGINAIRE_AMD_STRIDED_DGRAD', '1') == '1'
 _STRIDED_DGRAD_MIN_PIX = int(os.environ.get('IMAGINAIRE_AMD_STRIDED_DGRAD_MIN_PIX', 131072))
 
 
-def _strided_dgrad(dy, wb, H, W, s, padding, wts=None):
+_STRIDED_ONE_LAUNCH = os.environ.get('IMAGINAIRE_AMD_STRIDED_ONE_LAUNCH', '1') == '1'
+
+
+def _strided_dgrad(dy, wb, H, W, s, padding, wts=None, ncv=-1):
     """Data gradient of a stride-``s`` conv (weight ``wb`` [Cout, Cin, KH, KW], channels-last
     bf16) as s*s stride-1 phase convolutions on k10. Input row i = s*q + r receives
     dy[q + c0 - j] * w[kh0 + s*j] for kh0 = (r + p) mod s, c0 = (r + p - kh0) / s: a J-tap
@@ -357,6 +360,9 @@ def _strided_dgrad(dy, wb, H, W, s, padding, wts=None):
     cout, cin, kh, kw = wb.shape
     ho, wo = dy.shape[2], dy.shape[3]
     ph, pw = padding
+    if wts is None and _STRIDED_ONE_LAUNCH:
+        # every phase in one launch, stored straight into its parity sub-grid of dx
+        return X.conv2d_dgrad_strided(dy, wb, s, ph, pw, H, W, ncv)
     dx = None
     phases = []
     for ry in range(s):
@@ -380,6 +386,22 @@ def _strided_dgrad(dy, wb, H, W, s, padding, wts=None):
         out = X.conv2d_mfma(dy, wt, None, 1, 1, py, px, 1, 1, 1.0, 1)
         X.conv_phase_scatter(out, dx, s, ry, rx, cy - (jy - 1) + py, cx - (jx - 1) + px, qy, qx)
     return dx
+
+
+_OVERLAP_BWD = os.environ.get('IMAGINAIRE_AMD_CONV_BWD_OVERLAP', '1') == '1'
+_BWD_SIDE = {}
+
+
+def _bwd_side_stream():
+    """The per-device side stream of the conv backward's weight gradients (None when off, in
+    the conv log's timing mode, or under the eager reference path)."""
+    if not _OVERLAP_BWD or _CONV_LOG is not None:
+        return None
+    dev = torch.cuda.current_device()
+    st = _BWD_SIDE.get(dev)
+    if st is None:
+        st = _BWD_SIDE[dev] = torch.cuda.Stream(device=dev)
+    return st
 
 
 class _MfmaConv2d(torch.autograd.Function):
@@ -424,13 +446,26 @@ class _MfmaConv2d(torch.autograd.Function):
         # k10 stored only those, else the padded one), then dy is padded for the GEMMs; without
         # an activation / bias gradient that is ONE pad-cast pass from any dy layout
         db = None
-        if slope != 1.0 or need_b:
+        # the weight (and, without an activation, the bias) gradient runs on a side stream,
+        # concurrently with the data gradient: they are independent, and the small convs'
+        # grids leave most CUs idle on their own
+        side = _bwd_side_stream() if (need_x and (need_w or need_b)) else None
+        side_bias = side is not None and slope == 1.0 and need_b
+        if slope != 1.0 or (need_b and not side_bias):
             dy = _pad_channels(dy, y.shape[1] if y is not None else dy.shape[1], torch.bfloat16)
             # identity activation: the k2 kernel reads only dy (y stands in for the layout)
             dy, db = _ext.ext().bias_act_bwd(y if y is not None else dy, dy, slope)
         dy = _pad_channels(dy, wb.shape[0], torch.bfloat16)
         dx = dw = None
         cap = _capturing()
+        if side is not None:
+            main = torch.cuda.current_stream()
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                if side_bias:  # bias gradient only: the k2 kernel reads dy, writes no dx
+                    db = _ext.ext().bias_act_bwd(dy, dy, 1.0)[1]
+                if need_w:
+                    dw = _wgrad(dy, xb, wb, stride, padding, dilation, cout, cin, wdt)
         if need_x:
             kh, kw = wb.shape[2], wb.shape[3]
             pt = (dilation[0] * (kh - 1) - padding[0], dilation[1] * (kw - 1) - padding[1])
@@ -466,7 +501,8 @@ class _MfmaConv2d(torch.autograd.Function):
                 # large maps only: 1.3-1.6x MIOpen on the full-resolution PatchGAN layers, on par
                 # or slower below ~128K dx pixels (profiles/strided_dgrad_probe_mi355x.txt)
                 with _Logged('dgrad', 'k10s', fl, _gemm_desc(dy, wb, stride, padding)):
-                    dx = _strided_dgrad(dy, wb, xb.shape[2], xb.shape[3], stride[0], padding)
+                    dx = _strided_dgrad(dy, wb, xb.shape[2], xb.shape[3], stride[0], padding,
+                                        ncv=ncv)
             else:
                 with _Logged('dgrad', 'miopen', fl, _gemm_desc(dy, wb, stride, padding)):
                     dx = torch.ops.aten.convolution_backward(
@@ -475,8 +511,14 @@ class _MfmaConv2d(torch.autograd.Function):
             if dx.shape[1] != xc:
                 dx = dx[:, :xc]
             dx = dx.to(xdt)
+        if side is not None:
+            main.wait_stream(side)
+            for t in (dw, db):  # (allocated on the side stream, consumed on this one)
+                if t is not None:
+                    t.record_stream(main)
         if need_w:
-            dw = _wgrad(dy, xb, wb, stride, padding, dilation, cout, cin, wdt)
+            if side is None:
+                dw = _wgrad(dy, xb, wb, stride, padding, dilation, cout, cin, wdt)
             if dw.shape[0] != cout or dw.shape[1] != cin:
                 dw = dw[:cout, :cin]
             dw = dw.to(wdt)

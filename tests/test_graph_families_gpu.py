@@ -101,6 +101,10 @@ def _cases_worker(cases, q):
 def _run_case(name, seq_len):
     from imaginaire_amd.utils.cuda_graph import graph_routing, make_trainer_step
     torch.cuda.set_device(0)
+    # deterministic kernels on both paths: the flow-warp backward's image scatter (k9) uses
+    # float atomics in the default mode, so vid2vid's replay and eager run would otherwise differ
+    # in the last bits of the flow gradients and drift apart over the frames of a sequence
+    torch.use_deterministic_algorithms(True, warn_only=True)
     cfg, tr, batches = _build(name, seq_len)
     capturable = bool(getattr(tr, 'graph_capturable', False))
     step, graphed = make_trainer_step(tr, warmup=2, enabled=True)
@@ -121,6 +125,7 @@ def _run_case(name, seq_len):
     torch.cuda.synchronize()
     lg = _losses(tr)
     dg = [p.detach() - q for p, q in zip(gparams, p0)]
+    gg = [None if p.grad is None else p.grad.detach().float().clone() for p in gparams]
     with torch.no_grad():
         for t, c in zip(state, saved):
             t.copy_(c)
@@ -132,12 +137,15 @@ def _run_case(name, seq_len):
     torch.cuda.synchronize()
     le = _losses(tr)
     de = [p.detach() - q for p, q in zip(gparams, p0)]
+    ge = [None if p.grad is None else p.grad.detach().float() for p in gparams]
+    gnum = sum(float((x - y).pow(2).sum()) for x, y in zip(gg, ge) if x is not None)
+    gden = sum(float(y.pow(2).sum()) for x, y in zip(gg, ge) if x is not None)
     names = [n for n, _ in tr.net_G.named_parameters()]
     bad = [n for n, x in zip(names, dg) if not torch.isfinite(x).all()]
     num = sum(float((x - y).float().pow(2).sum()) for x, y in zip(dg, de))
     den = sum(float(y.float().pow(2).sum()) for y in de)
     return {'capturable': capturable, 'graphed': True, 'captured': captured, 'lg': lg,
-            'le': le, 'bad': bad[:8], 'num': num, 'den': den}
+            'le': le, 'bad': bad[:8], 'num': num, 'den': den, 'gnum': gnum, 'gden': gden}
 
 
 _CASES = [('munit', None), ('pix2pixHD', None), ('vid2vid_street', 3), ('fs_vid2vid_face', 2)]
@@ -171,9 +179,10 @@ def _results():
 @pytest.mark.parametrize('name,seq_len', _CASES)
 def test_family_graph_replay_matches_eager(name, seq_len):
     """The replayed iteration equals the eager one from the same state: losses to 1e-3 and the
-    G update to 1e-2 relative L2 (every kernel on both paths is deterministic and routed
-    alike, so the two runs differ only where a kernel's reduction order differs)."""
-    status, res = _results()[name]
+    G gradients to 1e-2 relative L2 (both paths run the same kernels). The G UPDATE is
+    compared more loosely: the first Adam steps move each weight by ~lr * sign(grad), so
+    rounding-level differences of near-zero gradients flip whole-size update elements."""
+    status, res = _results()[name]  # (run under torch.use_deterministic_algorithms)
     assert status == 'ok', res
     assert res['capturable'], name + ' is not marked capturable'
     assert res['graphed'] and res['captured'], 'step was not captured'
@@ -184,4 +193,5 @@ def test_family_graph_replay_matches_eager(name, seq_len):
     for k in le:
         assert lg[k] == lg[k], k  # finite
         assert abs(lg[k] - le[k]) <= 1e-3 * max(1.0, abs(le[k])), (k, lg[k], le[k])
-    assert res['den'] > 0 and res['num'] <= 1e-4 * res['den'], (res['num'], res['den'])
+    assert res['gden'] > 0 and res['gnum'] <= 1e-4 * res['gden'], (res['gnum'], res['gden'])
+    assert res['den'] > 0 and res['num'] <= 1e-2 * res['den'], (res['num'], res['den'])

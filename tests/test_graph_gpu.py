@@ -86,6 +86,7 @@ def test_graph_replay_matches_eager(tmp_path):
     torch.cuda.synchronize()
     lg = (float(tr.dis_losses['total']), float(tr.gen_losses['total']))
     dg = [p.detach() - q for p, q in zip(gparams, p0)]
+    gg = [None if p.grad is None else p.grad.detach().float().clone() for p in gparams]
     with torch.no_grad():
         for t, c in zip(state, saved):
             t.copy_(c)
@@ -94,12 +95,18 @@ def test_graph_replay_matches_eager(tmp_path):
     torch.cuda.synchronize()
     le = (float(tr.dis_losses['total']), float(tr.gen_losses['total']))
     de = [p.detach() - q for p, q in zip(gparams, p0)]
+    ge = [None if p.grad is None else p.grad.detach().float() for p in gparams]
     print('graph', lg, 'eager', le)
     assert abs(lg[0] - le[0]) <= 1e-3 * max(1.0, abs(le[0])), (lg, le)
     assert abs(lg[1] - le[1]) <= 1e-3 * max(1.0, abs(le[1])), (lg, le)
+    # gradients to 1e-2 relative L2; the Adam update (~lr * sign(grad) in the first steps, so
+    # rounding-level differences of near-zero gradients flip whole elements) to 1e-1
+    gnum = sum(float((x - y).pow(2).sum()) for x, y in zip(gg, ge) if x is not None)
+    gden = sum(float(y.pow(2).sum()) for x, y in zip(gg, ge) if x is not None)
+    assert gden > 0 and gnum <= 1e-4 * gden, (gnum, gden)
     num = sum(float((x - y).float().pow(2).sum()) for x, y in zip(dg, de))
     den = sum(float(y.float().pow(2).sum()) for y in de)
-    assert den > 0 and num <= 1e-4 * den, (num, den)  # relative L2 <= 1e-2
+    assert den > 0 and num <= 1e-2 * den, (num, den)
 
 
 @pytest.mark.gpu
@@ -197,6 +204,7 @@ def _dist_capture_worker(port, q, tmp):
     torch.cuda.synchronize()
     lg = (float(tr.dis_losses['total']), float(tr.gen_losses['total']))
     dg = [p.detach() - q for p, q in zip(gparams, p0)]
+    gg = [None if p.grad is None else p.grad.detach().float().clone() for p in gparams]
     with torch.no_grad():
         for t, c in zip(state, saved):
             t.copy_(c)
@@ -205,9 +213,12 @@ def _dist_capture_worker(port, q, tmp):
     torch.cuda.synchronize()
     le = (float(tr.dis_losses['total']), float(tr.gen_losses['total']))
     de = [p.detach() - q for p, q in zip(gparams, p0)]
+    ge = [None if p.grad is None else p.grad.detach().float() for p in gparams]
+    gnum = sum(float((x - y).pow(2).sum()) for x, y in zip(gg, ge) if x is not None)
+    gden = sum(float(y.pow(2).sum()) for x, y in zip(gg, ge) if x is not None)
     num = sum(float((x - y).float().pow(2).sum()) for x, y in zip(dg, de))
     den = sum(float(y.float().pow(2).sum()) for y in de)
-    q.put((captured, lg, le, num, den, deferred0, len(tr.net_G.buckets)))
+    q.put((captured, lg, le, num, den, deferred0, len(tr.net_G.buckets), gnum, gden))
     dist.destroy_process_group()
 
 
@@ -227,7 +238,7 @@ def test_graph_capture_with_rccl_collectives(tmp_path):
     p = ctx.Process(target=_dist_capture_worker, args=(port, q, str(tmp_path)))
     p.start()
     try:
-        captured, lg, le, num, den, deferred0, nb = q.get(timeout=175)
+        captured, lg, le, num, den, deferred0, nb, gnum, gden = q.get(timeout=175)
     finally:
         p.join(30)
         if p.is_alive():
@@ -238,7 +249,8 @@ def test_graph_capture_with_rccl_collectives(tmp_path):
     assert nb > 1
     assert abs(lg[0] - le[0]) <= 1e-3 * max(1.0, abs(le[0])), (lg, le)
     assert abs(lg[1] - le[1]) <= 1e-3 * max(1.0, abs(le[1])), (lg, le)
-    assert den > 0 and num <= 1e-4 * den, (num, den)  # relative L2 <= 1e-2
+    assert gden > 0 and gnum <= 1e-4 * gden, (gnum, gden)  # gradients: relative L2 <= 1e-2
+    assert den > 0 and num <= 1e-2 * den, (num, den)  # Adam update (sign-like): <= 1e-1
 
 
 def _native_comm_worker(port, q):

@@ -1516,3 +1516,34 @@ def test_mt_conv_weight_flip_t_matches_single():
     finally:
         nhwc_conv.register_dgrad_weights([], [], keys)
     assert torch.equal(dx0, dx1)
+
+
+@pytest.mark.parametrize('case', [
+    # B, Cin, Cout, H, W, k, stride, pad, ncv
+    (2, 128, 256, 32, 64, 4, 2, 1, None),   # PatchGAN 4x4 s2: four 2x2-tap phases
+    (2, 256, 512, 16, 32, 3, 2, 1, None),   # 3x3 s2: 2x2 / 2x1 / 1x2 / 1x1-tap phases
+    (1, 64, 128, 33, 17, 3, 2, 1, None),    # odd sizes: phases of different output sizes
+    (2, 96, 128, 16, 16, 4, 2, 1, 96),      # Cin 96: 96 of 128 padded channels stored
+    (1, 64, 64, 24, 24, 3, 3, 0, None),     # stride 3, no padding
+])
+def test_conv2d_dgrad_strided_one_launch(case):
+    """All s*s phase convs of a strided data gradient in one k10 launch, each storing into its
+    parity sub-grid of dx (negative phase padding where a phase starts inside dy) vs fp32
+    torch.nn.grad.conv2d_input."""
+    from imaginaire_amd.ops import _ext
+    B, cin, cout, H, W, k, s, p, ncv = case
+    torch.manual_seed(24)
+    cl = torch.channels_last
+    cp = (cin + 63) // 64 * 64
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = torch.randn(B, cout, Ho, Wo, device='cuda').to(torch.bfloat16).contiguous(memory_format=cl)
+    w = torch.zeros(cout, cp, k, k, device='cuda')
+    w[:, :cin] = torch.randn(cout, cin, k, k, device='cuda') / (cout * k * k / s / s) ** 0.5
+    w = w.to(torch.bfloat16).contiguous(memory_format=cl)
+    got = _ext.ext().conv2d_dgrad_strided(dy, w, s, p, p, H, W, -1 if ncv is None else ncv)
+    ref = torch.nn.grad.conv2d_input((B, cp, H, W), w.float(), dy.float(), s, p)
+    if ncv is not None:
+        ref = ref[:, :ncv]
+    assert got.shape == ref.shape
+    scale = ref.abs().max().item()
+    assert (got.float() - ref).abs().max().item() <= 1e-2 * scale
