@@ -1836,8 +1836,8 @@ at::Tensor conv2d_dgrad_strided(const at::Tensor& dy, const at::Tensor& w, int64
   const int B = (int)dy.size(0), K = (int)dy.size(1), Ho = (int)dy.size(2), Wo = (int)dy.size(3);
   const int N = (int)w.size(1), KH = (int)w.size(2), KW = (int)w.size(3);
   IAMD_CHECK(w.size(0) == K, "conv2d_dgrad_strided: dy channels != weight rows");
-  IAMD_CHECK(s >= 2 && s <= 4 && K % kBK == 0 && N % 64 == 0 && KH >= s && KW >= s &&
-                 ph >= 0 && pw >= 0 && ph < KH && pw < KW,
+  IAMD_CHECK(s >= 2 && s <= 4 && K % kBK == 0 && N % 64 == 0 && ph >= 0 && pw >= 0 &&
+                 ph < KH && pw < KW,
              "conv2d_dgrad_strided: unsupported geometry");
   IAMD_CHECK(Ho == (H + 2 * ph - KH) / s + 1 && Wo == (W + 2 * pw - KW) / s + 1,
              "conv2d_dgrad_strided: dy size does not match the conv geometry");

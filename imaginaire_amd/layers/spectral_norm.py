@@ -20,6 +20,8 @@ checkpoints interchange with the reference. Two changes in how it runs:
   again within the same network forward (weight sharing) falls back to its
   own power iteration — again the reference's behaviour.
 """
+import os
+
 import torch
 from torch.nn.utils.spectral_norm import (SpectralNorm as _TorchSN,
                                           SpectralNormLoadStateDictPreHook,
@@ -27,6 +29,9 @@ from torch.nn.utils.spectral_norm import (SpectralNorm as _TorchSN,
 import torch.nn.functional as F
 
 from imaginaire_amd.ops import _ext
+
+# IMAGINAIRE_AMD_SN_FLIP=0: each conv flips its own weight for the data gradient
+_SN_FLIP = os.environ.get('IMAGINAIRE_AMD_SN_FLIP', '1') == '1'
 
 
 class _SNScale(torch.autograd.Function):
@@ -167,7 +172,7 @@ class _SNGroup:
             v_all = torch.cat(vs)
             w16 = (_ext.ext().mt_sn_scale_cast(ws, sigma)
                    if _autocast_bf16(w0.device.type) else [None] * len(ws))
-        if w16[0] is not None and torch.is_grad_enabled() and net.training:
+        if w16[0] is not None and torch.is_grad_enabled() and net.training and _SN_FLIP:
             self._flip_for_dgrad(w16)
         ou = ov = 0
         for i, (m, h) in enumerate(self.entries):

@@ -360,7 +360,8 @@ def _strided_dgrad(dy, wb, H, W, s, padding, wts=None, ncv=-1):
     cout, cin, kh, kw = wb.shape
     ho, wo = dy.shape[2], dy.shape[3]
     ph, pw = padding
-    if wts is None and _STRIDED_ONE_LAUNCH:
+    if wts is None and _STRIDED_ONE_LAUNCH and cout % 64 == 0 and cin % 64 == 0 and \
+            0 <= ph < kh and 0 <= pw < kw:
         # every phase in one launch, stored straight into its parity sub-grid of dx
         return X.conv2d_dgrad_strided(dy, wb, s, ph, pw, H, W, ncv)
     dx = None
@@ -388,7 +389,10 @@ def _strided_dgrad(dy, wb, H, W, s, padding, wts=None, ncv=-1):
     return dx
 
 
-_OVERLAP_BWD = os.environ.get('IMAGINAIRE_AMD_CONV_BWD_OVERLAP', '1') == '1'
+# Off by default: the SPADE step ran 2% SLOWER with the weight / bias gradients on a side
+# stream (51.1-51.2 vs 52.2 images/s back to back, gpurun_out r4t) — the large dgrad and wgrad
+# grids each fill the chip, and sharing it costs both more than the launch gaps it hides.
+_OVERLAP_BWD = os.environ.get('IMAGINAIRE_AMD_CONV_BWD_OVERLAP', '0') == '1'
 _BWD_SIDE = {}
 
 
@@ -586,11 +590,14 @@ class _MfmaConvPerSample(torch.autograd.Function):
         return dx, dw, db, None, None
 
 
+_PER_SAMPLE = os.environ.get('IMAGINAIRE_AMD_PER_SAMPLE', '1') == '1'
+
+
 def per_sample_eligible(x, w, stride, groups):
     """k10/k11 batched path for HyperConv2d: bf16 compute, stride 1, groups 1, 4-D x and
     5-D per-sample weights, and enough pixels per sample to fill tiles."""
-    if not (x.is_cuda and x.dim() == 4 and w.dim() == 5 and groups == 1 and stride == 1 and
-            _mfma_enabled() and w.shape[0] == x.shape[0]):
+    if not (_PER_SAMPLE and x.is_cuda and x.dim() == 4 and w.dim() == 5 and groups == 1 and
+            stride == 1 and _mfma_enabled() and w.shape[0] == x.shape[0]):
         return False
     if _compute_dtype(x, w) != torch.bfloat16:
         return False
@@ -926,11 +933,15 @@ def pad(x, pad_lrtb, mode):
     return F.pad(x, pad_lrtb, mode=mode)
 
 
+_RESIDUAL_EPILOGUE = os.environ.get('IMAGINAIRE_AMD_CONV_RESIDUAL', '1') == '1'
+
+
 def _residual_fusible(res, x, weight, stride, padding, dilation):
     """The k10 epilogue can add ``res`` (a bf16 packed-NHWC tensor shaped like the conv output,
     whose channels k10 stores directly)."""
-    if res is None or not (torch.is_tensor(res) and res.is_cuda and res.dtype == torch.bfloat16
-                           and res.dim() == 4 and res.is_contiguous(memory_format=_CL)):
+    if res is None or not _RESIDUAL_EPILOGUE or not (
+            torch.is_tensor(res) and res.is_cuda and res.dtype == torch.bfloat16 and
+            res.dim() == 4 and res.is_contiguous(memory_format=_CL)):
         return False
     cout = weight.shape[0]
     op = _out_pad(cout)

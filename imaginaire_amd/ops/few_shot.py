@@ -13,9 +13,14 @@ a transposed operand. Here:
 
 CPU / unsupported inputs run the reference formulation.
 """
+import os
+
 import torch
 
 from imaginaire_amd.ops import _ext
+
+# IMAGINAIRE_AMD_FEW_SHOT_POOL=0: the reference formulation (softmax + bmm) everywhere
+_NATIVE_POOL = os.environ.get('IMAGINAIRE_AMD_FEW_SHOT_POOL', '1') == '1'
 
 _CL = torch.channels_last
 
@@ -93,7 +98,7 @@ class _SoftmaxPool(torch.autograd.Function):
 
 
 def _pool_native(a, s):
-    if not (a.is_cuda and a.dim() == 4 and s.dim() == 4 and _ext.use_native(a) and
+    if not (_NATIVE_POOL and a.is_cuda and a.dim() == 4 and s.dim() == 4 and _ext.use_native(a) and
             a.shape[0] == s.shape[0] and a.shape[2:] == s.shape[2:]):
         return False
     dt = torch.get_autocast_dtype('cuda') if torch.is_autocast_enabled('cuda') else a.dtype

@@ -19,6 +19,7 @@ name = sys.argv[1] if len(sys.argv) > 1 else 'pix2pixHD'
 seq = int(sys.argv[2]) if len(sys.argv) > 2 else None
 from imaginaire_amd.utils.cuda_graph import make_trainer_step  # noqa: E402
 torch.cuda.set_device(0)
+torch.use_deterministic_algorithms(True, warn_only=True)
 if os.environ.get('IAMD_PROBE_DET') == '1':  # MIOpen: deterministic (non-atomic) solvers
     torch.backends.cudnn.deterministic = True
 cfg, tr, batches = _build(name, seq)
@@ -36,7 +37,9 @@ for it in range(3):
     torch.cuda.synchronize()
     bad = [(n, p.shape) for n, p, q in zip(names, params, p0) if not torch.isfinite(p).all()]
     badg = [n for n, p in zip(names, params) if p.grad is not None and not torch.isfinite(p.grad).all()]
-    print('replay %d: non-finite params %d %s | non-finite grads %d %s' % (
-        it, len(bad), bad[:4], len(badg), badg[:4]), flush=True)
+    print('replay %d: non-finite params %d %s | non-finite grads %d' % (
+        it, len(bad), bad[:4], len(badg)), flush=True)
+    for n in badg:
+        print('    bad grad', n.replace('module.module.', ''))
     if bad:
         break

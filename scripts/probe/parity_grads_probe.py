@@ -19,11 +19,11 @@ def grads(config, amp, eager, seq_len, overrides):
     norms = {}
     orig = T._grad_norms
 
-    def capture(net):
+    def capture(net, *args):
         for n, p in net.named_parameters():
             if p.grad is not None:
                 norms[n] = float(p.grad.float().norm())
-        return orig(net)
+        return orig(net, *args)
     T._grad_norms = capture
     try:
         T._iteration(config, amp, eager, '/tmp/pgp_%d' % int(eager), seq_len=seq_len,

@@ -142,10 +142,11 @@ def _run_case(name, seq_len):
     gden = sum(float(y.pow(2).sum()) for x, y in zip(gg, ge) if x is not None)
     names = [n for n, _ in tr.net_G.named_parameters()]
     bad = [n for n, x in zip(names, dg) if not torch.isfinite(x).all()]
+    bad_eager = [n for n, x in zip(names, de) if not torch.isfinite(x).all()]
     num = sum(float((x - y).float().pow(2).sum()) for x, y in zip(dg, de))
     den = sum(float(y.float().pow(2).sum()) for y in de)
     return {'capturable': capturable, 'graphed': True, 'captured': captured, 'lg': lg,
-            'le': le, 'bad': bad[:8], 'num': num, 'den': den, 'gnum': gnum, 'gden': gden}
+            'le': le, 'bad': bad[:8], 'bad_eager': bad_eager[:8], 'num': num, 'den': den, 'gnum': gnum, 'gden': gden}
 
 
 _CASES = [('munit', None), ('pix2pixHD', None), ('vid2vid_street', 3), ('fs_vid2vid_face', 2)]
@@ -188,7 +189,8 @@ def test_family_graph_replay_matches_eager(name, seq_len):
     assert res['graphed'] and res['captured'], 'step was not captured'
     lg, le = res['lg'], res['le']
     print(name, 'graph', lg, '\n', name, 'eager', le)
-    assert not res['bad'], 'non-finite replayed G updates: %s' % res['bad']
+    assert not res['bad'], 'non-finite replayed G updates: %s (eager: %s; losses %s / %s)' % (
+        res['bad'], res['bad_eager'], lg, le)
     assert lg.keys() == le.keys() and lg
     for k in le:
         assert lg[k] == lg[k], k  # finite

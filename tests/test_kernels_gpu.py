@@ -864,6 +864,8 @@ def test_pad_nhwc(mode, dtype, pad):
     (3, 32, 48, 20, 24, 3, 1),     # odd channel counts -> padded to 64
     (2, 64, 128, 16, 32, 1, 0),
     (3, 128, 64, 16, 16, 3, 1),
+    (2, 64, 64, 16, 64, 3, 1),     # 64-pixel output rows: the multi-tap k11 shape class
+    (2, 64, 128, 8, 128, 5, 2),
 ])
 def test_conv2d_per_sample_batched(case):
     """Per-sample-weight (hyper) convolution as one batched k10 / k11 launch vs a loop of fp32
@@ -1525,6 +1527,9 @@ def test_mt_conv_weight_flip_t_matches_single():
     (1, 64, 128, 33, 17, 3, 2, 1, None),    # odd sizes: phases of different output sizes
     (2, 96, 128, 16, 16, 4, 2, 1, 96),      # Cin 96: 96 of 128 padded channels stored
     (1, 64, 64, 24, 24, 3, 3, 0, None),     # stride 3, no padding
+    (2, 128, 64, 32, 32, 1, 2, 0, None),    # 1x1 s2 shortcut: three phases get no taps
+    (1, 64, 128, 15, 20, 2, 4, 1, None),    # 2x2 s4: kernel smaller than the stride
+    (2, 16, 64, 128, 128, 3, 2, 1, 16),     # fs-vid2vid ref_img_down_0: 16 of 64 stored
 ])
 def test_conv2d_dgrad_strided_one_launch(case):
     """All s*s phase convs of a strided data gradient in one k10 launch, each storing into its
