@@ -130,6 +130,8 @@ void conv_phase_scatter(const at::Tensor& src, at::Tensor& dst, int64_t s, int64
                         int64_t i0, int64_t j0, int64_t Qy, int64_t Qx);
 at::Tensor conv_weight_flip_t(const at::Tensor& w, int64_t s, int64_t qy, int64_t qx,
                               int64_t nb);
+std::vector<at::Tensor> conv_weight_phase_flip(const at::Tensor& w, int64_t s);
+void lds_poison(int64_t blocks);
 at::Tensor pad_nhwc_fwd(const at::Tensor& x, int64_t pl, int64_t pr, int64_t pt, int64_t pb,
                         int64_t mode);
 at::Tensor pad_nhwc_bwd(const at::Tensor& dy, int64_t H, int64_t W, int64_t pl, int64_t pr,
@@ -207,6 +209,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "flipped, in/out-transposed channels-last conv weight (dgrad-as-conv); s/qy/qx select "
         "the taps of one stride-s phase; nb per-sample weights", py::arg("w"), py::arg("s") = 1,
         py::arg("qy") = 0, py::arg("qx") = 0, py::arg("nb") = 1);
+  m.def("lds_poison", &iamd::lds_poison,
+        "test support: fill every CU's LDS with NaN bits (finds reads of never-written LDS)",
+        py::arg("blocks") = 2048);
+  m.def("conv_weight_phase_flip", &iamd::conv_weight_phase_flip,
+        "all s*s phase weights conv_weight_flip_t(w, s, qy, qx) of a stride-s conv in one launch");
   m.def("sn_scale_backward", &iamd::sn_scale_backward, "spectral-norm W/sigma backward (k5d)");
   m.def("norm_stats", &iamd::norm_stats, "per-(group,channel) statistics (k1)",
         py::arg("x"), py::arg("per_instance"), py::arg("eps"), py::arg("weight"),

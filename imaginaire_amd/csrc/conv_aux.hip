@@ -21,6 +21,7 @@
 // (layers/conv.py:59-91); these kernels have no reference counterpart.
 #include "common.h"
 
+#include <array>
 #include <mutex>
 #include <unordered_map>
 
@@ -364,6 +365,96 @@ at::Tensor conv_weight_flip_t(const at::Tensor& w, int64_t s, int64_t qy, int64_
   return wt;
 }
 
+// Every phase sub-kernel of a stride-s conv weight in ONE launch (the strided data gradient's
+// s*s phase convolutions, conv_mfma.hip conv2d_dgrad_strided): original tap (ky, kx) belongs to
+// phase (ky mod s, kx mod s) at in-phase position ((ky - qy) / s, (kx - qx) / s), stored flipped
+// into that phase's [Cin][Jy][Jx][Cout] block of one flat buffer (block offsets poff[phase]).
+// Replaces s*s flip_t launches per strided conv (~85 small launches per SPADE step).
+namespace {
+struct PhaseOffsets {
+  int64_t off[16];
+};
+
+__global__ void __launch_bounds__(kT)
+phase_flip_kernel(const __hip_bfloat16* __restrict__ w, __hip_bfloat16* __restrict__ out,
+                  int Cout, int Cin, int KH, int KW, int s, PhaseOffsets po) {
+  __shared__ __hip_bfloat16 tile[kTile * kLdsStride];
+  const int ci0 = blockIdx.x * kTile, co0 = blockIdx.y * kTile;
+  const int ky = blockIdx.z / KW, kx = blockIdx.z - (blockIdx.z / KW) * KW;
+  const int qy = ky % s, qx = kx % s;
+  const int Jy = (KH - qy + s - 1) / s, Jx = (KW - qx + s - 1) / s;
+  const int jy = Jy - 1 - (ky - qy) / s, jx = Jx - 1 - (kx - qx) / s;
+  const int JJ = Jy * Jx, tap = jy * Jx + jx;
+  __hip_bfloat16* wt = out + po.off[qy * s + qx];
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int e = tid + r * kT;
+    const int row = e >> 3, ch = e & 7;
+    const int co = co0 + row, ci = ci0 + ch * 8;
+    Pack<__hip_bfloat16, 8> v;
+    if (co < Cout && ci < Cin) {
+      v = *reinterpret_cast<const Pack<__hip_bfloat16, 8>*>(
+          w + ((int64_t)co * KH * KW + blockIdx.z) * Cin + ci);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v.v[k] = __float2bfloat16(0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) tile[row * kLdsStride + ch * 8 + k] = v.v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int e = tid + r * kT;
+    const int row = e >> 3, ch = e & 7;
+    const int ci = ci0 + row, co = co0 + ch * 8;
+    if (ci >= Cin || co >= Cout) continue;
+    Pack<__hip_bfloat16, 8> v;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v.v[k] = tile[(ch * 8 + k) * kLdsStride + row];
+    *reinterpret_cast<Pack<__hip_bfloat16, 8>*>(wt + ((int64_t)ci * JJ + tap) * Cout + co) = v;
+  }
+}
+}  // namespace
+
+// w [Cout, Cin, KH, KW] bf16 channels-last, stride s (2..4) -> the s*s phase weights
+// conv_weight_flip_t(w, s, qy, qx) for (qy, qx) in row-major phase order, as channels-last views
+// of one buffer (an empty view for a phase without taps).
+std::vector<at::Tensor> conv_weight_phase_flip(const at::Tensor& w, int64_t s) {
+  IAMD_CHECK(w.is_cuda() && w.dim() == 4 && w.scalar_type() == at::kBFloat16 &&
+                 w.is_contiguous(at::MemoryFormat::ChannelsLast),
+             "conv_weight_phase_flip: packed channels-last 4-D bf16 CUDA weight expected");
+  IAMD_CHECK(s >= 1 && s <= 4, "conv_weight_phase_flip: stride must be 1..4");
+  const int Cout = (int)w.size(0), Cin = (int)w.size(1), KH = (int)w.size(2), KW = (int)w.size(3);
+  IAMD_CHECK(Cout % 8 == 0 && Cin % 8 == 0,
+             "conv_weight_phase_flip: channels must be multiples of 8");
+  PhaseOffsets po;
+  std::vector<std::array<int64_t, 3>> shp;  // (Jy, Jx, offset)
+  int64_t off = 0;
+  for (int qy = 0; qy < s; ++qy)
+    for (int qx = 0; qx < s; ++qx) {
+      const int64_t Jy = qy < KH ? (KH - qy + s - 1) / s : 0;
+      const int64_t Jx = qx < KW ? (KW - qx + s - 1) / s : 0;
+      po.off[qy * s + qx] = off;
+      shp.push_back({Jy, Jx, off});
+      off += (int64_t)Cin * Cout * Jy * Jx;
+    }
+  auto flat = at::empty({std::max<int64_t>(off, 1)}, w.options());
+  std::vector<at::Tensor> out;
+  for (auto& e : shp)
+    out.push_back(flat.as_strided({Cin, Cout, e[0], e[1]},
+                                  {e[0] * e[1] * Cout, 1, e[1] * Cout, Cout}, e[2]));
+  if (off == 0) return out;
+  const dim3 grid(ceil_div(Cin, kTile), ceil_div(Cout, kTile), (unsigned)(KH * KW));
+  hipLaunchKernelGGL(phase_flip_kernel, grid, dim3(kT), 0, stream(),
+                     reinterpret_cast<const __hip_bfloat16*>(w.data_ptr()),
+                     reinterpret_cast<__hip_bfloat16*>(flat.data_ptr()), Cout, Cin, KH, KW, (int)s,
+                     po);
+  IAMD_LAUNCH_CHECK();
+  return out;
+}
+
 namespace {
 
 // ---- multi-tensor plain flip (s = 1): every stride-1 conv weight of a network in one launch --
@@ -592,6 +683,28 @@ at::Tensor pad_channels_cast(const at::Tensor& x, int64_t Cp, at::ScalarType dty
   else launch(float(), float());
   IAMD_LAUNCH_CHECK();
   return y;
+}
+
+
+// ---- test support: fill the LDS of every CU with a NaN bit pattern ---------------------------
+// LDS is not cleared between workgroups, so a kernel that reads LDS it never wrote picks up
+// whatever the previous workgroup on that CU left there — in a hipGraph replay a different
+// predecessor than in an eager run. Running this right before a kernel under test turns such a
+// read into NaN outputs (tests/test_kernels_gpu.py).
+namespace {
+constexpr int kPoisonBytes = 160 * 1024;
+__global__ void __launch_bounds__(256) lds_poison_kernel(int iters) {
+  __shared__ __attribute__((aligned(16))) uint32_t buf[kPoisonBytes / 4];
+  volatile uint32_t* vb = buf;  // volatile: the stores have no reader and must not be dropped
+  for (int it = 0; it < iters; ++it)
+    for (int i = threadIdx.x; i < kPoisonBytes / 4; i += 256) vb[i] = 0xffffffffu;
+}
+}  // namespace
+
+void lds_poison(int64_t blocks) {
+  hipLaunchKernelGGL(lds_poison_kernel, dim3((unsigned)std::max<int64_t>(1, blocks)), dim3(256),
+                     0, stream(), 1);
+  IAMD_LAUNCH_CHECK();
 }
 
 }  // namespace iamd

@@ -1751,6 +1751,7 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
 
 
 at::Tensor conv_weight_flip_t(const at::Tensor& w, int64_t s, int64_t qy, int64_t qx, int64_t nb);
+std::vector<at::Tensor> conv_weight_phase_flip(const at::Tensor& w, int64_t s);
 
 // The transposed-weight (BT) v4 data gradient saves the flipped weight copy (one small
 // flip_t pass per backward) but runs 10-35% slower than v4 on the flipped copy: its
@@ -1848,7 +1849,9 @@ at::Tensor conv2d_dgrad_strided(const at::Tensor& dy, const at::Tensor& w, int64
              "conv2d_dgrad_strided: stored channels must be Cin or a multiple of 8 below it");
   auto dx = at::empty({B, ncv, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   std::vector<ConvArgs> phases;
-  std::vector<at::Tensor> keep;
+  // every phase's flipped sub-kernel in one launch (views of one buffer, freed on this stream
+  // after the kernels below)
+  const std::vector<at::Tensor> pw_all = conv_weight_phase_flip(w, s);
   bool zero_fill = false;
   const bool bn128 = N % 128 == 0;
   const int BN = bn128 ? 128 : 64;
@@ -1862,8 +1865,7 @@ at::Tensor conv2d_dgrad_strided(const at::Tensor& dy, const at::Tensor& w, int64
         continue;
       }
       const int cy = (int)((ry + ph - ky0) / s), cx = (int)((rx + pw - kx0) / s);
-      at::Tensor wt = conv_weight_flip_t(w, s, ky0, kx0, 1);  // [N, K, jy, jx]
-      keep.push_back(wt);
+      const at::Tensor& wt = pw_all[ky0 * s + kx0];  // [N, K, jy, jx]
       ConvArgs a;
       a.x = reinterpret_cast<const __hip_bfloat16*>(dy.data_ptr());
       a.w = reinterpret_cast<const __hip_bfloat16*>(wt.data_ptr());

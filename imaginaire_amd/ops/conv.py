@@ -573,13 +573,28 @@ class _MfmaConvPerSample(torch.autograd.Function):
         kh, kw = wb.shape[2], wb.shape[3]
         dy = _pad_channels(dy, op, torch.bfloat16)
         dx = dw = db = None
-        if ctx.needs_input_grad[0]:
+        dbg = _PS_DEBUG
+        if dbg:  # bisection switch: bit 1 dx, bit 2 dw on PyTorch's reference ops
+            xs = xb.float().detach()
+            ws_ = wb.float().reshape(B, op, cp, kh, kw)
+            if dbg & 1 and ctx.needs_input_grad[0]:
+                dx = torch.cat([torch.nn.grad.conv2d_input(
+                    (1,) + tuple(xs.shape[1:]), ws_[i], dy[i:i + 1].float(), 1, padding,
+                    dilation) for i in range(B)])
+                dx = (dx[:, :xc] if dx.shape[1] != xc else dx).to(xdt).contiguous(
+                    memory_format=_CL)
+            if dbg & 2 and ctx.needs_input_grad[1]:
+                g = torch.stack([torch.nn.grad.conv2d_weight(
+                    xs[i:i + 1], (op, cp, kh, kw), dy[i:i + 1].float(), 1, padding, dilation)
+                    for i in range(B)])
+                dw = g[:, :cout, :cin].to(wdt)
+        if ctx.needs_input_grad[0] and dx is None:
             pt = (dilation[0] * (kh - 1) - padding[0], dilation[1] * (kw - 1) - padding[1])
             wt = _ext.ext().conv_weight_flip_t(wb, 1, 0, 0, B)
             dx = _ext.ext().conv2d_mfma(dy, wt, None, 1, 1, pt[0], pt[1], dilation[0],
                                         dilation[1], 1.0, B)
             dx = (dx[:, :xc] if dx.shape[1] != xc else dx).to(xdt)
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and dw is None:
             g = _ext.ext().conv2d_wgrad_mfma(dy, xb, kh, kw, 1, 1, padding[0], padding[1],
                                              dilation[0], dilation[1], -1, -1, False, B)
             # [B * op, cp, kh, kw] (memory [B][op][kh][kw][cp]) -> [B, cout, cin, kh, kw]
@@ -591,6 +606,7 @@ class _MfmaConvPerSample(torch.autograd.Function):
 
 
 _PER_SAMPLE = os.environ.get('IMAGINAIRE_AMD_PER_SAMPLE', '1') == '1'
+_PS_DEBUG = int(os.environ.get('IMAGINAIRE_AMD_PS_DEBUG', '0'))
 
 
 def per_sample_eligible(x, w, stride, groups):

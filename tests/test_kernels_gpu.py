@@ -1531,6 +1531,36 @@ def test_mt_conv_weight_flip_t_matches_single():
     (1, 64, 128, 15, 20, 2, 4, 1, None),    # 2x2 s4: kernel smaller than the stride
     (2, 16, 64, 128, 128, 3, 2, 1, 16),     # fs-vid2vid ref_img_down_0: 16 of 64 stored
 ])
+def test_conv_weight_phase_flip_matches_per_phase(case):
+    """The one-launch phase flip of a strided conv weight equals conv_weight_flip_t per phase."""
+    from imaginaire_amd.ops import _ext
+    X = _ext.ext()
+    B, cin, cout, H, W, k, s, p, ncv = case
+    cp = (cin + 63) // 64 * 64
+    w = torch.randn(cout, cp, k, k, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    got = X.conv_weight_phase_flip(w, s)
+    assert len(got) == s * s
+    for qy in range(s):
+        for qx in range(s):
+            g = got[qy * s + qx]
+            if qy >= k or qx >= k or g.numel() == 0:
+                assert g.numel() == 0
+                continue
+            assert torch.equal(g, X.conv_weight_flip_t(w, s, qy, qx, 1)), (qy, qx)
+
+
+@pytest.mark.parametrize('case', [
+    # B, Cin, Cout, H, W, k, stride, pad, ncv
+    (2, 128, 256, 32, 64, 4, 2, 1, None),   # PatchGAN 4x4 s2: four 2x2-tap phases
+    (2, 256, 512, 16, 32, 3, 2, 1, None),   # 3x3 s2: 2x2 / 2x1 / 1x2 / 1x1-tap phases
+    (1, 64, 128, 33, 17, 3, 2, 1, None),    # odd sizes: phases of different output sizes
+    (2, 96, 128, 16, 16, 4, 2, 1, 96),      # Cin 96: 96 of 128 padded channels stored
+    (1, 64, 64, 24, 24, 3, 3, 0, None),     # stride 3, no padding
+    (2, 128, 64, 32, 32, 1, 2, 0, None),    # 1x1 s2 shortcut: three phases get no taps
+    (1, 64, 128, 15, 20, 2, 4, 1, None),    # 2x2 s4: kernel smaller than the stride
+    (2, 16, 64, 128, 128, 3, 2, 1, 16),     # fs-vid2vid ref_img_down_0: 16 of 64 stored
+])
 def test_conv2d_dgrad_strided_one_launch(case):
     """All s*s phase convs of a strided data gradient in one k10 launch, each storing into its
     parity sub-grid of dx (negative phase padding where a phase starts inside dy) vs fp32
@@ -1552,3 +1582,51 @@ def test_conv2d_dgrad_strided_one_launch(case):
     assert got.shape == ref.shape
     scale = ref.abs().max().item()
     assert (got.float() - ref).abs().max().item() <= 1e-2 * scale
+
+
+@pytest.mark.parametrize('ver', ['1', '3', '4', '5'])
+@pytest.mark.parametrize('case', [
+    # B, Cin, Cout, H, W, k, pad
+    (2, 128, 256, 8, 256, 5, 2),
+    (2, 64, 128, 16, 64, 3, 1),
+    (1, 256, 256, 16, 32, 3, 1),
+    (2, 128, 256, 12, 96, 5, 2),
+])
+def test_conv_kernels_never_read_unwritten_lds(case, ver):
+    """Every k10 forward variant and the k11 weight gradients give bitwise the same result after
+    the LDS of every CU was filled with NaN bits (lds_poison): no kernel reads LDS it did not
+    write in this launch (a hipGraph replay hands such a read a different predecessor's data
+    than an eager run)."""
+    import os
+    from imaginaire_amd.ops import _ext
+    X = _ext.ext()
+    B, cin, cout, H, W, k, p = case
+    torch.manual_seed(25)
+    x = torch.randn(B, cin, H, W, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    w = (torch.randn(cout, cin, k, k, device='cuda') / (cin * k * k) ** 0.5).to(
+        torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    bias = torch.randn(cout, device='cuda')
+    dy = torch.randn(B, cout, H, W, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    try:
+        os.environ['IMAGINAIRE_AMD_CONV_V'] = ver
+        outs = []
+        for poison in (False, True):
+            if poison:
+                X.lds_poison()
+            y = X.conv2d_mfma(x, w, bias, 1, 1, p, p, 1, 1, 0.2, 1, -1)
+            if poison:
+                X.lds_poison()
+            g = X.conv2d_wgrad_mfma(dy, x, k, k, 1, 1, p, p, 1, 1, -1, -1, False, 1,
+                                    int(ver) % 3)
+            if poison:
+                X.lds_poison()
+            dx = X.conv2d_dgrad_mfma(dy, w, p, p, -1)
+            torch.cuda.synchronize()
+            outs.append((y, g, dx))
+    finally:
+        os.environ.pop('IMAGINAIRE_AMD_CONV_V')
+    for name, a, b in zip(('y', 'dw', 'dx'), outs[0], outs[1]):
+        assert torch.isfinite(b.float()).all(), name
+        assert torch.equal(a, b), name
