@@ -845,9 +845,8 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
   const bool v2_off = variant == 1 || (v2_env != nullptr && v2_env[0] == '0');
   const bool v2 = !v2_off && (v2_force || (KW == 3 && Wo <= 32)) &&
                   wgrad_v2_shape_ok(Cout, Ho, Wo, KW, sh, sw, dh, dw, nb);
-  // (one gradient per launch: the multi-tap kernel has no per-sample operand / slab offsets)
-  const bool mt = !v2 && nb == 1 && (mt_env == nullptr || mt_env[0] != '0') && Wo % kBP == 0 &&
-                  sw == 1 && dw == 1 && (KW == 3 || KW == 5 || KW == 7);
+  const bool mt = !v2 && (mt_env == nullptr || mt_env[0] != '0') && Wo % kBP == 0 && sw == 1 &&
+                  dw == 1 && (KW == 3 || KW == 5 || KW == 7);
   // x tile: 128 input channels for 3 taps (192 accumulators per wave), 64 for 5 taps (160) or
   // when Cin % 128 != 0 — the 256 accumulation registers of a wave
   const int v2_bc = (KW == 3 && bc128) ? 128 : 64;

@@ -568,6 +568,10 @@ class _MfmaConvPerSample(torch.autograd.Function):
     def backward(ctx, dy):
         xb, wb = ctx.saved_tensors
         padding, dilation, cin, cout, xdt, wdt, xc, bdt = ctx.conf
+        if _PS_CHECK:
+            _ps_check('dy', dy)
+            _ps_check('xb', xb)
+            _ps_check('wb', wb)
         B, cp = xb.shape[0], xb.shape[1]
         op = wb.shape[0] // B
         kh, kw = wb.shape[2], wb.shape[3]
@@ -598,15 +602,53 @@ class _MfmaConvPerSample(torch.autograd.Function):
             g = _ext.ext().conv2d_wgrad_mfma(dy, xb, kh, kw, 1, 1, padding[0], padding[1],
                                              dilation[0], dilation[1], -1, -1, False, B)
             # [B * op, cp, kh, kw] (memory [B][op][kh][kw][cp]) -> [B, cout, cin, kh, kw]
+            if _PS_CHECK:
+                _ps_check('g', g)
             g = g.permute(0, 2, 3, 1).reshape(B, op, kh, kw, cp)[:, :cout, :, :, :cin]
             dw = g.permute(0, 1, 4, 2, 3).to(wdt)
+            if _PS_CHECK:
+                _ps_check('dw', dw)
         if ctx.needs_input_grad[2]:
-            db = dy.sum((2, 3), dtype=torch.float32)[:, :cout].to(bdt)  # no fp32 copy of dy
+            # per-sample bias gradients on the k2 column-sum kernel (one small launch per
+            # sample): torch's dy.sum((2, 3)) came out non-finite from finite dy inside the
+            # fs-vid2vid hipGraph replay (scripts/probe/graph_nan_probe.py, PS_CHECK)
+            db = torch.stack([_ext.ext().bias_act_bwd(dy[i:i + 1], dy[i:i + 1], 1.0)[1]
+                              for i in range(B)])[:, :cout].to(bdt)
+            if _PS_CHECK:
+                _ps_check('db', db)
+        if _PS_CHECK and dx is not None:
+            _ps_check('dx', dx)
         return dx, dw, db, None, None
 
 
 _PER_SAMPLE = os.environ.get('IMAGINAIRE_AMD_PER_SAMPLE', '1') == '1'
 _PS_DEBUG = int(os.environ.get('IMAGINAIRE_AMD_PS_DEBUG', '0'))
+# IMAGINAIRE_AMD_PS_CHECK=1 (debugging): the per-sample backward records isfinite() of its
+# operands and results into a device flag array (graph-capturable); read with ps_check_report()
+_PS_CHECK = os.environ.get('IMAGINAIRE_AMD_PS_CHECK', '0') == '1'
+_PS_FLAGS = {}
+
+
+def _ps_check(name, t):
+    st = _PS_FLAGS.setdefault('state', {'n': 0, 'labels': []})
+    if 'flags' not in _PS_FLAGS:
+        _PS_FLAGS['flags'] = torch.ones(4096, dtype=torch.bool, device=t.device)
+    i = st['n'] % 4096
+    st['n'] += 1
+    st['labels'].append((name, tuple(t.shape), t.dtype))
+    _PS_FLAGS['flags'][i:i + 1].copy_(torch.isfinite(t.detach()).all().reshape(1))
+
+
+def ps_check_report(reset=True):
+    """(label, finite) of every per-sample backward check recorded since the last reset."""
+    st = _PS_FLAGS.get('state')
+    if not st:
+        return []
+    f = _PS_FLAGS['flags'][:min(st['n'], 4096)].cpu().tolist()
+    out = list(zip(st['labels'][:len(f)], f))
+    if reset:
+        _PS_FLAGS['flags'].fill_(True)
+    return out
 
 
 def per_sample_eligible(x, w, stride, groups):
@@ -678,8 +720,9 @@ class _TapSplitConv2d(torch.autograd.Function):
                                              False, 1)
             # [t*cout + c, ci] -> [c, ci, kh, kw]
             dw = g.reshape(kh, kw, cout, cin).permute(2, 3, 0, 1).to(wdt)
-        if ctx.needs_input_grad[2]:
-            db = dy.float().sum((0, 2, 3)).to(bdt)
+        if ctx.needs_input_grad[2]:  # the k2 column-sum kernel (no torch reduction)
+            dyb = nhwc(dy if dy.dtype in (torch.bfloat16, torch.float32) else dy.float())
+            db = _ext.ext().bias_act_bwd(dyb, dyb, 1.0)[1].to(bdt)
         return dx, dw, db, None, None
 
 

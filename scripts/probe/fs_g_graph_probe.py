@@ -20,8 +20,11 @@ torch.cuda.set_device(0)
 torch.use_deterministic_algorithms(True, warn_only=True)
 cfg, tr, batches = _build('fs_vid2vid_face', 2)
 G = tr.net_G.module.module if hasattr(tr.net_G.module, 'module') else tr.net_G.module
-part = os.environ.get('IAMD_PROBE_PART', 'label_embedding')
-mod = getattr(G, part) if part != 'G' else G
+part = os.environ.get('IAMD_PROBE_PART', 'weight_generator.label_embedding')
+mod = G
+if part != 'G':
+    for a in part.split('.'):
+        mod = getattr(mod, a)
 wg = G.weight_generator
 rec = {}
 orig_fwd = mod.forward

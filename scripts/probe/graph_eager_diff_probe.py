@@ -83,4 +83,7 @@ for i, (m, A) in enumerate(zip(seqn, res)):
         rows.sort(reverse=True)
         print('   %s differing: %d of %d' % (net, len(rows), len(ga)))
         for r, n in rows[:5]:
-            print('      %.3g  %s' % (r, n.replace('module.module.', '')))
+            a_, b_ = ga.get(n.replace(' (missing)', '')), gb.get(n.replace(' (missing)', ''))
+            print('      %.3g  %s  |a| %.4g |b| %.4g' % (
+                r, n.replace('module.module.', ''), float(a_.norm()) if a_ is not None else -1,
+                float(b_.norm()) if b_ is not None else -1))

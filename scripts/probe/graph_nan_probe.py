@@ -41,5 +41,9 @@ for it in range(3):
         it, len(bad), bad[:4], len(badg)), flush=True)
     for n in badg:
         print('    bad grad', n.replace('module.module.', ''))
+    from imaginaire_amd.ops import conv as _C
+    rep = _C.ps_check_report()
+    nb = [r for r in rep if not r[1]]
+    print('    per-sample checks: %d, non-finite %d: %s' % (len(rep), len(nb), nb[:12]))
     if bad:
         break
