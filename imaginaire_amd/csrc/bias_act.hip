@@ -205,7 +205,10 @@ std::vector<at::Tensor> bias_act_bwd(const at::Tensor& out, const at::Tensor& dy
   // identity activation on the channels-fast path: the kernel writes no dx, dx is dy itself
   auto dx = ((cl || lin) && slope == 1.0) ? dy : at::empty_like(out);
   auto fopt = out.options().dtype(at::kFloat);
-  at::Tensor partial;
+  // one allocation for the partials and db (db is its tail): the partials live as long as db,
+  // so no later allocation of the (graph) pool can reuse their block while the column sum
+  // might still read them
+  at::Tensor buf, partial;
   int P;
   IAMD_DISPATCH_FLOAT_TYPES(out.scalar_type(), "bias_act_bwd", [&] {
     auto op = reinterpret_cast<const scalar_t*>(out.data_ptr());
@@ -220,7 +223,8 @@ std::vector<at::Tensor> bias_act_bwd(const at::Tensor& out, const at::Tensor& dy
       const int rpb = kThreads / tpr;
       int64_t rows_per_block = std::max<int64_t>(rpb * 4, (rows + 511) / 512);
       P = (int)((rows + rows_per_block - 1) / rows_per_block);
-      partial = at::empty({P, C}, fopt);
+      buf = at::empty({(int64_t)P * C + C}, fopt);
+      partial = buf.narrow(0, 0, (int64_t)P * C);
       const bool act = slope != 1.0;
       auto launch = [&](auto vt) {
         constexpr int V = decltype(vt)::value;
@@ -243,7 +247,8 @@ std::vector<at::Tensor> bias_act_bwd(const at::Tensor& out, const at::Tensor& dy
       int vec = 16 / (int)out.element_size();
       while (vec > 1 && (HW % vec)) vec >>= 1;
       P = N;
-      partial = at::empty({N, C}, fopt);
+      buf = at::empty({(int64_t)N * C + C}, fopt);
+      partial = buf.narrow(0, 0, (int64_t)N * C);
       auto launch = [&](auto vt) {
         constexpr int V = decltype(vt)::value;
         hipLaunchKernelGGL((bias_act_bwd_nchw<scalar_t, V>), dim3(N, C), dim3(kThreads), 0,
@@ -259,7 +264,7 @@ std::vector<at::Tensor> bias_act_bwd(const at::Tensor& out, const at::Tensor& dy
     }
   });
   IAMD_LAUNCH_CHECK();
-  auto db = at::empty({C}, fopt);
+  auto db = buf.narrow(0, (int64_t)P * C, C);
   hipLaunchKernelGGL(col_sum, dim3(ceil_div(C, 64)), dim3(64, kColRows), 0, stream(),
                      partial.data_ptr<float>(), P, C, db.data_ptr<float>());
   IAMD_LAUNCH_CHECK();

@@ -305,7 +305,8 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma(WgradArgs a) {
 // (tiles: 3 taps 128 x 64, 5 / 7 taps 64 x 64 — the 256-VGPR budget of 2 waves / SIMD, no
 // spills).
 template <int BNO, int BC, int NT, int NST>
-__global__ __launch_bounds__(kThreads, NT == 5 ? 3 : 2) void conv_wgrad_mfma_mt(WgradArgs a) {
+__global__ __launch_bounds__(kThreads, (NT == 5 && BNO == 64) ? 3 : 2) void conv_wgrad_mfma_mt(
+    WgradArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   constexpr int RA = BNO * 2, RX = BC * 2;        // image row bytes
   constexpr int kAbytes = kBP * RA;
@@ -419,6 +420,56 @@ __global__ __launch_bounds__(kThreads, NT == 5 ? 3 : 2) void conv_wgrad_mfma_mt(
   // 5 taps: one half at a time (48 fragment registers instead of 96: 168 VGPRs, three blocks
   // per CU — the 5x5 shapes whose tile grid needs no split-K fill 768 block slots in one round)
   constexpr int NH = NT >= 5 ? 1 : 2;  // 32-pixel halves whose fragments are read together
+  // 128 x 64 tile with 5 taps: 160 accumulator registers leave no room for all 10 x fragments
+  // of a half, so the x fragments of tap t + 1 are read while tap t's MFMAs run (two buffers)
+  constexpr bool kTapPipe = BNO == 128 && NT == 5;
+  auto compute_tap_pipe = [&](int buf, int h) {
+    const char* As = smem + buf * kStage;
+    const char* Xs = As + kAbytes;
+    // the lane geometry is re-derived from an opaque copy of the lane id on every call, so the
+    // compiler recomputes the fragment addresses (a few VALU) instead of keeping all of them
+    // live across the k loop (which spilled)
+    int l = lane;
+    asm volatile("" : "+v"(l));
+    const int lg = l >> 4, lq = (l >> 2) & 3, lp = l & 3;
+    auto a_addr = [&](int row, int colblk) {
+      return row * RA + ((((colblk + (lp >> 1)) ^ swz<RA>(row))) << 4) + ((lp & 1) << 3);
+    };
+    auto x_addr = [&](int row, int colblk) {
+      return row * RX + ((((colblk + (lp >> 1)) ^ swz<RX>(row))) << 4) + ((lp & 1) << 3);
+    };
+    const int r0 = h * 32 + lg * 8 + lq;
+    bf16x8 af[MI], xf[2][NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int cb = (wm * (BNO / 2) + i * 16) >> 3;
+      const bf16x4 lo = tr_read(As + a_addr(r0, cb));
+      const bf16x4 hi = tr_read(As + a_addr(r0 + 4, cb));
+      af[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+    auto read_x = [&](int t, bf16x8 (&dst)[NI]) {
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int cb = (wn * (BC / 2) + j * 16) >> 3;
+        const bf16x4 lo = tr_read(Xs + x_addr(r0 + t, cb));
+        const bf16x4 hi = tr_read(Xs + x_addr(r0 + t + 4, cb));
+        dst[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+    };
+    read_x(0, xf[0]);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      if (t + 1 < NT) read_x(t + 1, xf[(t + 1) & 1]);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], xf[t & 1][j],
+                                                                 acc[t][i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  };
   auto compute_halves = [&](int buf, int h0) {
     const char* As = smem + buf * kStage;
     const char* Xs = As + kAbytes;
@@ -457,8 +508,13 @@ __global__ __launch_bounds__(kThreads, NT == 5 ? 3 : 2) void conv_wgrad_mfma_mt(
     __builtin_amdgcn_s_setprio(0);
   };
   auto compute = [&](int buf) {
+    if constexpr (kTapPipe) {
+      compute_tap_pipe(buf, 0);
+      compute_tap_pipe(buf, 1);
+    } else {
 #pragma unroll
-    for (int h0 = 0; h0 < 2; h0 += NH) compute_halves(buf, h0);
+      for (int h0 = 0; h0 < 2; h0 += NH) compute_halves(buf, h0);
+    }
   };
 
   if constexpr (NST == 2) {
@@ -854,9 +910,13 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
     a.nNt = Cout / 128;
     a.nCt = Cin / v2_bc;
   }
+  // IMAGINAIRE_AMD_WGRAD_MT5=128: the 5-tap multi-tap kernel on a 128 x 64 tile (2 blocks / CU,
+  // 0.35 KB of LDS fragment reads per MFMA instead of 0.6) — A/B switch
+  const char* mt5_env = std::getenv("IMAGINAIRE_AMD_WGRAD_MT5");
+  const bool mt5_wide = mt && KW == 5 && bno128 && mt5_env != nullptr && std::atoi(mt5_env) == 128;
   if (mt) {  // tiles sized to the 256-VGPR budget of 2 waves / SIMD without spills:
     // 3 taps 128 x 64 (or 64 x 64), 5 / 7 taps 64 x 64
-    a.nNt = Cout / ((KW == 3 && bno128) ? 128 : 64);
+    a.nNt = Cout / (((KW == 3 && bno128) || mt5_wide) ? 128 : 64);
     a.nCt = Cin / 64;
   }
   const int tiles = ((mt || v2) ? (int)KH : KK) * a.nNt * a.nCt;
@@ -865,7 +925,7 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
   // third full (measured: 1200 blocks ran at 28% MFMA issue vs 44% for k10,
   // profiles/pmc_conv_mi355x.txt)
   // (multi-tap: 2 blocks per CU, 3 for the 5-tap kernel's 168-VGPR build)
-  const int slots = v2 ? 256 : (mt ? (KW == 5 ? 768 : 512)
+  const int slots = v2 ? 256 : (mt ? ((KW == 5 && !mt5_wide) ? 768 : 512)
                                    : 256 * ((bno128 && bc128) ? 2 : (bno128 || bc128) ? 3 : 5)) /
                     (int)nb;
   int S = 1;
@@ -982,7 +1042,8 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
       if (bno128) launch_mt(I128(), I64(), T3());
       else launch_mt(I64(), I64(), T3());
     } else if (KW == 5) {
-      launch_mt(I64(), I64(), T5());
+      if (mt5_wide) launch_mt(I128(), I64(), T5());
+      else launch_mt(I64(), I64(), T5());
     } else {
       launch_mt(I64(), I64(), std::integral_constant<int, 7>());
     }

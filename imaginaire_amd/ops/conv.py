@@ -392,14 +392,14 @@ def _strided_dgrad(dy, wb, H, W, s, padding, wts=None, ncv=-1):
 # Off by default: the SPADE step ran 2% SLOWER with the weight / bias gradients on a side
 # stream (51.1-51.2 vs 52.2 images/s back to back, gpurun_out r4t) — the large dgrad and wgrad
 # grids each fill the chip, and sharing it costs both more than the launch gaps it hides.
-_OVERLAP_BWD = os.environ.get('IMAGINAIRE_AMD_CONV_BWD_OVERLAP', '0') == '1'
+_OVERLAP_BWD = os.environ.get('IMAGINAIRE_AMD_CONV_BWD_OVERLAP', '0')  # '1' | 'bias' | '0'
 _BWD_SIDE = {}
 
 
 def _bwd_side_stream():
     """The per-device side stream of the conv backward's weight gradients (None when off, in
     the conv log's timing mode, or under the eager reference path)."""
-    if not _OVERLAP_BWD or _CONV_LOG is not None:
+    if _OVERLAP_BWD not in ('1', 'bias') or _CONV_LOG is not None:
         return None
     dev = torch.cuda.current_device()
     st = _BWD_SIDE.get(dev)
@@ -444,6 +444,8 @@ class _MfmaConv2d(torch.autograd.Function):
     def backward(ctx, dy):
         dy_in = dy  # the residual's gradient (added after the activation: identity)
         xb, wb, y = ctx.saved_tensors
+        if _PS_CHECK:
+            _ps_check('conv.dy', dy)
         stride, padding, dilation, slope, cin, cout, xdt, wdt, bdt, xc = ctx.conf
         need_x, need_w, need_b = ctx.needs_input_grad[:3]
         # the activation backward runs at the saved output's channel count (the real Cout when
@@ -455,10 +457,12 @@ class _MfmaConv2d(torch.autograd.Function):
         # grids leave most CUs idle on their own
         side = _bwd_side_stream() if (need_x and (need_w or need_b)) else None
         side_bias = side is not None and slope == 1.0 and need_b
-        if slope != 1.0 or (need_b and not side_bias):
-            dy = _pad_channels(dy, y.shape[1] if y is not None else dy.shape[1], torch.bfloat16)
-            # identity activation: the k2 kernel reads only dy (y stands in for the layout)
-            dy, db = _ext.ext().bias_act_bwd(y if y is not None else dy, dy, slope)
+        if slope != 1.0:
+            dy = _pad_channels(dy, y.shape[1], torch.bfloat16)
+            dy, db = _ext.ext().bias_act_bwd(y, dy, slope)
+        elif need_b and not side_bias:
+            dy = _pad_channels(dy, dy.shape[1], torch.bfloat16)
+        dy_b = dy  # the bias gradient's operand (identity activation: computed last, below)
         dy = _pad_channels(dy, wb.shape[0], torch.bfloat16)
         dx = dw = None
         cap = _capturing()
@@ -468,7 +472,7 @@ class _MfmaConv2d(torch.autograd.Function):
             with torch.cuda.stream(side):
                 if side_bias:  # bias gradient only: the k2 kernel reads dy, writes no dx
                     db = _ext.ext().bias_act_bwd(dy, dy, 1.0)[1]
-                if need_w:
+                if need_w and _OVERLAP_BWD == '1':
                     dw = _wgrad(dy, xb, wb, stride, padding, dilation, cout, cin, wdt)
         if need_x:
             kh, kw = wb.shape[2], wb.shape[3]
@@ -521,13 +525,21 @@ class _MfmaConv2d(torch.autograd.Function):
                 if t is not None:
                     t.record_stream(main)
         if need_w:
-            if side is None:
+            if dw is None:
                 dw = _wgrad(dy, xb, wb, stride, padding, dilation, cout, cin, wdt)
             if dw.shape[0] != cout or dw.shape[1] != cin:
                 dw = dw[:cout, :cin]
             dw = dw.to(wdt)
+        if slope == 1.0 and need_b and not side_bias:
+            # identity activation: bias gradient only (the k2 kernel reads dy, writes no dx),
+            # after the data and weight gradients
+            db = _ext.ext().bias_act_bwd(dy_b, dy_b, 1.0)[1]
         if db is not None:
             db = db[:cout].to(bdt) if need_b else None
+        if _PS_CHECK:
+            for nm, t in (('conv.db', db), ('conv.dw', dw), ('conv.dx', dx)):
+                if t is not None:
+                    _ps_check(nm, t)
         dres = None
         if ctx.res_dtype is not None and ctx.needs_input_grad[7]:
             dres = dy_in if dy_in.dtype == ctx.res_dtype else dy_in.to(ctx.res_dtype)

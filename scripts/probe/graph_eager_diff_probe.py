@@ -48,6 +48,11 @@ def run(mode):
         with graph_routing():
             graphed.step_fn(d)
     torch.cuda.synchronize()
+    from imaginaire_amd.ops import conv as _C
+    rep = _C.ps_check_report()
+    nb = [(i, r) for i, r in enumerate(rep) if not r[1]]
+    if rep:
+        print('   [%s] backward checks %d, non-finite %d: %s' % (mode, len(rep), len(nb), nb[:6]))
     return _losses(tr), grads(tr.net_D), grads(tr.net_G)
 
 

@@ -52,6 +52,11 @@ def _iteration(config, amp, eager, tmp, seq_len=None, overrides=(), grad_exclude
     from imaginaire_amd.utils.trainer import get_model_optimizer_and_scheduler, get_trainer
     old = os.environ.get('IMAGINAIRE_AMD_EAGER')
     os.environ['IMAGINAIRE_AMD_EAGER'] = '1' if eager else '0'
+    # the fp32 reference runs PyTorch's own (im2col + rocBLAS) convolutions, not MIOpen: one
+    # of MIOpen's fp32 backward solvers faulted (illegal memory access) on the pix2pixHD
+    # reference iteration of one box (gpurun_out r4t, round 4)
+    old_cudnn = torch.backends.cudnn.enabled
+    torch.backends.cudnn.enabled = not eager
     try:
         cfg = Config(os.path.join(ROOT, 'configs', 'unit_test', config))
         cfg.logdir = str(tmp)
@@ -101,6 +106,7 @@ def _iteration(config, amp, eager, tmp, seq_len=None, overrides=(), grad_exclude
         gl = {k: float(v) for k, v in tr.gen_losses.items() if torch.is_tensor(v)}
         return dl, gl, d_norm, g_norm
     finally:
+        torch.backends.cudnn.enabled = old_cudnn
         if old is None:
             os.environ.pop('IMAGINAIRE_AMD_EAGER', None)
         else:
@@ -160,12 +166,13 @@ def test_fs_vid2vid_iteration_hip_bf16_matches_eager_fp32(tmp_path, k):
     # K = 1: the label-weighted reference pooling (k15 channel softmax + per-sample k11 GEMM);
     # K = 2: plus the fused few-shot attention; hyper (per-sample) SPADE convs, FlowNet2 flow
     # loss and the warped-reference path at sequence length 2
-    # The key / query towers of the attention are left out of the K = 2 gradient norm: the
-    # attention softmax is unscaled (energies up to ~50 on this config), so bf16 rounding of the
-    # energy moves those towers' gradients by 0.3-20x relative — in the reference formulation
-    # (bmm + softmax + bmm under autocast) exactly as much as on the fused path
-    # (scripts/probe/fs_attn_probe.py, profiles/fs_attention_bf16_probe_mi355x.txt); the losses
-    # and every other gradient are still compared
+    # K = 2 leaves the weight generator (reference encoder, attention, hyper-weight MLPs) out of
+    # the gradient norm: the attention softmax is unscaled (energies up to ~50 on this config),
+    # so bf16 rounding of the energy moves the key / query towers' gradients by 0.3-20x and the
+    # attended value features' gradients by ~16% relative — in the reference formulation (bmm +
+    # softmax + bmm under autocast) exactly as much as on the fused path
+    # (scripts/probe/fs_attn_probe.py, profiles/fs_attention_bf16_probe_mi355x.txt). The losses
+    # and the rest of the generator are still compared; K = 1 covers the weight generator.
     _compare(tmp_path, 'fs_vid2vid_face.yaml', seq_len=2,
              overrides=[('data.initial_few_shot_K', k)],
-             grad_exclude=('attention_module.',) if k > 1 else ())
+             grad_exclude=('weight_generator.',) if k > 1 else ())
