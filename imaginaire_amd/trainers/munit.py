@@ -38,6 +38,23 @@ class Trainer(BaseTrainer):
         self.best_fid_a = None
         self.best_fid_b = None
 
+    def dis_update(self, data):
+        """The D update; with the gradient penalty, MIOpen is off for it: the penalty's D
+        forward runs on PyTorch ops (eager scope) and its double backward would otherwise take
+        MIOpen's backward solvers, which accumulate with atomics into workspaces they zero with
+        calls a hipGraph capture does not record — replays of the captured MUNIT step then
+        differed from each other and from the eager step (D conv bias gradients,
+        scripts/probe/graph_eager_diff_probe.py). PyTorch's own convolutions (im2col + rocBLAS)
+        are capture-safe and twice differentiable."""
+        if 'gp' not in self.weights:
+            return super().dis_update(data)
+        was = torch.backends.cudnn.enabled
+        torch.backends.cudnn.enabled = False
+        try:
+            return super().dis_update(data)
+        finally:
+            torch.backends.cudnn.enabled = was
+
     def _init_tensorboard(self):
         self.meters = {}
         for name in ['optim/gen_lr', 'optim/dis_lr', 'time/iteration', 'time/epoch']:
