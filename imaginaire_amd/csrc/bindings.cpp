@@ -140,13 +140,17 @@ at::Tensor wgrad_finalize(const at::Tensor& part, int64_t S, int64_t Cop, int64_
                           int64_t Cout, int64_t Cin, int64_t KH, int64_t KW,
                           at::ScalarType dtype);
 at::Tensor sn_scale_backward(const at::Tensor& grad_in, const at::Tensor& weight,
-                             const at::Tensor& u, const at::Tensor& v, const at::Tensor& sigma);
+                             const at::Tensor& u, const at::Tensor& v, const at::Tensor& sigma,
+                             const c10::optional<at::Tensor>& shadow);
 void register_lmdb(pybind11::module_& m);
 void profile_marker(int64_t tag);
 std::vector<at::Tensor> mt_sn_scale_cast(const std::vector<at::Tensor>& weights,
-                                         const at::Tensor& sigma);
+                                         const at::Tensor& sigma,
+                                         const std::vector<at::Tensor>& shadows,
+                                         int64_t shadow_mode);
 at::Tensor mt_sn_power(const std::vector<at::Tensor>& weights, const std::vector<at::Tensor>& us,
-                       const std::vector<at::Tensor>& vs, bool update, double eps);
+                       const std::vector<at::Tensor>& vs, bool update, double eps,
+                       const std::vector<at::Tensor>& shadows);
 }  // namespace iamd
 
 namespace iamd {
@@ -160,8 +164,13 @@ void rccl_all_gather(const at::Tensor& out, const at::Tensor& in, int64_t h);
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "imaginaire_amd gfx950 HIP kernels";
   iamd::register_lmdb(m);
-  m.def("mt_sn_power", &iamd::mt_sn_power, "batched spectral-norm power iteration (k5b)");
-  m.def("mt_sn_scale_cast", &iamd::mt_sn_scale_cast, "batched W/sigma -> bf16 (k5c)");
+  m.def("mt_sn_power", &iamd::mt_sn_power, "batched spectral-norm power iteration (k5b)",
+        py::arg("weights"), py::arg("us"), py::arg("vs"), py::arg("update"), py::arg("eps"),
+        py::arg("shadows") = std::vector<at::Tensor>());
+  m.def("mt_sn_scale_cast", &iamd::mt_sn_scale_cast,
+        "batched W/sigma -> bf16 (k5c); shadow_mode 1 reads bf16 copies of W, 2 writes them",
+        py::arg("weights"), py::arg("sigma"), py::arg("shadows") = std::vector<at::Tensor>(),
+        py::arg("shadow_mode") = 0);
   m.def("profile_marker", &iamd::profile_marker, "named no-op kernel for trace phase splits");
   m.def("rccl_unique_id", &iamd::rccl_unique_id, "RCCL unique id (128-byte CPU tensor)");
   m.def("rccl_comm_init", &iamd::rccl_comm_init, "join an RCCL communicator; returns a handle");
@@ -214,7 +223,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("blocks") = 2048);
   m.def("conv_weight_phase_flip", &iamd::conv_weight_phase_flip,
         "all s*s phase weights conv_weight_flip_t(w, s, qy, qx) of a stride-s conv in one launch");
-  m.def("sn_scale_backward", &iamd::sn_scale_backward, "spectral-norm W/sigma backward (k5d)");
+  m.def("sn_scale_backward", &iamd::sn_scale_backward, "spectral-norm W/sigma backward (k5d)",
+        py::arg("grad"), py::arg("weight"), py::arg("u"), py::arg("v"), py::arg("sigma"),
+        py::arg("shadow") = c10::optional<at::Tensor>());
   m.def("norm_stats", &iamd::norm_stats, "per-(group,channel) statistics (k1)",
         py::arg("x"), py::arg("per_instance"), py::arg("eps"), py::arg("weight"),
         py::arg("bias"), py::arg("partial_only"), py::arg("running_mean") = py::none(),

@@ -185,6 +185,98 @@ __global__ __launch_bounds__(64) void corr_fwd_mfma(
       }
 }
 
+// The same banded MFMA product, organised along the image-2 row (multi-wave): every (output row
+// oy, displacement row tj) pair with oy + (tj - R) S2 = const reads the SAME image-2 strip, so a
+// block owns one image-2 row y2 and one TX-pixel segment, stages that strip (TX + 2 R S2 pixels x
+// all C channels) in LDS once, and its 4 waves run the D pairs of the diagonal (wave w: tj = w,
+// w + 4, ...), each reading its image-1 fragments from global / L2 and the strip fragments from
+// LDS. Per pair that is ~18 KB of L2 traffic instead of ~64 KB (the strip was re-read by each of
+// the D blocks sharing it). LDS rows are padded by 16 B so the 16 fragment rows of a read (S2
+// strip pixels apart) fall in different banks.
+template <int S2>
+__global__ __launch_bounds__(256) void corr_fwd_mfma_diag(
+    const __hip_bfloat16* __restrict__ in1, const __hip_bfloat16* __restrict__ in2,
+    __hip_bfloat16* __restrict__ out, int H, int W, int C, int oH, int oW, int pad, int md,
+    int R, int D) {
+  typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+  typedef __attribute__((ext_vector_type(4))) float f32x4;
+  constexpr int TX = 16 * S2;
+  constexpr int NP = 48 * S2;                   // strip pixels staged (3 x 16 per parity)
+  extern __shared__ __attribute__((aligned(16))) char strip[];
+  const int rowb = C * 2 + 16;                  // LDS bytes per strip pixel (padded)
+  const int ox0 = blockIdx.x * TX;
+  const int n = blockIdx.z;
+  const int y2 = (md - pad - R * S2) + (int)blockIdx.y;  // image-2 row of this diagonal
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int xa0 = ox0 + md - pad;   // image column of tile pixel 0
+  const int xb0 = xa0 - R * S2;     // image column of strip pixel 0
+  const bool row2 = (unsigned)y2 < (unsigned)H;
+  // ---- stage the strip: NP pixels x C channels, 16-byte chunks, zeros outside the image ------
+  const int cpp = C / 8;  // chunks per pixel
+  const __hip_bfloat16* r2 = in2 + ((int64_t)n * H + (row2 ? y2 : 0)) * W * C;
+  for (int e = tid; e < NP * cpp; e += 256) {
+    const int pxl = e / cpp, ch = e - pxl * cpp;
+    const int xb = xb0 + pxl;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (row2 && (unsigned)xb < (unsigned)W)
+      v = *reinterpret_cast<const uint4*>(r2 + (int64_t)xb * C + ch * 8);
+    *reinterpret_cast<uint4*>(strip + pxl * rowb + ch * 16) = v;
+  }
+  __syncthreads();
+  const int fr = lane & 15, fk = (lane >> 4) * 8;
+  const float inv = 1.f / (float)C;
+  const int DD = D * D;
+  const bf16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int tj = wid; tj < D; tj += 4) {
+    const int y1 = y2 - (tj - R) * S2;          // image-1 row of this pair
+    const int oy = y1 - md + pad;
+    if ((unsigned)oy >= (unsigned)oH) continue;
+    const bool row1 = row2 && (unsigned)y1 < (unsigned)H;
+    const __hip_bfloat16* r1 = in1 + ((int64_t)n * H + (row1 ? y1 : 0)) * W * C;
+    int aoff[S2];
+    bool aok[S2];
+#pragma unroll
+    for (int r = 0; r < S2; ++r) {
+      const int xa = xa0 + S2 * fr + r;
+      aok[r] = row1 && (unsigned)xa < (unsigned)W && ox0 + S2 * fr + r < oW;
+      aoff[r] = aok[r] ? xa * C + fk : 0;
+    }
+    f32x4 acc[S2][3];
+#pragma unroll
+    for (int r = 0; r < S2; ++r)
+#pragma unroll
+      for (int cf = 0; cf < 3; ++cf) acc[r][cf] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (row1) {
+      for (int c0 = 0; c0 < C; c0 += 32) {
+#pragma unroll
+        for (int r = 0; r < S2; ++r) {
+          const bf16x8 af = aok[r] ? *reinterpret_cast<const bf16x8*>(r1 + aoff[r] + c0) : zero;
+#pragma unroll
+          for (int cf = 0; cf < 3; ++cf) {
+            const int pxl = S2 * (cf * 16 + fr) + r;
+            const bf16x8 bfr =
+                *reinterpret_cast<const bf16x8*>(strip + pxl * rowb + (c0 + fk) * 2);
+            acc[r][cf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[r][cf], 0, 0, 0);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < S2; ++r)
+#pragma unroll
+      for (int cf = 0; cf < 3; ++cf)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int a = (lane >> 4) * 4 + e;
+          const int t = cf * 16 + fr - a;
+          const int ox = ox0 + S2 * a + r;
+          if (t >= 0 && t < D && ox < oW)
+            out[(((int64_t)n * oH + oy) * oW + ox) * DD + tj * D + t] =
+                __float2bfloat16(acc[r][cf][e] * inv);
+        }
+  }
+}
+
 // Generic forward (any kernel_size): one workgroup (one wave) per output pixel.
 template <typename T>
 __global__ __launch_bounds__(kWave) void corr_fwd_generic(
@@ -432,7 +524,20 @@ at::Tensor correlation_forward(const at::Tensor& input1, const at::Tensor& input
     auto pa = reinterpret_cast<const __hip_bfloat16*>(a.data_ptr());
     auto pb = reinterpret_cast<const __hip_bfloat16*>(b.data_ptr());
     auto po = reinterpret_cast<__hip_bfloat16*>(out.data_ptr());
-    if (s2 == 2)
+    // the diagonal multi-wave kernel (strip staged once per image-2 row) when the strip fits in
+    // LDS; IMAGINAIRE_AMD_CORR_DIAG=0 keeps the one-wave-per-(row, tj) kernel
+    const char* dg = std::getenv("IMAGINAIRE_AMD_CORR_DIAG");
+    const size_t strip_bytes = (size_t)48 * s2 * (C * 2 + 16);
+    const bool diag = (dg == nullptr || dg[0] != '0') && strip_bytes <= 64 * 1024;
+    const dim3 gdiag((unsigned)ceil_div(oW, 16 * (int)s2), (unsigned)(oH + 2 * R * (int)s2),
+                     (unsigned)N);
+    if (diag && s2 == 2)
+      hipLaunchKernelGGL((corr_fwd_mfma_diag<2>), gdiag, dim3(256), strip_bytes, stream(), pa, pb,
+                         po, H, W, C, oH, oW, (int)pad, (int)md, R, D);
+    else if (diag)
+      hipLaunchKernelGGL((corr_fwd_mfma_diag<1>), gdiag, dim3(256), strip_bytes, stream(), pa, pb,
+                         po, H, W, C, oH, oW, (int)pad, (int)md, R, D);
+    else if (s2 == 2)
       hipLaunchKernelGGL((corr_fwd_mfma<2>), dim3(ceil_div(oW, 32), oH, N * D), dim3(64), 0,
                          stream(), pa, pb, po, H, W, C, oH, oW, (int)pad, (int)md, R, D);
     else

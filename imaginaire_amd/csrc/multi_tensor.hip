@@ -137,7 +137,8 @@ Table& get_table(const std::vector<std::vector<at::Tensor>>& lists, const at::De
   // freed tensor's address reused by one of another shape must not hit a stale entry)
   for (size_t i = 0; i < T; ++i) {
     for (auto& l : lists) {
-      h = mix(h, reinterpret_cast<uint64_t>(l[i].data_ptr()));
+      // (an empty tensor stands for "no operand": the optional bf16 shadow of a parameter)
+      h = mix(h, l[i].numel() ? reinterpret_cast<uint64_t>(l[i].data_ptr()) : 0);
       h = mix(h, (uint64_t)l[i].numel());
     }
     const at::Tensor& t0 = lists[0][i];
@@ -151,7 +152,8 @@ Table& get_table(const std::vector<std::vector<at::Tensor>>& lists, const at::De
   std::vector<TensorEntry> ents(T);
   std::vector<int32_t> bm;
   for (size_t i = 0; i < T; ++i) {
-    for (size_t k = 0; k < 5; ++k) ents[i].p[k] = k < lists.size() ? lists[k][i].data_ptr() : nullptr;
+    for (size_t k = 0; k < 5; ++k)
+      ents[i].p[k] = (k < lists.size() && lists[k][i].numel()) ? lists[k][i].data_ptr() : nullptr;
     ents[i].numel = lists[0][i].numel();
     ents[i].cols = lists[0][i].dim() > 0 && lists[0][i].size(0) > 0
                        ? ents[i].numel / lists[0][i].size(0) : 1;
@@ -456,8 +458,15 @@ void mt_adam(const std::vector<at::Tensor>& params, const std::vector<at::Tensor
   check_same_dtype(grads, gdt, "mt_adam grads");
   std::vector<std::vector<at::Tensor>> lists{params, grads, exp_avgs, exp_avg_sqs};
   if (!shadows.empty()) {
+    // optional per parameter: an empty tensor = no shadow for that parameter
     IAMD_CHECK(shadows.size() == params.size(), "mt_adam: shadow list size");
-    check_same_dtype(shadows, at::kBFloat16, "mt_adam shadow");
+    for (size_t i = 0; i < shadows.size(); ++i) {
+      if (shadows[i].numel() == 0) continue;
+      IAMD_CHECK(shadows[i].scalar_type() == at::kBFloat16 && shadows[i].is_cuda() &&
+                     shadows[i].sizes() == params[i].sizes() &&
+                     shadows[i].strides() == params[i].strides(),
+                 "mt_adam: a shadow must be a bf16 tensor laid out like its parameter");
+    }
     lists.push_back(shadows);
   }
   Table& tb = get_table(lists, params[0].device());

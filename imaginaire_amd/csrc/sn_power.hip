@@ -33,6 +33,7 @@ constexpr int kRowsPerBlock = 4;  // rows (waves) per K3 block
 
 struct SnEntry {
   const float* W;
+  const __hip_bfloat16* Wb;  // bf16 copy of W (the optimizer's shadow): read instead when set
   float* u;
   float* v;
   float* t;  // workspace [w]
@@ -89,13 +90,23 @@ __global__ void __launch_bounds__(kT) sn_colsum(const SnEntry* __restrict__ ents
       const int64_t rr = r + i;
       const bool ok = rr < r1;
       uv[i] = ok ? e.u[rr] : 0.f;
-      const float* src = e.W + (ok ? rr : r0) * e.w + c;
-      if (vec) {
-        const float4 v4 = *reinterpret_cast<const float4*>(src);
-        wv[i][0] = v4.x; wv[i][1] = v4.y; wv[i][2] = v4.z; wv[i][3] = v4.w;
-      } else {
+      const int64_t off = (ok ? rr : r0) * e.w + c;
+      if (e.Wb) {
+        if (vec) {
+          load_vec<__hip_bfloat16, 4>(e.Wb + off, wv[i]);
+        } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) wv[i][k] = c + k < e.w ? src[k] : 0.f;
+          for (int k = 0; k < 4; ++k) wv[i][k] = c + k < e.w ? __bfloat162float(e.Wb[off + k]) : 0.f;
+        }
+      } else {
+        const float* src = e.W + off;
+        if (vec) {
+          const float4 v4 = *reinterpret_cast<const float4*>(src);
+          wv[i][0] = v4.x; wv[i][1] = v4.y; wv[i][2] = v4.z; wv[i][3] = v4.w;
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) wv[i][k] = c + k < e.w ? src[k] : 0.f;
+        }
       }
     }
 #pragma unroll
@@ -152,7 +163,22 @@ __global__ void __launch_bounds__(64 * kRowsPerBlock) sn_rows(const SnEntry* __r
   const float k = update ? 1.f / fmaxf(sqrtf(scal[4 * bm[0]]), eps) : 1.f;
   const float* row = e.W + r * e.w;
   float acc = 0.f;
-  if (update) {  // t is in memory order: straight dot, 16-B loads, 4 per lane in flight
+  if (update && e.Wb) {  // bf16 copy of W: 8 elements per lane and trip
+    const __hip_bfloat16* rb = e.Wb + r * e.w;
+    const float* x = e.t;
+    if (e.vec && e.w % 8 == 0) {
+      for (int64_t c = lane * 8; c < e.w; c += 64 * 8) {
+        float a[8], b[8];
+        load_vec<__hip_bfloat16, 8>(rb + c, a);
+        load_vec<float, 4>(x + c, *reinterpret_cast<float(*)[4]>(b));
+        load_vec<float, 4>(x + c + 4, *reinterpret_cast<float(*)[4]>(b + 4));
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc = fmaf(a[k], b[k], acc);
+      }
+    } else {
+      for (int64_t c = lane; c < e.w; c += 64) acc = fmaf(__bfloat162float(rb[c]), x[c], acc);
+    }
+  } else if (update) {  // t is in memory order: straight dot, 16-B loads, 4 per lane in flight
     const float* x = e.t;
     if (e.vec) {
       const float4* r4 = reinterpret_cast<const float4*>(row);
@@ -174,6 +200,10 @@ __global__ void __launch_bounds__(64 * kRowsPerBlock) sn_rows(const SnEntry* __r
     } else {
       for (int64_t c = lane; c < e.w; c += 64) acc = fmaf(row[c], x[c], acc);
     }
+  } else if (e.Wb) {
+    const __hip_bfloat16* rb = e.Wb + r * e.w;
+    for (int64_t c = lane; c < e.w; c += 64)
+      acc = fmaf(__bfloat162float(rb[c]), e.v[logical_col(e, c)], acc);
   } else {
     for (int64_t c = lane; c < e.w; c += 64) acc = fmaf(row[c], e.v[logical_col(e, c)], acc);
   }
@@ -221,8 +251,10 @@ std::mutex g_sn_mu;
 std::unordered_map<uint64_t, SnPlan> g_sn_cache;
 
 SnPlan& get_plan(const std::vector<at::Tensor>& W, const std::vector<at::Tensor>& U,
-                 const std::vector<at::Tensor>& V) {
+                 const std::vector<at::Tensor>& V, const std::vector<at::Tensor>& WB) {
   uint64_t hsh = 0x51ed270b0b6e3a6dULL;
+  for (size_t i = 0; i < WB.size(); ++i)
+    hsh ^= reinterpret_cast<uint64_t>(WB[i].data_ptr()) * 0x2545F4914F6CDD1DULL + (hsh << 5);
   for (size_t i = 0; i < W.size(); ++i) {
     hsh ^= reinterpret_cast<uint64_t>(W[i].data_ptr()) + 0x9e3779b97f4a7c15ULL + (hsh << 6);
     hsh ^= reinterpret_cast<uint64_t>(U[i].data_ptr()) + (hsh >> 2);
@@ -255,6 +287,14 @@ SnPlan& get_plan(const std::vector<at::Tensor>& W, const std::vector<at::Tensor>
     IAMD_CHECK(U[i].is_contiguous() && V[i].is_contiguous(), "mt_sn_power: u/v contiguous");
     SnEntry& e = ents[i];
     e.W = w.data_ptr<float>();
+    e.Wb = nullptr;
+    if (!WB.empty()) {
+      IAMD_CHECK(WB[i].scalar_type() == at::kBFloat16 && WB[i].sizes() == w.sizes() &&
+                     WB[i].strides() == w.strides() &&
+                     (reinterpret_cast<uintptr_t>(WB[i].data_ptr()) & 15) == 0,
+                 "mt_sn_power: a bf16 copy must be laid out like its weight, 16-B aligned");
+      e.Wb = reinterpret_cast<const __hip_bfloat16*>(WB[i].data_ptr());
+    }
     e.u = U[i].data_ptr<float>();
     e.v = V[i].data_ptr<float>();
     e.h = w.size(0);
@@ -307,11 +347,15 @@ SnPlan& get_plan(const std::vector<at::Tensor>& W, const std::vector<at::Tensor>
 }  // namespace
 
 // Returns sigma [L] (fp32). update=true runs one power iteration (u, v updated in place).
+// shadows (optional, parallel to weights): bf16 copies of W (written by the optimizer step) that
+// the GEMV passes read instead of the fp32 weights (half the bytes).
 at::Tensor mt_sn_power(const std::vector<at::Tensor>& weights, const std::vector<at::Tensor>& us,
-                       const std::vector<at::Tensor>& vs, bool update, double eps) {
+                       const std::vector<at::Tensor>& vs, bool update, double eps,
+                       const std::vector<at::Tensor>& shadows) {
   IAMD_CHECK(!weights.empty() && weights.size() == us.size() && us.size() == vs.size(),
              "mt_sn_power: list sizes");
-  SnPlan& p = get_plan(weights, us, vs);
+  IAMD_CHECK(shadows.empty() || shadows.size() == weights.size(), "mt_sn_power: shadow list size");
+  SnPlan& p = get_plan(weights, us, vs, shadows);
   auto fopt = weights[0].options().dtype(at::kFloat);
   auto sigma = at::empty({p.L}, fopt);
   auto scal = at::empty({p.L, 4}, fopt);
@@ -349,6 +393,8 @@ constexpr int kScChunk = 256 * 8 * 8;
 
 struct ScEntry {
   const float* W;
+  const __hip_bfloat16* Wb;  // read this bf16 copy of W instead (shadow), or
+  __hip_bfloat16* Ws;        // write bf16(W) here too (refresh the shadow)
   int64_t numel;
   int64_t off;
   int64_t vec;  // W 16-byte aligned: vector path
@@ -364,19 +410,33 @@ __global__ void __launch_bounds__(kT) sn_scale_cast(const ScEntry* __restrict__ 
   const int64_t start = (int64_t)chunk * kScChunk;
   const int64_t end = min(e.numel, start + (int64_t)kScChunk);
   __hip_bfloat16* o = out + e.off;  // 16-B aligned (offsets are multiples of 8 elements)
-  if (e.vec) {  // 8 elements per lane per trip: two 16-B fp32 loads, one 16-B bf16 store
+  auto wat = [&](int64_t i) { return e.Wb ? __bfloat162float(e.Wb[i]) : e.W[i]; };
+  if (e.vec) {  // 8 elements per lane per trip: two 16-B fp32 (or one bf16) loads, 16-B stores
     const int64_t vend = start + ((end - start) & ~(int64_t)7);
     for (int64_t i = start + threadIdx.x * 8; i < vend; i += kT * 8) {
       float v[8];
-      load_vec<float, 4>(e.W + i, *reinterpret_cast<float(*)[4]>(v));
-      load_vec<float, 4>(e.W + i + 4, *reinterpret_cast<float(*)[4]>(v + 4));
+      if (e.Wb) {
+        load_vec<__hip_bfloat16, 8>(e.Wb + i, v);
+      } else {
+        load_vec<float, 4>(e.W + i, *reinterpret_cast<float(*)[4]>(v));
+        load_vec<float, 4>(e.W + i + 4, *reinterpret_cast<float(*)[4]>(v + 4));
+        if (e.Ws) store_vec<__hip_bfloat16, 8>(e.Ws + i, v);
+      }
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] *= inv;
       store_vec<__hip_bfloat16, 8>(o + i, v);
     }
-    for (int64_t i = vend + threadIdx.x; i < end; i += kT) o[i] = __float2bfloat16(e.W[i] * inv);
+    for (int64_t i = vend + threadIdx.x; i < end; i += kT) {
+      const float w = wat(i);
+      if (e.Ws) e.Ws[i] = __float2bfloat16(w);
+      o[i] = __float2bfloat16(w * inv);
+    }
   } else {
-    for (int64_t i = start + threadIdx.x; i < end; i += kT) o[i] = __float2bfloat16(e.W[i] * inv);
+    for (int64_t i = start + threadIdx.x; i < end; i += kT) {
+      const float w = wat(i);
+      if (e.Ws) e.Ws[i] = __float2bfloat16(w);
+      o[i] = __float2bfloat16(w * inv);
+    }
   }
 }
 
@@ -389,10 +449,12 @@ struct ScPlan {
 std::mutex g_sc_mu;
 std::unordered_map<uint64_t, ScPlan> g_sc_cache;
 
-ScPlan& get_sc_plan(const std::vector<at::Tensor>& W) {
-  uint64_t h = 0x2545F4914F6CDD1DULL;
+// mode 0: read fp32 W; 1: read the bf16 shadows; 2: read fp32 W and write the shadows too
+ScPlan& get_sc_plan(const std::vector<at::Tensor>& W, const std::vector<at::Tensor>& S, int mode) {
+  uint64_t h = 0x2545F4914F6CDD1DULL ^ (uint64_t)(mode * 0x9E3779B1);
   for (auto& w : W) h ^= reinterpret_cast<uint64_t>(w.data_ptr()) + 0x9e3779b97f4a7c15ULL +
                         (h << 6) + (h >> 2) + (uint64_t)w.numel();
+  for (auto& t : S) h ^= reinterpret_cast<uint64_t>(t.data_ptr()) * 0x100000001b3ULL + (h << 7);
   std::lock_guard<std::mutex> lk(g_sc_mu);
   auto it = g_sc_cache.find(h);
   if (it != g_sc_cache.end()) return it->second;
@@ -403,7 +465,17 @@ ScPlan& get_sc_plan(const std::vector<at::Tensor>& W) {
   for (size_t i = 0; i < W.size(); ++i) {
     IAMD_CHECK(W[i].scalar_type() == at::kFloat && W[i].is_non_overlapping_and_dense(),
                "mt_sn_scale_cast: weights must be dense fp32");
-    ents.push_back({W[i].data_ptr<float>(), W[i].numel(), off,
+    const __hip_bfloat16* wb = nullptr;
+    __hip_bfloat16* ws = nullptr;
+    if (mode) {
+      IAMD_CHECK(S[i].scalar_type() == at::kBFloat16 && S[i].sizes() == W[i].sizes() &&
+                     S[i].strides() == W[i].strides() &&
+                     (reinterpret_cast<uintptr_t>(S[i].data_ptr()) & 15) == 0,
+                 "mt_sn_scale_cast: a shadow must be laid out like its weight, 16-B aligned");
+      if (mode == 1) wb = reinterpret_cast<const __hip_bfloat16*>(S[i].data_ptr());
+      else ws = reinterpret_cast<__hip_bfloat16*>(S[i].data_ptr());
+    }
+    ents.push_back({W[i].data_ptr<float>(), wb, ws, W[i].numel(), off,
                     (int64_t)((reinterpret_cast<uintptr_t>(W[i].data_ptr()) & 15) == 0)});
     p.offs.push_back(off);
     const int64_t nch = (W[i].numel() + kScChunk - 1) / kScChunk;
@@ -424,12 +496,18 @@ ScPlan& get_sc_plan(const std::vector<at::Tensor>& W) {
 
 }  // namespace
 
+// shadows (optional): bf16 copies of the weights; shadow_mode 1 reads them instead of the fp32
+// weights, 2 writes them (bf16(W)) in the same pass.
 std::vector<at::Tensor> mt_sn_scale_cast(const std::vector<at::Tensor>& weights,
-                                         const at::Tensor& sigma) {
+                                         const at::Tensor& sigma,
+                                         const std::vector<at::Tensor>& shadows,
+                                         int64_t shadow_mode) {
   IAMD_CHECK(!weights.empty() && sigma.numel() == (int64_t)weights.size() &&
                  sigma.scalar_type() == at::kFloat,
              "mt_sn_scale_cast: sigma must be fp32 [L]");
-  ScPlan& p = get_sc_plan(weights);
+  IAMD_CHECK(shadow_mode == 0 || shadows.size() == weights.size(),
+             "mt_sn_scale_cast: shadow list size");
+  ScPlan& p = get_sc_plan(weights, shadows, shadow_mode == 0 ? 0 : (int)shadow_mode);
   auto flat = at::empty({p.total}, weights[0].options().dtype(at::kBFloat16));
   hipLaunchKernelGGL(sn_scale_cast, dim3(p.nblocks), dim3(kT), 0, stream(),
                      reinterpret_cast<const ScEntry*>(p.ents.data_ptr()),
@@ -458,9 +536,17 @@ namespace {
 
 constexpr int kSnbT = 256;
 
-template <typename G>
+__device__ __forceinline__ void load_w8(const float* p, float (&v)[8]) {
+  load_vec<float, 4>(p, *reinterpret_cast<float(*)[4]>(v));
+  load_vec<float, 4>(p + 4, *reinterpret_cast<float(*)[4]>(v + 4));
+}
+__device__ __forceinline__ void load_w8(const __hip_bfloat16* p, float (&v)[8]) {
+  load_vec<__hip_bfloat16, 8>(p, v);
+}
+
+template <typename G, typename WT>
 __global__ void __launch_bounds__(kSnbT)
-snb_reduce(const G* __restrict__ g, const float* __restrict__ W, int64_t n,
+snb_reduce(const G* __restrict__ g, const WT* __restrict__ W, int64_t n,
            const float* __restrict__ v, float* __restrict__ vm, int64_t w, int64_t cl_cin,
            int64_t cl_khw, float* __restrict__ partial) {
   __shared__ float sh[kSnbT / 64];
@@ -481,12 +567,10 @@ snb_reduce(const G* __restrict__ g, const float* __restrict__ W, int64_t n,
       const bool two = j < n;
       float gv[2][8], wv[2][8];
       load_vec<G, 8>(g + i, gv[0]);
-      load_vec<float, 4>(W + i, *reinterpret_cast<float(*)[4]>(wv[0]));
-      load_vec<float, 4>(W + i + 4, *reinterpret_cast<float(*)[4]>(wv[0] + 4));
+      load_w8(W + i, wv[0]);
       if (two) {
         load_vec<G, 8>(g + j, gv[1]);
-        load_vec<float, 4>(W + j, *reinterpret_cast<float(*)[4]>(wv[1]));
-        load_vec<float, 4>(W + j + 4, *reinterpret_cast<float(*)[4]>(wv[1] + 4));
+        load_w8(W + j, wv[1]);
       } else {
 #pragma unroll
         for (int k = 0; k < 8; ++k) gv[1][k] = wv[1][k] = 0.f;
@@ -497,7 +581,7 @@ snb_reduce(const G* __restrict__ g, const float* __restrict__ W, int64_t n,
       for (int k = 0; k < 8; ++k) acc = fmaf(gv[1][k], wv[1][k], acc);
     }
   } else {
-    for (int64_t i = gtid; i < n; i += gsz) acc = fmaf(to_f<G>(g[i]), W[i], acc);
+    for (int64_t i = gtid; i < n; i += gsz) acc = fmaf(to_f<G>(g[i]), to_f<WT>(W[i]), acc);
   }
   acc = wave_sum(acc);
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
@@ -505,6 +589,7 @@ snb_reduce(const G* __restrict__ g, const float* __restrict__ W, int64_t n,
   if (threadIdx.x == 0) {
     float s = 0.f;
     for (int k = 0; k < kSnbT / 64; ++k) s += sh[k];
+    // a bf16 W read is the shadow bf16(W), already the weight itself: no rescale needed
     partial[blockIdx.x] = s;
   }
 }
@@ -554,8 +639,11 @@ snb_apply(const G* __restrict__ g, const float* __restrict__ u, const float* __r
 
 }  // namespace
 
+// shadow (optional, may be undefined / empty): bf16(W) laid out like W, read instead of the fp32
+// weight for the <G, W> reduction (half the bytes of that pass)
 at::Tensor sn_scale_backward(const at::Tensor& grad_in, const at::Tensor& weight,
-                             const at::Tensor& u, const at::Tensor& v, const at::Tensor& sigma) {
+                             const at::Tensor& u, const at::Tensor& v, const at::Tensor& sigma,
+                             const c10::optional<at::Tensor>& shadow) {
   IAMD_CHECK(weight.is_cuda() && weight.scalar_type() == at::kFloat, "sn_scale_backward: fp32 W");
   IAMD_CHECK(u.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat &&
                  sigma.scalar_type() == at::kFloat && sigma.numel() >= 1,
@@ -580,11 +668,21 @@ at::Tensor sn_scale_backward(const at::Tensor& grad_in, const at::Tensor& weight
                           ? (int)std::max<int64_t>(1, std::min<int64_t>(4096, (n + 2047) / 2048))
                           : (int)std::max<int64_t>(1, std::min<int64_t>(h, 1024));
   hipStream_t st = stream();
+  const bool use_shadow = shadow.has_value() && shadow->defined() && shadow->numel() == n;
+  if (use_shadow)
+    IAMD_CHECK(shadow->scalar_type() == at::kBFloat16 && shadow->strides() == weight.strides() &&
+                   (reinterpret_cast<uintptr_t>(shadow->data_ptr()) & 15) == 0,
+               "sn_scale_backward: the shadow must be bf16, laid out like W, 16-B aligned");
   auto run = [&](auto* gp) {
     using G = std::remove_const_t<std::remove_pointer_t<decltype(gp)>>;
-    hipLaunchKernelGGL((snb_reduce<G>), dim3(P), dim3(kSnbT), 0, st, gp,
-                       weight.data_ptr<float>(), n, v.data_ptr<float>(), vm, w, cl_cin, cl_khw,
-                       partial);
+    if (use_shadow)
+      hipLaunchKernelGGL((snb_reduce<G, __hip_bfloat16>), dim3(P), dim3(kSnbT), 0, st, gp,
+                         reinterpret_cast<const __hip_bfloat16*>(shadow->data_ptr()), n,
+                         v.data_ptr<float>(), vm, w, cl_cin, cl_khw, partial);
+    else
+      hipLaunchKernelGGL((snb_reduce<G, float>), dim3(P), dim3(kSnbT), 0, st, gp,
+                         weight.data_ptr<float>(), n, v.data_ptr<float>(), vm, w, cl_cin, cl_khw,
+                         partial);
     hipLaunchKernelGGL((snb_apply<G>), dim3(ablocks), dim3(kSnbT), 0, st, gp,
                        u.data_ptr<float>(), vm, sigma.data_ptr<float>(), partial, P,
                        dw.data_ptr<float>(), h, w);

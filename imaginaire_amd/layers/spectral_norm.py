@@ -32,6 +32,9 @@ from imaginaire_amd.ops import _ext
 
 # IMAGINAIRE_AMD_SN_FLIP=0: each conv flips its own weight for the data gradient
 _SN_FLIP = os.environ.get('IMAGINAIRE_AMD_SN_FLIP', '1') == '1'
+# IMAGINAIRE_AMD_SN_SHADOW=0: the power iteration and the W / sigma cast read the fp32 weights
+# (default: a bf16 copy of each weight that the optimizer step writes in its own pass)
+_SN_SHADOW = os.environ.get('IMAGINAIRE_AMD_SN_SHADOW', '1') == '1'
 
 
 class _SNScale(torch.autograd.Function):
@@ -47,7 +50,9 @@ class _SNScale(torch.autograd.Function):
         weight, u, v, sigma = ctx.saved_tensors
         if _ext.use_native(weight) and weight.dtype == torch.float32 and \
                 grad.dtype in (torch.float32, torch.bfloat16):
-            return _ext.ext().sn_scale_backward(grad, weight, u, v, sigma), None, None, None
+            # <G, W> reads the bf16 shadow of W when the forward had one (half the bytes)
+            return _ext.ext().sn_scale_backward(grad, weight, u, v, sigma,
+                                                getattr(ctx, 'shadow', None)), None, None, None
         g = grad.float()
         dot = (g * weight).sum()
         outer = torch.outer(u, v).view(weight.shape)
@@ -61,13 +66,18 @@ class _SNScaleCast(torch.autograd.Function):
     so autocast's per-layer divide + cast disappear from the forward."""
 
     @staticmethod
-    def forward(ctx, weight, u, v, sigma, w16):
+    def forward(ctx, weight, u, v, sigma, w16, shadow=None):
         ctx.save_for_backward(weight, u, v, sigma)
+        ctx.shadow = shadow  # bf16(W) (the optimizer keeps it in sync), or None
         return w16
 
     @staticmethod
     def backward(ctx, grad):
-        return _SNScale.backward(ctx, grad) + (None,)
+        return _SNScale.backward(ctx, grad) + (None, None)
+
+
+def w_shape(w):
+    return tuple(w.shape)
 
 
 def _autocast_bf16(dev):
@@ -80,9 +90,9 @@ class SpectralNorm(_TorchSN):
         if batched is not None:
             self._batched = None  # consumed: a second call this forward iterates itself
             weight = getattr(module, self.name + '_orig')
-            u, v, sigma, w16 = batched
+            u, v, sigma, w16, shadow = batched
             if w16 is not None and _autocast_bf16(weight.device.type):
-                return _SNScaleCast.apply(weight, u, v, sigma, w16)
+                return _SNScaleCast.apply(weight, u, v, sigma, w16, shadow)
             return _SNScale.apply(weight, u, v, sigma)
         dev = getattr(module, self.name + '_orig').device.type
         with torch.autocast(device_type=dev, enabled=False):
@@ -164,22 +174,60 @@ class _SNGroup:
             vs.append(getattr(m, h.name + '_v'))
         if any(w.dtype != torch.float32 for w in ws):
             return
+        X = _ext.ext()
+        eps = float(self.entries[0][1].eps)
+        bf16 = _autocast_bf16(w0.device.type)
         with torch.no_grad():
-            sigma = _ext.ext().mt_sn_power(ws, us, vs, bool(net.training),
-                                           float(self.entries[0][1].eps))
+            shadows = self._shadows(ws) if (bf16 and net.training and _SN_SHADOW) else None
+            if shadows is not None:
+                # the optimizer's step writes bf16(W) with the update: the GEMV passes and the
+                # W / sigma cast read half the bytes. Stale shadows (first step, a loaded or
+                # restored state) are refreshed first, so the result depends on W alone —
+                # an eager step and a graph replay from the same state agree bitwise.
+                self._sync_stale(ws)
+                sigma = X.mt_sn_power(ws, us, vs, True, eps, shadows)
+                w16 = X.mt_sn_scale_cast(ws, sigma, shadows, 1)
+            else:
+                sigma = X.mt_sn_power(ws, us, vs, bool(net.training), eps)
+                w16 = X.mt_sn_scale_cast(ws, sigma) if bf16 else [None] * len(ws)
             # snapshots of u, v for the backward (the next forward updates them in place)
             u_all = torch.cat(us)
             v_all = torch.cat(vs)
-            w16 = (_ext.ext().mt_sn_scale_cast(ws, sigma)
-                   if _autocast_bf16(w0.device.type) else [None] * len(ws))
         if w16[0] is not None and torch.is_grad_enabled() and net.training and _SN_FLIP:
             self._flip_for_dgrad(w16)
         ou = ov = 0
         for i, (m, h) in enumerate(self.entries):
             nu, nv = us[i].numel(), vs[i].numel()
-            h._batched = (u_all[ou:ou + nu], v_all[ov:ov + nv], sigma[i], w16[i])
+            h._batched = (u_all[ou:ou + nu], v_all[ov:ov + nv], sigma[i], w16[i],
+                          shadows[i] if shadows is not None else None)
             ou += nu
             ov += nv
+
+    def _shadows(self, ws):
+        """bf16 copies of the group's weights, one per parameter and shared by every group that
+        holds it (optimizers/fused_adam.py registry), each laid out like its weight; the missing
+        ones are allocated together, outside graph capture. None when unavailable."""
+        from imaginaire_amd.optimizers import fused_adam as FA
+        out = [FA.shadow_of(w) for w in ws]
+        missing = [i for i, t in enumerate(out)
+                   if t is None or t.shape != w_shape(ws[i]) or t.stride() != ws[i].stride()]
+        if missing:
+            if torch.cuda.is_current_stream_capturing():
+                return None
+            offs, tot = [], 0
+            for i in missing:
+                offs.append(tot)
+                tot += (ws[i].numel() + 7) // 8 * 8  # 16-byte aligned views
+            flat = torch.empty(tot, dtype=torch.bfloat16, device=ws[0].device)
+            for i, o in zip(missing, offs):
+                out[i] = flat.as_strided(ws[i].shape, ws[i].stride(), o)
+                FA.register_shadow(ws[i], out[i])
+        return out
+
+    @staticmethod
+    def _sync_stale(ws):
+        from imaginaire_amd.optimizers import fused_adam as FA
+        FA.sync_shadows([w for w in ws if not FA.shadow_synced(w)])
 
     def _flip_for_dgrad(self, w16):
         """The flipped, transposed bf16 copies of every stride-1 conv weight of the group, for

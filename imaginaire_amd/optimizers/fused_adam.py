@@ -14,11 +14,79 @@ unchanged. States written by torch ``Adam`` (per-parameter ``'step'``) are
 accepted too: the group step is taken from them when the group has none.
 """
 import math
+import weakref
 
 import torch
 from torch.optim import Optimizer
 
 from imaginaire_amd.ops import _ext
+
+# A parameter may carry a bf16 copy that the native step keeps in sync with it (the
+# spectral-norm group's shadow weights, layers/spectral_norm.py), written in the same pass as the
+# update. Stored as attributes of the parameter itself (tensors hash by identity but compare
+# elementwise, so they make poor weak-dictionary keys).
+
+
+_SHADOWED = {}  # id(param) -> weakref(param): every parameter that has a shadow
+
+
+def register_shadow(param, shadow):
+    """Have every native step of the optimizer owning ``param`` also write ``bf16(param)`` into
+    ``shadow`` (same shape and strides); ``None`` unregisters."""
+    param._iamd_shadow = shadow
+    param._iamd_shadow_sync = None
+    if shadow is None:
+        _SHADOWED.pop(id(param), None)
+    else:
+        _SHADOWED[id(param)] = weakref.ref(param)
+
+
+@torch.no_grad()
+def sync_shadows(params):
+    """shadow <- bf16(param) for each of ``params`` (one multi-tensor copy) and mark them synced."""
+    if not params:
+        return
+    torch._foreach_copy_([shadow_of(p) for p in params], list(params))
+    for p in params:
+        p._iamd_shadow_sync = p._version
+
+
+@torch.no_grad()
+def resync_shadows():
+    """Rewrite the shadow of every parameter changed since its shadow was last synced (a loaded
+    checkpoint, a restored snapshot, any in-place write outside the native step). Eager forwards
+    notice such writes themselves (:func:`shadow_synced`); a replayed graph cannot — its
+    spectral-norm kernels read the shadows unconditionally — so graph replays call this first
+    (utils/cuda_graph.py). A few microseconds of host work when nothing changed."""
+    stale = []
+    for key, ref in list(_SHADOWED.items()):
+        p = ref()
+        if p is None:
+            del _SHADOWED[key]
+            continue
+        v = getattr(p, '_iamd_shadow_sync', None)
+        if shadow_of(p) is None or v is None or v == p._version:
+            continue  # never synced (its first forward writes it) or still in sync
+        stale.append(p)
+    sync_shadows(stale)
+    return len(stale)
+
+
+def shadow_of(param):
+    return getattr(param, '_iamd_shadow', None)
+
+
+def mark_shadow_synced(param):
+    """``shadow_of(param)`` was just written from ``param``."""
+    param._iamd_shadow_sync = param._version
+
+
+def shadow_synced(param):
+    """The shadow holds bf16(param): written from it and the parameter untouched since, or
+    changed only by native optimizer steps (which rewrite the shadow in the same pass and do not
+    bump the version counter; every other in-place write does)."""
+    v = getattr(param, '_iamd_shadow_sync', None)
+    return v is not None and v == param._version and shadow_of(param) is not None
 
 
 class FusedAdam(Optimizer):
@@ -132,8 +200,13 @@ class FusedAdam(Optimizer):
                 gl = [g if (g.dtype == gdt and g.stride() == p.stride())
                       else torch.empty_like(p, dtype=gdt).copy_(g)
                       for g, p in zip(grads, params)]
-                _ext.ext().mt_adam(params, gl, m, v, [], lr, beta1, beta2, eps, int(step), wd,
-                                   bool(adamw), 1.0, hyper)
+                shadows = []
+                sh = [shadow_of(p) for p in params]
+                if any(t is not None for t in sh):
+                    none = params[0].new_empty(0, dtype=torch.bfloat16)
+                    shadows = [t if t is not None else none for t in sh]
+                _ext.ext().mt_adam(params, gl, m, v, shadows, lr, beta1, beta2, eps, int(step),
+                                   wd, bool(adamw), 1.0, hyper)
             else:
                 _reference_adam(params, grads, m, v, lr, beta1, beta2, eps, step, wd, adamw)
         return loss

@@ -157,6 +157,14 @@ def _signature(x):
         return ('V', repr(x))
 
 
+def _resync_shadows():
+    """bf16 shadow weights (optimizers/fused_adam.py) of parameters written outside the graph
+    since the last replay — a restored snapshot, a loaded checkpoint — are refreshed before the
+    replay reads them."""
+    from imaginaire_amd.optimizers import fused_adam
+    fused_adam.resync_shadows()
+
+
 class graph_routing(object):
     """Kernel routing of a graphed step, for its warm-up, its capture and any eager run compared
     against its replay: every conv k10 / k11 can run takes them, whatever its grid size or
@@ -244,6 +252,7 @@ class GraphedStep(object):
         self._last = ent
         if ent['graph'] is not None:
             _static_copy(ent['static'], data)
+            _resync_shadows()
             if self.pre_replay:
                 self.pre_replay()
             ent['graph'].replay()
@@ -311,6 +320,7 @@ class GraphedStep(object):
             self.name, sum(1 for e in self.entries.values() if e['graph'] is not None),
             self.capture_s))
         # the capture itself executed nothing: run this iteration as the first replay
+        _resync_shadows()
         if self.pre_replay:
             self.pre_replay()
         g.replay()

@@ -154,18 +154,20 @@ class ModelAverage(nn.Module):
             torch._foreach_copy_(self._ints[0], self._ints[1])
 
     def copy_t2s(self):
+        # (state_dict tensors share their parameter's version counter: the in-place copy is
+        # visible to version checks — e.g. the spectral-norm group's bf16 shadow weights)
         target_dict = self.module.state_dict()
         source_dict = self.averaged_model.state_dict()
         with torch.no_grad():
             for key in source_dict:
-                target_dict[key].data.copy_(source_dict[key].data)
+                target_dict[key].copy_(source_dict[key])
 
     def copy_s2t(self):
         source_dict = self.module.state_dict()
         target_dict = self.averaged_model.state_dict()
         with torch.no_grad():
             for key in source_dict:
-                target_dict[key].data.copy_(source_dict[key].data)
+                target_dict[key].copy_(source_dict[key])
 
     def __repr__(self):
         return self.module.__repr__()

@@ -373,9 +373,18 @@ def test_sn_scale_cast_under_bf16_autocast():
     net = net.to(memory_format=torch.channels_last)
     assert install_batched_spectral_norm(net) == 3
     x = torch.randn(4, 6, 6, 6, device='cuda')
-    with torch.autocast('cuda', dtype=torch.bfloat16):
-        y_ref = ref(x)
-        y = net(x.contiguous(memory_format=torch.channels_last))
+    # the fp32-W cast under test: the shadow path's bf16(bf16(W)/σ) (one extra rounding, tested
+    # in test_spectral_norm_bf16_shadow_weights) flips the LeakyReLU slope of a few near-zero
+    # activations of this tiny net, beyond this test's elementwise gradient tolerance
+    from imaginaire_amd.layers import spectral_norm as snm
+    old = snm._SN_SHADOW
+    snm._SN_SHADOW = False
+    try:
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            y_ref = ref(x)
+            y = net(x.contiguous(memory_format=torch.channels_last))
+    finally:
+        snm._SN_SHADOW = old
     assert y.dtype == torch.bfloat16
     torch.testing.assert_close(y.float(), y_ref.float(), atol=3e-2, rtol=3e-2)
     g = torch.randn_like(y)
@@ -1630,3 +1639,101 @@ def test_conv_kernels_never_read_unwritten_lds(case, ver):
     for name, a, b in zip(('y', 'dw', 'dx'), outs[0], outs[1]):
         assert torch.isfinite(b.float()).all(), name
         assert torch.equal(a, b), name
+
+
+def test_spectral_norm_bf16_shadow_weights():
+    """Under bf16 autocast the batched spectral norm reads bf16 shadow copies of the weights
+    that the native FusedAdam step writes in its update pass: sigma and W / sigma match the fp32
+    path (IMAGINAIRE_AMD_SN_SHADOW=0 semantics) to bf16 tolerance before and after optimizer
+    steps, the shadow equals bf16(W) after every step, and an in-place write to a weight outside
+    the optimizer invalidates it (the next forward rewrites it)."""
+    from torch import nn
+    from imaginaire_amd.layers import spectral_norm as snm
+    from imaginaire_amd.optimizers import fused_adam as FA
+    torch.manual_seed(26)
+    cl = torch.channels_last
+
+    def make():
+        return nn.Sequential(snm.spectral_norm(nn.Conv2d(64, 128, 3, padding=1)), nn.LeakyReLU(0.2),
+                             snm.spectral_norm(nn.Conv2d(128, 64, 5, padding=2)))
+    net = make().cuda().to(memory_format=cl)
+    ref = make().cuda().to(memory_format=cl)
+    ref.load_state_dict(net.state_dict())
+    snm.install_batched_spectral_norm(net)
+    snm.install_batched_spectral_norm(ref)
+    opt = FA.FusedAdam(net.parameters(), lr=1e-3)
+    x = torch.randn(2, 64, 16, 32, device='cuda').contiguous(memory_format=cl)
+    convs = [net[0], net[2]]
+    rconvs = [ref[0], ref[2]]
+    old = snm._SN_SHADOW
+    try:
+        for it in range(4):
+            if it == 3:
+                with torch.no_grad():
+                    net[0].weight_orig.add_(1e-3)   # outside the optimizer: bumps _version
+                    ref[0].weight_orig.add_(1e-3)
+            with torch.autocast('cuda', dtype=torch.bfloat16):
+                snm._SN_SHADOW = True
+                y = net(x)
+                snm._SN_SHADOW = False
+                y_ref = ref(x)
+            for c, rc in zip(convs, rconvs):
+                w = c.weight_orig
+                sh = FA.shadow_of(w)
+                assert sh is not None and torch.equal(sh, w.to(torch.bfloat16)), it
+                assert torch.allclose(c.weight_u, rc.weight_u, atol=2e-3, rtol=2e-2), it
+            assert (y.float() - y_ref.float()).abs().max() <= 3e-2 * y_ref.float().abs().max(), it
+            g = torch.randn_like(y)
+            opt.zero_grad()
+            y.backward(g)
+            opt.step()
+            with torch.no_grad():  # the reference follows the shadowed net's weights
+                for p, rp in zip(net.parameters(), ref.parameters()):
+                    rp.copy_(p)
+    finally:
+        snm._SN_SHADOW = old
+
+
+@pytest.mark.gpu
+def test_spectral_norm_shadow_result_depends_on_weights_only():
+    """A forward reading shadows the optimizer wrote and a forward after the same weights were
+    restored from a snapshot (shadows refreshed from W) give bitwise-equal outputs: an eager
+    step and a graph replay from one state agree (utils/cuda_graph.py resyncs before replays)."""
+    from torch import nn
+    from imaginaire_amd.layers import spectral_norm as snm
+    from imaginaire_amd.optimizers import fused_adam as FA
+    torch.manual_seed(27)
+    cl = torch.channels_last
+    net = nn.Sequential(snm.spectral_norm(nn.Conv2d(64, 128, 3, padding=1)), nn.LeakyReLU(0.2),
+                        snm.spectral_norm(nn.Conv2d(128, 64, 5, padding=2))).cuda().to(
+                            memory_format=cl)
+    snm.install_batched_spectral_norm(net)
+    opt = FA.FusedAdam(net.parameters(), lr=1e-3)
+    x = torch.randn(2, 64, 16, 32, device='cuda').contiguous(memory_format=cl)
+    old = snm._SN_SHADOW
+    snm._SN_SHADOW = True
+    try:
+        for _ in range(2):
+            with torch.autocast('cuda', dtype=torch.bfloat16):
+                y = net(x)
+            opt.zero_grad()
+            y.float().pow(2).mean().backward()
+            opt.step()
+        bufs = [b.detach().clone() for b in net.buffers()]
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            y1 = net(x)  # shadows written by the optimizer step
+        with torch.no_grad():
+            for b, c in zip(net.buffers(), bufs):
+                b.copy_(c)
+            for p in net.parameters():
+                p.copy_(p.detach().clone())  # same values, version bumped: shadows stale
+            for m in (net[0], net[2]):
+                FA.shadow_of(m.weight_orig).zero_()
+        assert FA.resync_shadows() == 2  # what a graph replay does first
+        for m in (net[0], net[2]):
+            assert torch.equal(FA.shadow_of(m.weight_orig), m.weight_orig.to(torch.bfloat16))
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            y2 = net(x)
+        assert torch.equal(y1, y2)
+    finally:
+        snm._SN_SHADOW = old
