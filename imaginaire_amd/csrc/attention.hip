@@ -1,0 +1,443 @@
+// k16: fused few-shot attention  O = softmax_keys(scale * Q K^T) V   (bf16 in / out, fp32 inside)
+//
+// The fs_vid2vid reference-frame attention (reference generators/fs_vid2vid.py:944-951: energy
+// = bmm(key^T, query), softmax over the K*HW reference positions, bmm with the features) without
+// the B x KHW x HW energy / attention matrices in HBM: one forward kernel with an online softmax
+// (flash-attention style) that also writes the per-query log-sum-exp, and two backward kernels
+// that recompute the probabilities from it (one owns key blocks and accumulates dK, dV; one owns
+// query blocks and accumulates dQ — no atomics, deterministic).
+//
+// MFMA v_mfma_f32_16x16x32_bf16 throughout, 64-wide waves, 16 queries (or keys) per wave, 4 waves
+// per workgroup sharing LDS tiles. Layout trick: scores are computed TRANSPOSED where the next
+// product needs the probabilities as its B operand — the C layout of one 16x16 tile (lane l holds
+// rows 4*(l/16)+e, column l%16) then feeds the B operand of the next MFMA directly (column l%16,
+// k = 8*(l/16)+t) once the 32-long k dimension is taken in the order {tile 0: rows 4g..4g+3,
+// tile 1: rows 4g..4g+3}; the A operand of that MFMA reads its LDS tile in the same order (two
+// 8-byte reads). Per-query softmax statistics stay per lane (the query is the lane's column);
+// only the running max needs a 4-lane reduction (xor 16, 32).
+//
+// Shapes: q [B, Lq, D], k [B, Lk, D], v [B, Lk, DV] contiguous bf16; D in {32, 64, 128}, DV a
+// multiple of 32 up to 256 (the caller zero-pads: zero columns change no dot product), Lq and Lk
+// multiples of 64. Scores in the log2 domain: p = exp2(s * scale * log2(e) - lse2).
+#include "common.h"
+
+#include <cmath>
+
+namespace iamd {
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+constexpr int kAttnT = 256;  // 4 waves
+constexpr float kNegBig = -1.0e30f;
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ bf16x8 join4(const bf16x4& lo, const bf16x4& hi) {
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+__device__ __forceinline__ bf16x8 pack8(const float (&lo)[4], const float (&hi)[4]) {
+  bf16x8 r;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    r[t] = (__bf16)lo[t];
+    r[4 + t] = (__bf16)hi[t];
+  }
+  return r;
+}
+
+// A operand of a 32-deep product whose k index runs over two 16-row tiles (rows 4g..4g+3 of
+// each): two 8-byte LDS reads from a row-major [row][k] tile (row = the lane's A row).
+__device__ __forceinline__ bf16x8 read_a_split(const __bf16* row, int g) {
+  return join4(*reinterpret_cast<const bf16x4*>(row + g * 4),
+               *reinterpret_cast<const bf16x4*>(row + 16 + g * 4));
+}
+
+// ---- forward -----------------------------------------------------------------------------
+// workgroup: 64 queries (wave w: queries 16w..16w+15) x all keys in blocks of 64 staged in LDS
+// (K row-major, V transposed). Per block and wave: S^T (4 key tiles x D/32 MFMAs), the online
+// softmax, O^T += V^T P^T (DV/16 tiles x 2 MFMAs).
+template <int D, int DV>
+__global__ __launch_bounds__(kAttnT) void attn_fwd_kernel(
+    const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v,
+    __bf16* __restrict__ o, float* __restrict__ lse2, int Lq, int Lk, float sl2) {
+  constexpr int KB = 64, KP = D + 8, VP = KB + 8;
+  __shared__ __attribute__((aligned(16))) __bf16 Ks[KB * KP];
+  __shared__ __attribute__((aligned(16))) __bf16 Vt[DV * VP];
+  const int b = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int l16 = lane & 15, g = lane >> 4;
+  const int qi = blockIdx.x * 64 + wid * 16 + l16;  // this lane's query (the B/C column)
+  const __bf16* kb = k + (int64_t)b * Lk * D;
+  const __bf16* vb = v + (int64_t)b * Lk * DV;
+  bf16x8 qf[D / 32];
+#pragma unroll
+  for (int ks = 0; ks < D / 32; ++ks)
+    qf[ks] = *reinterpret_cast<const bf16x8*>(q + ((int64_t)b * Lq + qi) * D + ks * 32 + g * 8);
+  f32x4 acc[DV / 16];
+#pragma unroll
+  for (int i = 0; i < DV / 16; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = kNegBig, lsum = 0.f;
+  for (int k0 = 0; k0 < Lk; k0 += KB) {
+    __syncthreads();
+    for (int e = tid; e < KB * D / 8; e += kAttnT) {
+      const int r = e / (D / 8), c = (e - r * (D / 8)) * 8;
+      *reinterpret_cast<bf16x8*>(&Ks[r * KP + c]) =
+          *reinterpret_cast<const bf16x8*>(kb + (int64_t)(k0 + r) * D + c);
+    }
+    for (int e = tid; e < KB * DV / 8; e += kAttnT) {
+      const int r = e / (DV / 8), c = (e - r * (DV / 8)) * 8;
+      const bf16x8 x = *reinterpret_cast<const bf16x8*>(vb + (int64_t)(k0 + r) * DV + c);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) Vt[(c + t) * VP + r] = x[t];
+    }
+    __syncthreads();
+    f32x4 s[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < D / 32; ++ks)
+        s[kt] = mfma16(*reinterpret_cast<const bf16x8*>(&Ks[(kt * 16 + l16) * KP + ks * 32 + g * 8]),
+                       qf[ks], s[kt]);
+    }
+    // s[kt][e] = score of query qi and key k0 + 16 kt + 4 g + e
+    float mx = m;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) mx = fmaxf(mx, s[kt][e] * sl2);
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float alpha = exp2f(m - mx);
+    m = mx;
+    float p[4][4];
+    float ps = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        p[kt][e] = exp2f(fmaf(s[kt][e], sl2, -mx));
+        ps += p[kt][e];
+      }
+    lsum = fmaf(lsum, alpha, ps);
+#pragma unroll
+    for (int i = 0; i < DV / 16; ++i) acc[i] *= alpha;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const bf16x8 pb = pack8(p[2 * h], p[2 * h + 1]);
+#pragma unroll
+      for (int i = 0; i < DV / 16; ++i)
+        acc[i] = mfma16(read_a_split(&Vt[(i * 16 + l16) * VP + h * 32], g), pb, acc[i]);
+    }
+  }
+  lsum += __shfl_xor(lsum, 16);
+  lsum += __shfl_xor(lsum, 32);
+  const float inv = 1.f / lsum;
+  __bf16* orow = o + ((int64_t)b * Lq + qi) * DV;
+#pragma unroll
+  for (int i = 0; i < DV / 16; ++i) {
+    bf16x4 w;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) w[e] = (__bf16)(acc[i][e] * inv);
+    *reinterpret_cast<bf16x4*>(orow + i * 16 + g * 4) = w;
+  }
+  if (g == 0) lse2[(int64_t)b * Lq + qi] = m + log2f(lsum);
+}
+
+// ---- backward: dK, dV ----------------------------------------------------------------------
+// workgroup: 64 keys (wave w: keys 16w..16w+15, held in registers as B operands) x all queries
+// in blocks of 32 staged in LDS both row-major (A operands of S, dP) and transposed (A operands
+// of dV^T, dK^T). S = Q K^T and dP = dO V^T put the key in the lane's column, so P and dS feed
+// dV^T += dO^T P and dK^T += Q^T dS as B operands.
+template <int D, int DV>
+__global__ __launch_bounds__(kAttnT) void attn_bwd_dkv_kernel(
+    const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v,
+    const __bf16* __restrict__ dout, const float* __restrict__ lse2,
+    const float* __restrict__ dsum, __bf16* __restrict__ dk, __bf16* __restrict__ dv, int Lq,
+    int Lk, float sl2, float scale) {
+  constexpr int QB = 32, QP = D + 8, OP = DV + 8, TP = QB + 8;
+  __shared__ __attribute__((aligned(16))) __bf16 Qs[QB * QP];
+  __shared__ __attribute__((aligned(16))) __bf16 Qt[D * TP];
+  __shared__ __attribute__((aligned(16))) __bf16 Os[QB * OP];
+  __shared__ __attribute__((aligned(16))) __bf16 Ot[DV * TP];
+  __shared__ __attribute__((aligned(16))) float Ls[QB];
+  __shared__ __attribute__((aligned(16))) float Ds[QB];
+  const int b = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int l16 = lane & 15, g = lane >> 4;
+  const int ki = blockIdx.x * 64 + wid * 16 + l16;  // this lane's key (the B/C column)
+  const __bf16* qb = q + (int64_t)b * Lq * D;
+  const __bf16* ob = dout + (int64_t)b * Lq * DV;
+  bf16x8 kf[D / 32], vf[DV / 32];
+#pragma unroll
+  for (int ks = 0; ks < D / 32; ++ks)
+    kf[ks] = *reinterpret_cast<const bf16x8*>(k + ((int64_t)b * Lk + ki) * D + ks * 32 + g * 8);
+#pragma unroll
+  for (int ks = 0; ks < DV / 32; ++ks)
+    vf[ks] = *reinterpret_cast<const bf16x8*>(v + ((int64_t)b * Lk + ki) * DV + ks * 32 + g * 8);
+  f32x4 dkt[D / 16], dvt[DV / 16];
+#pragma unroll
+  for (int i = 0; i < D / 16; ++i) dkt[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < DV / 16; ++i) dvt[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int q0 = 0; q0 < Lq; q0 += QB) {
+    __syncthreads();
+    for (int e = tid; e < QB * D / 8; e += kAttnT) {
+      const int r = e / (D / 8), c = (e - r * (D / 8)) * 8;
+      const bf16x8 x = *reinterpret_cast<const bf16x8*>(qb + (int64_t)(q0 + r) * D + c);
+      *reinterpret_cast<bf16x8*>(&Qs[r * QP + c]) = x;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) Qt[(c + t) * TP + r] = x[t];
+    }
+    for (int e = tid; e < QB * DV / 8; e += kAttnT) {
+      const int r = e / (DV / 8), c = (e - r * (DV / 8)) * 8;
+      const bf16x8 x = *reinterpret_cast<const bf16x8*>(ob + (int64_t)(q0 + r) * DV + c);
+      *reinterpret_cast<bf16x8*>(&Os[r * OP + c]) = x;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) Ot[(c + t) * TP + r] = x[t];
+    }
+    if (tid < QB) {
+      Ls[tid] = lse2[(int64_t)b * Lq + q0 + tid];
+      Ds[tid] = dsum[(int64_t)b * Lq + q0 + tid];
+    }
+    __syncthreads();
+    float p[2][4], ds[2][4];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < D / 32; ++ks)
+        s = mfma16(*reinterpret_cast<const bf16x8*>(&Qs[(qt * 16 + l16) * QP + ks * 32 + g * 8]),
+                   kf[ks], s);
+#pragma unroll
+      for (int ks = 0; ks < DV / 32; ++ks)
+        dp = mfma16(*reinterpret_cast<const bf16x8*>(&Os[(qt * 16 + l16) * OP + ks * 32 + g * 8]),
+                    vf[ks], dp);
+      // s[e], dp[e]: query q0 + 16 qt + 4 g + e, key ki
+      const f32x4 lq = *reinterpret_cast<const f32x4*>(&Ls[qt * 16 + g * 4]);
+      const f32x4 dq = *reinterpret_cast<const f32x4*>(&Ds[qt * 16 + g * 4]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        p[qt][e] = exp2f(fmaf(s[e], sl2, -lq[e]));
+        ds[qt][e] = p[qt][e] * (dp[e] - dq[e]) * scale;
+      }
+    }
+    const bf16x8 pb = pack8(p[0], p[1]), dsb = pack8(ds[0], ds[1]);
+#pragma unroll
+    for (int i = 0; i < DV / 16; ++i)
+      dvt[i] = mfma16(read_a_split(&Ot[(i * 16 + l16) * TP], g), pb, dvt[i]);
+#pragma unroll
+    for (int i = 0; i < D / 16; ++i)
+      dkt[i] = mfma16(read_a_split(&Qt[(i * 16 + l16) * TP], g), dsb, dkt[i]);
+  }
+  __bf16* dkr = dk + ((int64_t)b * Lk + ki) * D;
+  __bf16* dvr = dv + ((int64_t)b * Lk + ki) * DV;
+#pragma unroll
+  for (int i = 0; i < D / 16; ++i) {
+    bf16x4 w;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) w[e] = (__bf16)dkt[i][e];
+    *reinterpret_cast<bf16x4*>(dkr + i * 16 + g * 4) = w;
+  }
+#pragma unroll
+  for (int i = 0; i < DV / 16; ++i) {
+    bf16x4 w;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) w[e] = (__bf16)dvt[i][e];
+    *reinterpret_cast<bf16x4*>(dvr + i * 16 + g * 4) = w;
+  }
+}
+
+// ---- backward: dQ --------------------------------------------------------------------------
+// workgroup: 64 queries (registers: Q and dO rows as B operands) x all keys in blocks of 32
+// (K row-major and transposed, V row-major in LDS). S^T = K Q^T and dP^T = V dO^T put the query
+// in the lane's column; dQ^T += K^T dS^T.
+template <int D, int DV>
+__global__ __launch_bounds__(kAttnT) void attn_bwd_dq_kernel(
+    const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v,
+    const __bf16* __restrict__ dout, const float* __restrict__ lse2,
+    const float* __restrict__ dsum, __bf16* __restrict__ dq, int Lq, int Lk, float sl2,
+    float scale) {
+  constexpr int KB = 32, KP = D + 8, VP = DV + 8, TP = KB + 8;
+  __shared__ __attribute__((aligned(16))) __bf16 Ks[KB * KP];
+  __shared__ __attribute__((aligned(16))) __bf16 Kt[D * TP];
+  __shared__ __attribute__((aligned(16))) __bf16 Vs[KB * VP];
+  const int b = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int l16 = lane & 15, g = lane >> 4;
+  const int qi = blockIdx.x * 64 + wid * 16 + l16;
+  const __bf16* kb = k + (int64_t)b * Lk * D;
+  const __bf16* vb = v + (int64_t)b * Lk * DV;
+  bf16x8 qf[D / 32], of[DV / 32];
+#pragma unroll
+  for (int ks = 0; ks < D / 32; ++ks)
+    qf[ks] = *reinterpret_cast<const bf16x8*>(q + ((int64_t)b * Lq + qi) * D + ks * 32 + g * 8);
+#pragma unroll
+  for (int ks = 0; ks < DV / 32; ++ks)
+    of[ks] = *reinterpret_cast<const bf16x8*>(dout + ((int64_t)b * Lq + qi) * DV + ks * 32 + g * 8);
+  const float lq = lse2[(int64_t)b * Lq + qi], dq0 = dsum[(int64_t)b * Lq + qi];
+  f32x4 acc[D / 16];
+#pragma unroll
+  for (int i = 0; i < D / 16; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < Lk; k0 += KB) {
+    __syncthreads();
+    for (int e = tid; e < KB * D / 8; e += kAttnT) {
+      const int r = e / (D / 8), c = (e - r * (D / 8)) * 8;
+      const bf16x8 x = *reinterpret_cast<const bf16x8*>(kb + (int64_t)(k0 + r) * D + c);
+      *reinterpret_cast<bf16x8*>(&Ks[r * KP + c]) = x;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) Kt[(c + t) * TP + r] = x[t];
+    }
+    for (int e = tid; e < KB * DV / 8; e += kAttnT) {
+      const int r = e / (DV / 8), c = (e - r * (DV / 8)) * 8;
+      *reinterpret_cast<bf16x8*>(&Vs[r * VP + c]) =
+          *reinterpret_cast<const bf16x8*>(vb + (int64_t)(k0 + r) * DV + c);
+    }
+    __syncthreads();
+    float ds[2][4];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < D / 32; ++ks)
+        s = mfma16(*reinterpret_cast<const bf16x8*>(&Ks[(kt * 16 + l16) * KP + ks * 32 + g * 8]),
+                   qf[ks], s);
+#pragma unroll
+      for (int ks = 0; ks < DV / 32; ++ks)
+        dp = mfma16(*reinterpret_cast<const bf16x8*>(&Vs[(kt * 16 + l16) * VP + ks * 32 + g * 8]),
+                    of[ks], dp);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float pe = exp2f(fmaf(s[e], sl2, -lq));
+        ds[kt][e] = pe * (dp[e] - dq0) * scale;
+      }
+    }
+    const bf16x8 dsb = pack8(ds[0], ds[1]);
+#pragma unroll
+    for (int i = 0; i < D / 16; ++i)
+      acc[i] = mfma16(read_a_split(&Kt[(i * 16 + l16) * TP], g), dsb, acc[i]);
+  }
+  __bf16* dqr = dq + ((int64_t)b * Lq + qi) * D;
+#pragma unroll
+  for (int i = 0; i < D / 16; ++i) {
+    bf16x4 w;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) w[e] = (__bf16)acc[i][e];
+    *reinterpret_cast<bf16x4*>(dqr + i * 16 + g * 4) = w;
+  }
+}
+
+void check_attn(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v) {
+  IAMD_CHECK(q.is_cuda() && q.scalar_type() == at::kBFloat16 && k.scalar_type() == at::kBFloat16 &&
+                 v.scalar_type() == at::kBFloat16,
+             "fused_attention: bf16 CUDA tensors expected");
+  IAMD_CHECK(q.dim() == 3 && k.dim() == 3 && v.dim() == 3 && q.is_contiguous() &&
+                 k.is_contiguous() && v.is_contiguous(),
+             "fused_attention: contiguous [B, L, D] tensors expected");
+  IAMD_CHECK(q.size(0) == k.size(0) && k.size(0) == v.size(0) && q.size(2) == k.size(2) &&
+                 k.size(1) == v.size(1),
+             "fused_attention: shape mismatch");
+  const int64_t d = q.size(2), dvv = v.size(2);
+  IAMD_CHECK(d == 32 || d == 64 || d == 128, "fused_attention: head dim must be 32, 64 or 128");
+  IAMD_CHECK(dvv % 32 == 0 && dvv >= 32 && dvv <= 256 && dvv != 224,
+             "fused_attention: value dim must be 32..256 in steps of 32 (not 224)");
+  IAMD_CHECK(q.size(1) % 64 == 0 && k.size(1) % 64 == 0 && q.size(1) > 0 && k.size(1) > 0,
+             "fused_attention: sequence lengths must be multiples of 64");
+  IAMD_CHECK(q.size(0) < 65536, "fused_attention: batch too large");
+}
+
+// (D, DV) dispatch onto the launcher template FN<D, DV>(args...)
+#define IAMD_ATTN_CASES(FN, DD, ...)                              \
+  switch (dvv) {                                                  \
+    case 32: FN<DD, 32>(__VA_ARGS__); break;                      \
+    case 64: FN<DD, 64>(__VA_ARGS__); break;                      \
+    case 96: FN<DD, 96>(__VA_ARGS__); break;                      \
+    case 128: FN<DD, 128>(__VA_ARGS__); break;                    \
+    case 160: FN<DD, 160>(__VA_ARGS__); break;                    \
+    case 192: FN<DD, 192>(__VA_ARGS__); break;                    \
+    case 256: FN<DD, 256>(__VA_ARGS__); break;                    \
+    default: IAMD_CHECK(false, "fused_attention: value dim");     \
+  }
+#define IAMD_ATTN_DISPATCH(FN, ...)            \
+  if (d == 32) {                               \
+    IAMD_ATTN_CASES(FN, 32, __VA_ARGS__)       \
+  } else if (d == 64) {                        \
+    IAMD_ATTN_CASES(FN, 64, __VA_ARGS__)       \
+  } else {                                     \
+    IAMD_ATTN_CASES(FN, 128, __VA_ARGS__)      \
+  }
+
+inline const __bf16* bp(const at::Tensor& t) {
+  return reinterpret_cast<const __bf16*>(t.data_ptr());
+}
+inline __bf16* bpm(at::Tensor& t) { return reinterpret_cast<__bf16*>(t.data_ptr()); }
+
+template <int D, int DV>
+void launch_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& out,
+                at::Tensor& lse, float sl2) {
+  const int64_t B = q.size(0), Lq = q.size(1), Lk = k.size(1);
+  hipLaunchKernelGGL((attn_fwd_kernel<D, DV>), dim3((unsigned)(Lq / 64), (unsigned)B),
+                     dim3(kAttnT), 0, stream(), bp(q), bp(k), bp(v), bpm(out),
+                     lse.data_ptr<float>(), (int)Lq, (int)Lk, sl2);
+}
+
+template <int D, int DV>
+void launch_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                const at::Tensor& dout, const at::Tensor& lse, const at::Tensor& dsum,
+                at::Tensor& dq, at::Tensor& dk, at::Tensor& dv, float sl2, float sc) {
+  const int64_t B = q.size(0), Lq = q.size(1), Lk = k.size(1);
+  hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, DV>), dim3((unsigned)(Lk / 64), (unsigned)B),
+                     dim3(kAttnT), 0, stream(), bp(q), bp(k), bp(v), bp(dout),
+                     lse.data_ptr<float>(), dsum.data_ptr<float>(), bpm(dk), bpm(dv), (int)Lq,
+                     (int)Lk, sl2, sc);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, DV>), dim3((unsigned)(Lq / 64), (unsigned)B),
+                     dim3(kAttnT), 0, stream(), bp(q), bp(k), bp(v), bp(dout),
+                     lse.data_ptr<float>(), dsum.data_ptr<float>(), bpm(dq), (int)Lq, (int)Lk,
+                     sl2, sc);
+}
+
+}  // namespace
+
+// returns (out [B, Lq, DV] bf16, lse2 [B, Lq] fp32: log2-domain log-sum-exp of the scaled scores)
+std::vector<at::Tensor> attention_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                      double scale) {
+  check_attn(q, k, v);
+  const int64_t B = q.size(0), Lq = q.size(1);
+  auto out = at::empty({B, Lq, v.size(2)}, q.options());
+  auto lse = at::empty({B, Lq}, q.options().dtype(at::kFloat));
+  const float sl2 = (float)(scale * 1.4426950408889634);
+  const int64_t d = q.size(2), dvv = v.size(2);
+  IAMD_ATTN_DISPATCH(launch_fwd, q, k, v, out, lse, sl2)
+  IAMD_LAUNCH_CHECK();
+  return {out, lse};
+}
+
+// returns (dq, dk, dv), bf16; dsum = rowsum(dout * out) in fp32 is computed here
+std::vector<at::Tensor> attention_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                      const at::Tensor& out, const at::Tensor& lse,
+                                      const at::Tensor& dout_in, double scale) {
+  check_attn(q, k, v);
+  const int64_t B = q.size(0), Lq = q.size(1);
+  const at::Tensor dout = dout_in.to(at::kBFloat16).contiguous();
+  IAMD_CHECK(dout.sizes() == out.sizes() && lse.scalar_type() == at::kFloat &&
+                 lse.numel() == B * Lq && lse.is_contiguous(),
+             "attention_bwd: out / dout / lse shapes");
+  const at::Tensor dsum = (dout.to(at::kFloat) * out.to(at::kFloat)).sum(-1).contiguous();
+  auto dq = at::empty_like(q), dk = at::empty_like(k), dv = at::empty_like(v);
+  const float sl2 = (float)(scale * 1.4426950408889634), sc = (float)scale;
+  const int64_t d = q.size(2), dvv = v.size(2);
+  IAMD_ATTN_DISPATCH(launch_bwd, q, k, v, dout, lse, dsum, dq, dk, dv, sl2, sc)
+  IAMD_LAUNCH_CHECK();
+  return {dq, dk, dv};
+}
+
+}  // namespace iamd

@@ -80,6 +80,11 @@ bool stream_capturing();
 void mt_scale(const std::vector<at::Tensor>& xs, const at::Tensor& s);
 at::Tensor mt_sqnorm(const std::vector<at::Tensor>& xs);
 // correlation.hip (k6 correlation, k8 channelnorm)
+std::vector<at::Tensor> attention_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                      double scale);
+std::vector<at::Tensor> attention_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                      const at::Tensor& out, const at::Tensor& lse,
+                                      const at::Tensor& dout, double scale);
 at::Tensor correlation_forward(const at::Tensor& input1, const at::Tensor& input2, int64_t pad,
                                int64_t ks, int64_t md, int64_t s1, int64_t s2);
 std::vector<at::Tensor> correlation_backward(const at::Tensor& input1, const at::Tensor& input2,
@@ -267,6 +272,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dout"), py::arg("need_dimg") = true);
   m.def("resample2d_forward", &iamd::resample2d_forward, "FlowNet2 Resample2d (k7)");
   m.def("resample2d_backward", &iamd::resample2d_backward, "k7 backward");
+  m.def("attention_fwd", &iamd::attention_fwd,
+        "fused attention forward (k16): (softmax(scale q k^T) v, log2-domain lse)");
+  m.def("attention_bwd", &iamd::attention_bwd, "fused attention backward (k16): (dq, dk, dv)");
   m.def("correlation_forward", &iamd::correlation_forward, "FlowNet correlation (k6)");
   m.def("correlation_backward", &iamd::correlation_backward, "k6 backward");
   m.def("channelnorm_forward", &iamd::channelnorm_forward, "channel L2 norm (k8)");

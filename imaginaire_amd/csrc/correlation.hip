@@ -462,6 +462,126 @@ __global__ __launch_bounds__(256) void corr_bwd_k1(
   }
 }
 
+// Register-blocked variant of corr_bwd_k1 (the default for s2 in {1, 2} and 16-bit inputs): 96
+// pixels x 64 channels per workgroup, each lane owns kRPX = 3 pixels of one parity class (s2
+// apart) x 8 channels. Pixel m at displacement ti reads strip row (m + ti) s2 for d(in1) and
+// (m + 2R - ti) s2 for d(in2), so stepping ti slides a 3-row register window by one row: one
+// 16-byte (bf16) LDS read per window and ti feeds 24 FMAs, against 8 FMAs per 32-byte read in
+// corr_bwd_k1, which is bound by LDS bandwidth. Strips are kept in the input dtype (half the LDS
+// bytes of fp32), so the FlowNetC shape needs 54 KB.
+constexpr int kRPX = 3;            // pixels per lane
+constexpr int kRBX = 32 * kRPX;    // pixels per workgroup
+template <typename T>
+__global__ __launch_bounds__(256) void corr_bwd_k1r(
+    const T* __restrict__ in1, const T* __restrict__ in2, const float* __restrict__ gout,
+    float* __restrict__ g1, float* __restrict__ g2, int H, int W, int C, int oH, int oW, int off,
+    int s2, int R, int D) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int span = kRBX + 2 * R * s2;
+  float* G1 = smem;                            // [kRBX][D]
+  float* G2 = G1 + kRBX * D;                   // [span][D]
+  T* S2 = reinterpret_cast<T*>(G2 + (span * D + 3) / 4 * 4);  // in2 strip [span][kBCC]
+  T* S1 = S2 + span * kBCC;                    // in1 strip [span][kBCC]
+  const int x0 = blockIdx.x * kRBX, y = blockIdx.y;
+  const int nc = C / kBCC;
+  const int n = blockIdx.z / nc, c0 = (blockIdx.z - n * nc) * kBCC;
+  const int tid = threadIdx.x, pl = tid >> 3, cl = (tid & 7) * 8;
+  // this lane's pixels: base + m s2, m < kRPX (strip / tile index)
+  const int base = s2 == 1 ? pl * kRPX : (pl >> 1) * (2 * kRPX) + (pl & 1);
+  const int DD = D * D;
+  const int ws = x0 - R * s2;
+  float a1[kRPX][8], a2[kRPX][8];
+#pragma unroll
+  for (int m = 0; m < kRPX; ++m)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a1[m][k] = a2[m][k] = 0.f;
+  const int oy1 = y - off;
+  for (int tj = 0; tj < D; ++tj) {
+    const int dy = (tj - R) * s2;
+    const int y2 = y + dy, yb = y - dy, oy2 = yb - off;
+    __syncthreads();
+    for (int e = tid; e < kRBX * D; e += 256) {
+      const int p = e / D, ti = e - p * D;
+      const int ox = x0 + p - off;
+      float v = 0.f;
+      if ((unsigned)oy1 < (unsigned)oH && (unsigned)ox < (unsigned)oW)
+        v = gout[(((int64_t)n * oH + oy1) * oW + ox) * DD + tj * D + ti];
+      G1[e] = v;
+    }
+    for (int e = tid; e < span * D; e += 256) {
+      const int p = e / D, ti = e - p * D;
+      const int ox = ws + p - off;
+      float v = 0.f;
+      if ((unsigned)oy2 < (unsigned)oH && (unsigned)ox < (unsigned)oW)
+        v = gout[(((int64_t)n * oH + oy2) * oW + ox) * DD + tj * D + ti];
+      G2[e] = v;
+    }
+    for (int e = tid; e < span * (kBCC / 8); e += 256) {
+      const int p = e / (kBCC / 8), c8 = (e - p * (kBCC / 8)) * 8;
+      const int x = ws + p;
+      float v2[8], v1[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v2[k] = v1[k] = 0.f;
+      if ((unsigned)x < (unsigned)W) {
+        if ((unsigned)y2 < (unsigned)H)
+          load_vec<T, 8>(in2 + (((int64_t)n * H + y2) * W + x) * C + c0 + c8, v2);
+        if ((unsigned)yb < (unsigned)H)
+          load_vec<T, 8>(in1 + (((int64_t)n * H + yb) * W + x) * C + c0 + c8, v1);
+      }
+      store_vec<T, 8>(S2 + p * kBCC + c8, v2);
+      store_vec<T, 8>(S1 + p * kBCC + c8, v1);
+    }
+    __syncthreads();
+    // windows (kRPX rows): r2[m] = S2 row base + (ti + m) s2, r1[m] = S1 row base + (m + 2R - ti) s2
+    float r2[kRPX][8], r1[kRPX][8];
+#pragma unroll
+    for (int m = 0; m < kRPX; ++m) {
+      load_vec<T, 8>(S2 + (base + m * s2) * kBCC + cl, r2[m]);
+      load_vec<T, 8>(S1 + (base + (m + 2 * R) * s2) * kBCC + cl, r1[m]);
+    }
+    for (int ti = 0; ti < D; ++ti) {
+      float w1[kRPX], w2[kRPX];
+#pragma unroll
+      for (int m = 0; m < kRPX; ++m) {
+        w1[m] = G1[(base + m * s2) * D + ti];
+        w2[m] = G2[(base + (m + 2 * R - ti) * s2) * D + ti];
+      }
+#pragma unroll
+      for (int m = 0; m < kRPX; ++m)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          a1[m][k] = fmaf(w1[m], r2[m][k], a1[m][k]);
+          a2[m][k] = fmaf(w2[m], r1[m][k], a2[m][k]);
+        }
+      if (ti + 1 < D) {
+#pragma unroll
+        for (int m = 0; m < kRPX - 1; ++m)
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            r2[m][k] = r2[m + 1][k];
+            r1[kRPX - 1 - m][k] = r1[kRPX - 2 - m][k];
+          }
+        load_vec<T, 8>(S2 + (base + (ti + kRPX) * s2) * kBCC + cl, r2[kRPX - 1]);
+        load_vec<T, 8>(S1 + (base + (2 * R - ti - 1) * s2) * kBCC + cl, r1[0]);
+      }
+    }
+  }
+  const float inv = 1.f / (float)C;
+#pragma unroll
+  for (int m = 0; m < kRPX; ++m) {
+    const int x = x0 + base + m * s2;
+    if (x >= W) continue;
+    const int64_t o = (((int64_t)n * H + y) * W + x) * C + c0 + cl;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      reinterpret_cast<float4*>(g1 + o)[q] = make_float4(a1[m][4 * q] * inv, a1[m][4 * q + 1] * inv,
+                                                         a1[m][4 * q + 2] * inv, a1[m][4 * q + 3] * inv);
+      reinterpret_cast<float4*>(g2 + o)[q] = make_float4(a2[m][4 * q] * inv, a2[m][4 * q + 1] * inv,
+                                                         a2[m][4 * q + 2] * inv, a2[m][4 * q + 3] * inv);
+    }
+  }
+}
+
 // ---- k8 channel norm (generic 4-D strides, fp32 accumulate) -------------------
 template <typename T>
 __global__ void chnorm_fwd(const T* __restrict__ x, T* __restrict__ out, int N, int C, int H,
@@ -587,6 +707,23 @@ std::vector<at::Tensor> correlation_backward(const at::Tensor& input1, const at:
   const size_t span = (size_t)(kBX + 2 * R * s2);
   const size_t lds = ((size_t)kBX * D + (span * D + 3) / 4 * 4 + 2 * span * kBCC) * sizeof(float);
   const char* tb = std::getenv("IMAGINAIRE_AMD_CORR_BWD_TILED");
+  // register-blocked tiled kernel (default; IMAGINAIRE_AMD_CORR_BWD_TILED=1 keeps corr_bwd_k1)
+  const size_t rspan = (size_t)(kRBX + 2 * R * s2);
+  const size_t rlds = ((size_t)kRBX * D + (rspan * D + 3) / 4 * 4) * sizeof(float) +
+                      2 * rspan * kBCC * a.element_size();
+  if ((tb == nullptr || tb[0] == '2') && ks == 1 && s1 == 1 && (s2 == 1 || s2 == 2) &&
+      a.element_size() == 2 && C % kBCC == 0 && rlds <= 64 * 1024) {
+    IAMD_DISPATCH_FLOAT_TYPES(a.scalar_type(), "correlation_bwd_k1r", [&] {
+      dim3 grid(ceil_div(W, kRBX), H, N * (C / kBCC));
+      hipLaunchKernelGGL((corr_bwd_k1r<scalar_t>), grid, dim3(256), rlds, stream(),
+                         reinterpret_cast<const scalar_t*>(a.data_ptr()),
+                         reinterpret_cast<const scalar_t*>(b.data_ptr()), g.data_ptr<float>(),
+                         g1.data_ptr<float>(), g2.data_ptr<float>(), H, W, C, oH, oW,
+                         (int)(md - pad), (int)s2, R, D);
+    });
+    IAMD_LAUNCH_CHECK();
+    return {g1, g2};
+  }
   if ((tb == nullptr || tb[0] != '0') && ks == 1 && s1 == 1 && C % kBCC == 0 &&
       lds <= 96 * 1024) {
     IAMD_DISPATCH_FLOAT_TYPES(a.scalar_type(), "correlation_bwd_k1", [&] {

@@ -224,26 +224,42 @@ adam_kernel(const TensorEntry* __restrict__ ents, const int* __restrict__ blocks
   const bool vec_ok = (((uintptr_t)p | (uintptr_t)m | (uintptr_t)v) % 16 == 0) &&
                       ((uintptr_t)g % (4 * sizeof(G)) == 0) && (start % 4 == 0);
   if (vec_ok) {
-    for (int64_t i = start + threadIdx.x * 4; i + 3 < end; i += kThreads * 4) {
-      float pv[4], gv[4], mv[4], vv[4];
-      load_vec<float, 4>(p + i, pv);
-      load_vec<G, 4>(g + i, gv);
-      load_vec<float, 4>(m + i, mv);
-      load_vec<float, 4>(v + i, vv);
+    // U groups of 4 elements per lane per trip, all loads issued before any math: 4 x U 16-B
+    // loads in flight per lane (one group at a time left the kernel latency-bound at ~1.5 TB/s)
+    constexpr int U = 4;
+    for (int64_t base = start + threadIdx.x * 4; base < end; base += kThreads * 4 * U) {
+      float pv[U][4], gv[U][4], mv[U][4], vv[U][4];
+      bool ok[U];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float gr = gv[k] * grad_scale;
-        if (!adamw && wd != 0.f) gr = fmaf(wd, pv[k], gr);
-        mv[k] = fmaf(beta1, mv[k], (1.f - beta1) * gr);
-        vv[k] = fmaf(beta2, vv[k], (1.f - beta2) * gr * gr);
-        const float denom = sqrtf(vv[k]) * rbc2 + eps;
-        if (adamw && wd != 0.f) pv[k] *= (1.f - lr * wd);
-        pv[k] -= step_size * mv[k] / denom;
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = base + (int64_t)u * kThreads * 4;
+        ok[u] = i + 3 < end;
+        if (ok[u]) {
+          load_vec<float, 4>(p + i, pv[u]);
+          load_vec<G, 4>(g + i, gv[u]);
+          load_vec<float, 4>(m + i, mv[u]);
+          load_vec<float, 4>(v + i, vv[u]);
+        }
       }
-      store_vec<float, 4>(p + i, pv);
-      store_vec<float, 4>(m + i, mv);
-      store_vec<float, 4>(v + i, vv);
-      if (shadow) store_vec<__hip_bfloat16, 4>(shadow + i, pv);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (!ok[u]) continue;
+        const int64_t i = base + (int64_t)u * kThreads * 4;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float gr = gv[u][k] * grad_scale;
+          if (!adamw && wd != 0.f) gr = fmaf(wd, pv[u][k], gr);
+          mv[u][k] = fmaf(beta1, mv[u][k], (1.f - beta1) * gr);
+          vv[u][k] = fmaf(beta2, vv[u][k], (1.f - beta2) * gr * gr);
+          const float denom = sqrtf(vv[u][k]) * rbc2 + eps;
+          if (adamw && wd != 0.f) pv[u][k] *= (1.f - lr * wd);
+          pv[u][k] -= step_size * mv[u][k] / denom;
+        }
+        store_vec<float, 4>(p + i, pv[u]);
+        store_vec<float, 4>(m + i, mv[u]);
+        store_vec<float, 4>(v + i, vv[u]);
+        if (shadow) store_vec<__hip_bfloat16, 4>(shadow + i, pv[u]);
+      }
     }
     // tail (numel not multiple of 4)
     const int64_t tail0 = start + ((end - start) / 4) * 4;
@@ -382,8 +398,36 @@ ema_kernel(const TensorEntry* __restrict__ ents, const int* __restrict__ blocks,
   const float a = 1.f - beta;
   const int64_t start = (int64_t)chunk * kChunk;
   const int64_t end = min(e.numel, start + (int64_t)kChunk);
+  const float as = a * sc;
+  if (sizeof(T) == 4 && (((uintptr_t)dst | (uintptr_t)src) & 15) == 0) {
+    // 16-B accesses, U groups per lane per trip with every load issued first
+    constexpr int U = 4;
+    const int64_t vend = start + ((end - start) & ~(int64_t)3);
+    for (int64_t base = start + threadIdx.x * 4; base < vend; base += kThreads * 4 * U) {
+      float dv[U][4], sv[U][4];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = base + (int64_t)u * kThreads * 4;
+        if (i < vend) {
+          load_vec<T, 4>(dst + i, dv[u]);
+          load_vec<T, 4>(src + i, sv[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = base + (int64_t)u * kThreads * 4;
+        if (i >= vend) continue;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dv[u][k] = fmaf(beta, dv[u][k], as * sv[u][k]);
+        store_vec<T, 4>(dst + i, dv[u]);
+      }
+    }
+    for (int64_t i = vend + threadIdx.x; i < end; i += kThreads)
+      dst[i] = from_f<T>(fmaf(beta, to_f<T>(dst[i]), as * to_f<T>(src[i])));
+    return;
+  }
   for (int64_t i = start + threadIdx.x; i < end; i += kThreads)
-    dst[i] = from_f<T>(fmaf(beta, to_f<T>(dst[i]), a * sc * to_f<T>(src[i])));
+    dst[i] = from_f<T>(fmaf(beta, to_f<T>(dst[i]), as * to_f<T>(src[i])));
 }
 
 template <typename T>

@@ -44,6 +44,7 @@ from imaginaire_amd.utils.init_weight import weights_init
 _FUSED_ATTN = os.environ.get('IMAGINAIRE_AMD_FUSED_ATTN', '1') == '1'
 from imaginaire_amd.utils.misc import get_and_setattr, get_nested_attr
 from imaginaire_amd.ops.resize import interpolate, Upsample
+from imaginaire_amd.ops import attention as fused_attention_ops
 
 
 def _filters(num_filters, max_num_filters, n):
@@ -558,7 +559,8 @@ class AttentionModule(nn.Module):
     def fused(self, features, label, ref_label):
         """The attention of :meth:`forward` applied to every tensor of ``features`` (each
         [B*K, C_i, H, W]) without materialising the B x KHW x HW attention matrix: one fused
-        scaled-dot-product attention (scale 1, softmax over the K*HW reference positions) whose
+        attention (the k16 HIP kernel, ops/attention.py; PyTorch SDPA off the GPU; scale 1,
+        softmax over the K*HW reference positions) whose
         values are the features' channels plus K frame-indicator channels, so the same call
         also returns, per query position, the attention mass on each reference frame (the
         reference's ``attention.reshape(b, k, hw, hw).sum(2)``). Returns (outputs, atn_vis
@@ -578,17 +580,21 @@ class AttentionModule(nn.Module):
         ind = torch.eye(k, device=q.device, dtype=vals[0].dtype).repeat_interleave(hw, 0)
         vals.append(ind.unsqueeze(0).expand(b, -1, -1))
         v = torch.cat(vals, 2)
-        # one head dim for q, k and v (zero columns change no dot product)
-        d = max(ck, v.shape[2])
-        d = (d + 7) // 8 * 8
-        q = F.pad(q, (0, d - ck))
-        key = F.pad(key, (0, d - ck))
-        v = F.pad(v, (0, d - v.shape[2]))
         dt = torch.get_autocast_dtype('cuda') if q.is_cuda and torch.is_autocast_enabled('cuda') \
             else q.dtype
-        with torch.autocast('cuda', enabled=False):
-            o = F.scaled_dot_product_attention(q.unsqueeze(1).to(dt), key.unsqueeze(1).to(dt),
-                                               v.unsqueeze(1).to(dt), scale=1.0).squeeze(1)
+        if fused_attention_ops.native_ok(q, key, v):
+            # the k16 HIP kernel: online softmax over the K*HW keys, no attention matrix in HBM
+            o = fused_attention_ops.fused_attention(q, key, v, 1.0)
+        else:
+            # one head dim for q, k and v (zero columns change no dot product)
+            d = max(ck, v.shape[2])
+            d = (d + 7) // 8 * 8
+            q = F.pad(q, (0, d - ck))
+            key = F.pad(key, (0, d - ck))
+            v = F.pad(v, (0, d - v.shape[2]))
+            with torch.autocast('cuda', enabled=False):
+                o = F.scaled_dot_product_attention(q.unsqueeze(1).to(dt), key.unsqueeze(1).to(dt),
+                                                   v.unsqueeze(1).to(dt), scale=1.0).squeeze(1)
         outs, off = [], 0
         for f in features:
             cf = f.shape[1]

@@ -1,0 +1,82 @@
+"""Fused attention ``softmax(scale * q k^T) v`` over a long key axis (k16, ``csrc/attention.hip``).
+
+The few-shot vid2vid reference-frame attention (reference generators/fs_vid2vid.py:944-951)
+materialises a B x (K*HW) x HW energy matrix, softmaxes it over the reference positions and
+multiplies it into the features with a second bmm. Here one HIP kernel streams the keys through
+LDS with an online softmax (MFMA 16x16x32 bf16, fp32 statistics) and writes only the output and
+a per-query log-sum-exp; the backward recomputes the probabilities from it in two kernels (dK/dV
+per key block, dQ per query block; deterministic, no atomics).
+
+``fused_attention(q, k, v, scale)`` takes q [B, Lq, d], k [B, Lk, d], v [B, Lk, dv] of any float
+dtype and returns [B, Lq, dv] (bf16 on the HIP path). Head dims are zero-padded to the kernel's
+sizes (d -> 32 / 64 / 128, dv -> a multiple of 32): zero columns change no dot product. Shapes
+the kernel does not take (sequence lengths not multiples of 64, d > 128, dv > 256) and CPU
+tensors run PyTorch's ``scaled_dot_product_attention``.
+
+    IMAGINAIRE_AMD_FUSED_ATTN_KERNEL=0   PyTorch SDPA everywhere (A/B switch)
+"""
+import os
+
+import torch
+import torch.nn.functional as F
+
+from imaginaire_amd.ops import _ext
+
+_NATIVE = os.environ.get('IMAGINAIRE_AMD_FUSED_ATTN_KERNEL', '1') != '0'
+
+
+def _pad_head(d):
+    for c in (32, 64, 128):
+        if d <= c:
+            return c
+    return None
+
+
+def _pad_value(dv):
+    c = (dv + 31) // 32 * 32
+    if c == 224:
+        c = 256
+    return c if c <= 256 else None
+
+
+def native_ok(q, k, v):
+    return (_NATIVE and q.is_cuda and _ext.use_native(q) and q.dim() == 3 and
+            q.shape[1] % 64 == 0 and k.shape[1] % 64 == 0 and
+            _pad_head(q.shape[2]) is not None and _pad_value(v.shape[2]) is not None)
+
+
+class _FusedAttentionFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, scale):
+        o, lse = _ext.ext().attention_fwd(q, k, v, float(scale))
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.scale = float(scale)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        dq, dk, dv = _ext.ext().attention_bwd(q, k, v, o, lse, do.contiguous(), ctx.scale)
+        return dq, dk, dv, None
+
+
+def attention_reference(q, k, v, scale=1.0):
+    """The reference formulation in the input dtype: explicit scores, softmax over keys, bmm."""
+    a = torch.softmax(torch.bmm(q, k.transpose(1, 2)) * scale, dim=2)
+    return torch.bmm(a, v)
+
+
+def fused_attention(q, k, v, scale=1.0):
+    if not native_ok(q, k, v):
+        dt = q.dtype
+        with torch.autocast(q.device.type, enabled=False):
+            return F.scaled_dot_product_attention(q.unsqueeze(1), k.to(dt).unsqueeze(1),
+                                                  v.to(dt).unsqueeze(1), scale=scale).squeeze(1)
+    d, dv = q.shape[2], v.shape[2]
+    D, DV = _pad_head(d), _pad_value(dv)
+    with torch.autocast('cuda', enabled=False):
+        qp = F.pad(q.to(torch.bfloat16), (0, D - d)).contiguous()
+        kp = F.pad(k.to(torch.bfloat16), (0, D - d)).contiguous()
+        vp = F.pad(v.to(torch.bfloat16), (0, DV - dv)).contiguous()
+        o = _FusedAttentionFn.apply(qp, kp, vp, scale)
+    return o[:, :, :dv] if DV != dv else o

@@ -1,0 +1,61 @@
+"""k16 fused attention vs PyTorch SDPA vs the explicit formulation (bmm -> softmax -> bmm), bf16,
+forward and forward+backward, at the fs_vid2vid attention shapes.
+
+    python scripts/probe/attn_probe.py
+"""
+import os
+import sys
+import time
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from imaginaire_amd.ops import attention as A  # noqa: E402
+
+
+def timeit(fn, iters=20):
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters * 1e3
+
+
+def sdpa(q, k, v):
+    return F.scaled_dot_product_attention(q.unsqueeze(1), k.unsqueeze(1), v.unsqueeze(1),
+                                          scale=1.0).squeeze(1)
+
+
+torch.manual_seed(0)
+for B, Lq, K, d, dv in ((1, 1024, 2, 64, 130), (1, 4096, 2, 64, 130), (2, 4096, 4, 128, 250),
+                        (1, 8192, 1, 64, 66)):
+    Lk = Lq * K
+    q = torch.randn(B, Lq, d, device='cuda').to(torch.bfloat16)
+    k = torch.randn(B, Lk, d, device='cuda').to(torch.bfloat16)
+    v = torch.randn(B, Lk, dv, device='cuda').to(torch.bfloat16)
+    if not A.native_ok(q, k, v):
+        print('skip (shape)', B, Lq, Lk, d, dv)
+        continue
+    dvp = (dv + 7) // 8 * 8
+    vpad = F.pad(v, (0, dvp - dv))
+    ref = A.attention_reference(q.float(), k.float(), v.float())
+    out = A.fused_attention(q, k, v)
+    err = float((out.float() - ref).norm() / ref.norm())
+    row = {}
+    row['k16'] = timeit(lambda: A.fused_attention(q, k, v))
+    row['sdpa'] = timeit(lambda: sdpa(q, k, vpad))
+    row['bmm'] = timeit(lambda: A.attention_reference(q, k, v))
+    qg, kg, vg = (t.clone().requires_grad_(True) for t in (q, k, v))
+    vpg = vpad.clone().requires_grad_(True)
+    go = torch.randn(B, Lq, dv, device='cuda').to(torch.bfloat16)
+    gop = F.pad(go, (0, dvp - dv))
+    row['k16 f+b'] = timeit(lambda: A.fused_attention(qg, kg, vg).backward(go))
+    row['sdpa f+b'] = timeit(lambda: sdpa(qg, kg, vpg).backward(gop))
+    row['bmm f+b'] = timeit(lambda: A.attention_reference(qg, kg, vg).backward(go))
+    flops = 2.0 * B * Lq * Lk * (d + dv)
+    print('B=%d Lq=%d Lk=%d d=%d dv=%d rel err %.1e | ' % (B, Lq, Lk, d, dv, err) +
+          ' | '.join('%s %.3f ms' % (n, t) for n, t in row.items()) +
+          ' | k16 fwd %.0f TF/s' % (flops / row['k16'] / 1e9), flush=True)

@@ -1737,3 +1737,36 @@ def test_spectral_norm_shadow_result_depends_on_weights_only():
         assert torch.equal(y1, y2)
     finally:
         snm._SN_SHADOW = old
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('B,Lq,Lk,d,dv,scale', [
+    (1, 1024, 2048, 64, 130, 1.0),   # fs_vid2vid unit config, K = 2 (64 + 64 + 2 value channels)
+    (2, 256, 256, 32, 66, 1.0),      # K = 1, small head dims (padded to 32 / 96)
+    (1, 128, 384, 128, 256, 0.125),  # widest head dims, scaled scores
+    (3, 64, 192, 20, 40, 0.5),       # ragged dims padded to 32 / 64
+])
+def test_fused_attention_matches_fp32_reference(B, Lq, Lk, d, dv, scale):
+    """k16 (csrc/attention.hip): softmax(scale q k^T) v and its gradients against the explicit
+    fp32 formulation on the same bf16-rounded inputs; no attention matrix is materialised."""
+    from imaginaire_amd.ops import attention as A
+    torch.manual_seed(31)
+    q = torch.randn(B, Lq, d, device='cuda').to(torch.bfloat16)
+    k = torch.randn(B, Lk, d, device='cuda').to(torch.bfloat16)
+    v = torch.randn(B, Lk, dv, device='cuda').to(torch.bfloat16)
+    assert A.native_ok(q, k, v)
+    qs, ks, vs = (t.clone().requires_grad_(True) for t in (q, k, v))
+    qr, kr, vr = (t.float().requires_grad_(True) for t in (q, k, v))
+    o = A.fused_attention(qs, ks, vs, scale)
+    ref = A.attention_reference(qr, kr, vr, scale)
+    assert o.shape == ref.shape and o.dtype == torch.bfloat16
+
+    def rel(a, b):
+        return float((a.float() - b).norm() / b.norm())
+    assert rel(o, ref) < 1e-2, rel(o, ref)
+    go = torch.randn_like(ref)
+    o.backward(go.to(torch.bfloat16))
+    ref.backward(go)
+    for name, a, b in (('dq', qs.grad, qr.grad), ('dk', ks.grad, kr.grad), ('dv', vs.grad, vr.grad)):
+        assert a is not None and a.shape == b.shape, name
+        assert rel(a, b) < 3e-2, (name, rel(a, b))
