@@ -83,6 +83,26 @@ __global__ void __launch_bounds__(kT) sn_colsum(const SnEntry* __restrict__ ents
   const int64_t r1 = min(e.h, r0 + kRowsPerSplit);
   const bool vec = e.vec;  // then c + 3 < w as well
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  if (e.Wb && vec) {
+    // bf16 shadow rows: 8-byte loads, so 16 rows in flight per thread (8 left the pass
+    // latency-bound at ~1.6 TB/s)
+    for (int64_t r = r0; r < r1; r += 16) {
+      float wv[16][4], uv[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int64_t rr = r + i;
+        const bool ok = rr < r1;
+        uv[i] = ok ? e.u[rr] : 0.f;
+        load_vec<__hip_bfloat16, 4>(e.Wb + (ok ? rr : r0) * e.w + c, wv[i]);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[k] = fmaf(wv[i][k], uv[i], acc[k]);
+    }
+    *reinterpret_cast<float4*>(e.tp + bm[2] * e.w + c) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    return;
+  }
   for (int64_t r = r0; r < r1; r += 8) {
     float wv[8][4], uv[8];
 #pragma unroll
@@ -167,13 +187,26 @@ __global__ void __launch_bounds__(64 * kRowsPerBlock) sn_rows(const SnEntry* __r
     const __hip_bfloat16* rb = e.Wb + r * e.w;
     const float* x = e.t;
     if (e.vec && e.w % 8 == 0) {
-      for (int64_t c = lane * 8; c < e.w; c += 64 * 8) {
-        float a[8], b[8];
-        load_vec<__hip_bfloat16, 8>(rb + c, a);
-        load_vec<float, 4>(x + c, *reinterpret_cast<float(*)[4]>(b));
-        load_vec<float, 4>(x + c + 4, *reinterpret_cast<float(*)[4]>(b + 4));
+      // two 16-byte row loads per lane and trip in flight
+      for (int64_t c = lane * 8; c < e.w; c += 64 * 16) {
+        const int64_t c2 = c + 64 * 8;
+        const bool two = c2 < e.w;
+        float a[2][8], b[2][8];
+        load_vec<__hip_bfloat16, 8>(rb + c, a[0]);
+        load_vec<float, 4>(x + c, *reinterpret_cast<float(*)[4]>(b[0]));
+        load_vec<float, 4>(x + c + 4, *reinterpret_cast<float(*)[4]>(b[0] + 4));
+        if (two) {
+          load_vec<__hip_bfloat16, 8>(rb + c2, a[1]);
+          load_vec<float, 4>(x + c2, *reinterpret_cast<float(*)[4]>(b[1]));
+          load_vec<float, 4>(x + c2 + 4, *reinterpret_cast<float(*)[4]>(b[1] + 4));
+        } else {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc = fmaf(a[k], b[k], acc);
+          for (int k = 0; k < 8; ++k) a[1][k] = b[1][k] = 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc = fmaf(a[0][k], b[0][k], acc);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc = fmaf(a[1][k], b[1][k], acc);
       }
     } else {
       for (int64_t c = lane; c < e.w; c += 64) acc = fmaf(__bfloat162float(rb[c]), x[c], acc);
@@ -411,7 +444,26 @@ __global__ void __launch_bounds__(kT) sn_scale_cast(const ScEntry* __restrict__ 
   const int64_t end = min(e.numel, start + (int64_t)kScChunk);
   __hip_bfloat16* o = out + e.off;  // 16-B aligned (offsets are multiples of 8 elements)
   auto wat = [&](int64_t i) { return e.Wb ? __bfloat162float(e.Wb[i]) : e.W[i]; };
-  if (e.vec) {  // 8 elements per lane per trip: two 16-B fp32 (or one bf16) loads, 16-B stores
+  if (e.vec && e.Wb) {  // shadow reads: 4 x 16-B loads per lane in flight, then the stores
+    const int64_t vend = start + ((end - start) & ~(int64_t)7);
+    for (int64_t i0 = start + threadIdx.x * 8; i0 < vend; i0 += kT * 8 * 4) {
+      float v[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t i = i0 + (int64_t)u * kT * 8;
+        if (i < vend) load_vec<__hip_bfloat16, 8>(e.Wb + i, v[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t i = i0 + (int64_t)u * kT * 8;
+        if (i >= vend) continue;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[u][k] *= inv;
+        store_vec<__hip_bfloat16, 8>(o + i, v[u]);
+      }
+    }
+    for (int64_t i = vend + threadIdx.x; i < end; i += kT) o[i] = __float2bfloat16(wat(i) * inv);
+  } else if (e.vec) {  // 8 elements per lane per trip: two 16-B fp32 loads, 16-B stores
     const int64_t vend = start + ((end - start) & ~(int64_t)7);
     for (int64_t i = start + threadIdx.x * 8; i < vend; i += kT * 8) {
       float v[8];
@@ -612,19 +664,31 @@ snb_apply(const G* __restrict__ g, const float* __restrict__ u, const float* __r
   const float coef = dot / (s * s);
   const int64_t n = h * w;
   if ((w & 7) == 0) {  // flat walk, 8 columns of one row per lane: 16-B loads and stores
-    for (int64_t i = ((int64_t)blockIdx.x * kSnbT + threadIdx.x) * 8; i < n;
-         i += (int64_t)gridDim.x * kSnbT * 8) {
-      const uint32_t r = (uint32_t)i / (uint32_t)w;  // n < 2^31 (checked on the host)
-      const int64_t c = i - (int64_t)r * w;
-      const float cu = coef * u[r];
-      float gv[8], vv[8], o[8];
-      load_vec<G, 8>(g + i, gv);
-      load_vec<float, 4>(vm + c, *reinterpret_cast<float(*)[4]>(vv));
-      load_vec<float, 4>(vm + c + 4, *reinterpret_cast<float(*)[4]>(vv + 4));
+    const int64_t step = (int64_t)gridDim.x * kSnbT * 8;
+    // two trips' loads in flight per lane
+    for (int64_t i0 = ((int64_t)blockIdx.x * kSnbT + threadIdx.x) * 8; i0 < n; i0 += 2 * step) {
+      float gv[2][8], vv[2][8], cu[2];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) o[k] = fmaf(gv[k], inv, -cu * vv[k]);
-      store_vec<float, 4>(dw + i, *reinterpret_cast<float(*)[4]>(o));
-      store_vec<float, 4>(dw + i + 4, *reinterpret_cast<float(*)[4]>(o + 4));
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int64_t i = i0 + h2 * step;
+        if (i >= n) continue;
+        const uint32_t r = (uint32_t)i / (uint32_t)w;  // n < 2^31 (checked on the host)
+        const int64_t c = i - (int64_t)r * w;
+        cu[h2] = coef * u[r];
+        load_vec<G, 8>(g + i, gv[h2]);
+        load_vec<float, 4>(vm + c, *reinterpret_cast<float(*)[4]>(vv[h2]));
+        load_vec<float, 4>(vm + c + 4, *reinterpret_cast<float(*)[4]>(vv[h2] + 4));
+      }
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int64_t i = i0 + h2 * step;
+        if (i >= n) continue;
+        float o[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = fmaf(gv[h2][k], inv, -cu[h2] * vv[h2][k]);
+        store_vec<float, 4>(dw + i, *reinterpret_cast<float(*)[4]>(o));
+        store_vec<float, 4>(dw + i + 4, *reinterpret_cast<float(*)[4]>(o + 4));
+      }
     }
     return;
   }

@@ -55,3 +55,28 @@ def test_softmax_pool_matches_reference():
     p = softmax_pool(conv, lab)
     ref = torch.bmm(conv.reshape(2, 32, 35), torch.softmax(lab, 1).reshape(2, 48, 35).transpose(1, 2))
     assert p.shape == (2, 32, 48) and torch.allclose(p, ref, atol=1e-6)
+
+
+def test_fused_attention_op_cpu_path_matches_reference():
+    """ops/attention.py off the GPU (PyTorch SDPA) equals the explicit formulation, values and
+    gradients; the padding helpers map head dims onto the k16 kernel's sizes."""
+    from imaginaire_amd.ops import attention as A
+    assert [A._pad_head(d) for d in (1, 32, 33, 64, 100, 128, 129)] == [32, 32, 64, 64, 128, 128,
+                                                                      None]
+    assert [A._pad_value(d) for d in (2, 32, 130, 200, 224, 256, 257)] == [32, 32, 160, 256, 256,
+                                                                         256, None]
+    torch.manual_seed(0)
+    q, k, v = (torch.randn(2, 64, 20, dtype=torch.float64), torch.randn(2, 128, 20,
+                                                                        dtype=torch.float64),
+               torch.randn(2, 128, 12, dtype=torch.float64))
+    qa, ka, va = (t.clone().requires_grad_(True) for t in (q, k, v))
+    qb, kb, vb = (t.clone().requires_grad_(True) for t in (q, k, v))
+    assert not A.native_ok(qa, ka, va)
+    o = A.fused_attention(qa, ka, va, 0.5)
+    r = A.attention_reference(qb, kb, vb, 0.5)
+    torch.testing.assert_close(o, r)
+    g = torch.randn_like(r)
+    o.backward(g)
+    r.backward(g)
+    for a, b in ((qa, qb), (ka, kb), (va, vb)):
+        torch.testing.assert_close(a.grad, b.grad)
