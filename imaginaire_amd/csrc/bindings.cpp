@@ -85,6 +85,7 @@ std::vector<at::Tensor> attention_fwd(const at::Tensor& q, const at::Tensor& k, 
 std::vector<at::Tensor> attention_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                       const at::Tensor& out, const at::Tensor& lse,
                                       const at::Tensor& dout, double scale);
+void nhwc_concat_into(at::Tensor& out, const at::Tensor& a, const at::Tensor& b);
 at::Tensor correlation_forward(const at::Tensor& input1, const at::Tensor& input2, int64_t pad,
                                int64_t ks, int64_t md, int64_t s1, int64_t s2);
 std::vector<at::Tensor> correlation_backward(const at::Tensor& input1, const at::Tensor& input2,
@@ -275,6 +276,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attention_fwd", &iamd::attention_fwd,
         "fused attention forward (k16): (softmax(scale q k^T) v, log2-domain lse)");
   m.def("attention_bwd", &iamd::attention_bwd, "fused attention backward (k16): (dq, dk, dv)");
+  m.def("nhwc_concat_into", &iamd::nhwc_concat_into,
+        "out = cat(a, b, zeros) along channels, NHWC (discriminator inputs)");
   m.def("correlation_forward", &iamd::correlation_forward, "FlowNet correlation (k6)");
   m.def("correlation_backward", &iamd::correlation_backward, "k6 backward");
   m.def("channelnorm_forward", &iamd::channelnorm_forward, "channel L2 norm (k8)");

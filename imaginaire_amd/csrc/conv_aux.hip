@@ -285,6 +285,60 @@ int pad_grid(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n 
 
 // x [B, C, H, W] channels-last (C % 8 == 0, bf16 / fp32) -> padded [B, C, H+pt+pb, W+pl+pr];
 // mode 0 reflect, 1 replicate.
+namespace {
+// out[p, 0:ca] = a[p], out[p, ca:ca+cb] = b[p], out[p, ca+cb:cp] = 0 for every pixel p of NHWC
+// tensors: one 8-channel output group per lane, 16-byte (bf16) stores; the sources' odd channel
+// counts (the 185-channel COCO-Stuff label) are gathered element-wise, coalesced across lanes.
+template <typename T>
+__global__ void __launch_bounds__(256) nhwc_concat_kernel(const T* __restrict__ a,
+                                                         const T* __restrict__ b,
+                                                         T* __restrict__ out, int64_t P, int ca,
+                                                         int cb, int cp) {
+  const int G = cp / 8;
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= P * G) return;
+  const int64_t p = idx / G;
+  const int c0 = (int)(idx - p * G) * 8;
+  float v[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = c0 + k;
+    v[k] = c < ca ? to_f<T>(a[p * ca + c])
+                  : (c < ca + cb ? to_f<T>(b[p * cb + (c - ca)]) : 0.f);
+  }
+  store_vec<T, 8>(out + p * cp + c0, v);
+}
+}  // namespace
+
+// Write cat(a, b, zeros) along channels into ``out`` (all NHWC-dense: [N, C, H, W] with
+// channels-last strides, same N/H/W; out has cp >= ca + cb channels, cp % 8 == 0): the
+// discriminator input ``cat(label, image)`` in one pass (the strided slice copies ran on
+// PyTorch's generic element-offset copy kernel).
+void nhwc_concat_into(at::Tensor& out, const at::Tensor& a, const at::Tensor& b) {
+  auto cl = at::MemoryFormat::ChannelsLast;
+  IAMD_CHECK(out.dim() == 4 && a.dim() == 4 && b.dim() == 4 && out.is_cuda(),
+             "nhwc_concat_into: 4-D CUDA tensors expected");
+  IAMD_CHECK(out.is_contiguous(cl) && a.is_contiguous(cl) && b.is_contiguous(cl),
+             "nhwc_concat_into: channels-last dense tensors expected");
+  IAMD_CHECK(a.scalar_type() == out.scalar_type() && b.scalar_type() == out.scalar_type(),
+             "nhwc_concat_into: one dtype expected");
+  const int64_t N = out.size(0), H = out.size(2), W = out.size(3);
+  IAMD_CHECK(a.size(0) == N && b.size(0) == N && a.size(2) == H && b.size(2) == H &&
+                 a.size(3) == W && b.size(3) == W,
+             "nhwc_concat_into: batch / spatial sizes differ");
+  const int ca = (int)a.size(1), cb = (int)b.size(1), cp = (int)out.size(1);
+  IAMD_CHECK(cp % 8 == 0 && ca + cb <= cp, "nhwc_concat_into: channel counts");
+  const int64_t P = N * H * W;
+  if (P == 0) return;
+  IAMD_DISPATCH_FLOAT_TYPES(out.scalar_type(), "nhwc_concat_into", [&] {
+    hipLaunchKernelGGL((nhwc_concat_kernel<scalar_t>), dim3(ceil_div(P * (cp / 8), 256)),
+                       dim3(256), 0, stream(), reinterpret_cast<const scalar_t*>(a.data_ptr()),
+                       reinterpret_cast<const scalar_t*>(b.data_ptr()),
+                       reinterpret_cast<scalar_t*>(out.data_ptr()), P, ca, cb, cp);
+  });
+  IAMD_LAUNCH_CHECK();
+}
+
 at::Tensor pad_nhwc_fwd(const at::Tensor& x, int64_t pl, int64_t pr, int64_t pt, int64_t pb,
                         int64_t mode) {
   IAMD_CHECK(x.is_cuda() && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast) &&

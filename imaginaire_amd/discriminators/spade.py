@@ -23,6 +23,7 @@ from imaginaire_amd.ops.resize import interpolate
 from imaginaire_amd.discriminators.multires_patch import NLayerPatchDiscriminator
 from imaginaire_amd.layers.spectral_norm import (extra_sn_power_iteration,
                                                  refresh_batched_spectral_norm)
+from imaginaire_amd.ops import _ext
 from imaginaire_amd.registry import canonical_module_name
 from imaginaire_amd.utils.data import (get_paired_input_image_channel_number,
                                        get_paired_input_label_channel_number)
@@ -43,11 +44,18 @@ class _PatchInput(torch.autograd.Function):
         out = torch.empty((sum(n), cp) + tuple(lab.shape[2:]), dtype=dtype, device=lab.device,
                           memory_format=torch.channels_last)
         o = 0
+        native = out.is_cuda and _ext.use_native(out)
         for lb, im, k in zip(labels, images, n):
-            out[o:o + k, :cl] = lb
-            out[o:o + k, cl:c] = im
+            if native:
+                # one pass per half (label | image | zero tail) on the HIP concat kernel
+                _ext.ext().nhwc_concat_into(
+                    out[o:o + k], lb.to(dtype).contiguous(memory_format=torch.channels_last),
+                    im.to(dtype).contiguous(memory_format=torch.channels_last))
+            else:
+                out[o:o + k, :cl] = lb
+                out[o:o + k, cl:c] = im
             o += k
-        if cp > c:
+        if cp > c and not native:
             out[:, c:].zero_()
         ctx.conf = (cl, c, n, [t.dtype for t in tensors])
         return out

@@ -1770,3 +1770,21 @@ def test_fused_attention_matches_fp32_reference(B, Lq, Lk, d, dv, scale):
     for name, a, b in (('dq', qs.grad, qr.grad), ('dk', ks.grad, kr.grad), ('dv', vs.grad, vr.grad)):
         assert a is not None and a.shape == b.shape, name
         assert rel(a, b) < 3e-2, (name, rel(a, b))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+def test_nhwc_concat_into_matches_cat(dtype):
+    """The discriminator-input concat kernel: cat(label, image) + zero tail, NHWC, per half."""
+    from imaginaire_amd.ops import _ext
+    torch.manual_seed(33)
+    cl = torch.channels_last
+    for n, ca, cb, cp, h, w in ((2, 185, 3, 192, 17, 33), (1, 5, 3, 8, 4, 4), (3, 13, 6, 24, 9, 1)):
+        a = torch.randn(n, ca, h, w, device='cuda').to(dtype).contiguous(memory_format=cl)
+        b = torch.randn(n, cb, h, w, device='cuda').to(dtype).contiguous(memory_format=cl)
+        out = torch.full((2 * n, cp, h, w), float('nan'), device='cuda', dtype=dtype).contiguous(
+            memory_format=cl)
+        _ext.ext().nhwc_concat_into(out[n:], a, b)
+        ref = torch.cat([a, b, torch.zeros(n, cp - ca - cb, h, w, device='cuda', dtype=dtype)], 1)
+        assert torch.equal(out[n:], ref)
+        assert torch.isnan(out[:n]).all()  # the other half untouched
