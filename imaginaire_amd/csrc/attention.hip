@@ -21,6 +21,7 @@
 // multiples of 64. Scores in the log2 domain: p = exp2(s * scale * log2(e) - lse2).
 #include "common.h"
 
+#include <algorithm>
 #include <cmath>
 
 namespace iamd {
@@ -65,14 +66,18 @@ __device__ __forceinline__ bf16x8 read_a_split(const __bf16* row, int g) {
 // workgroup: 64 queries (wave w: queries 16w..16w+15) x all keys in blocks of 64 staged in LDS
 // (K row-major, V transposed). Per block and wave: S^T (4 key tiles x D/32 MFMAs), the online
 // softmax, O^T += V^T P^T (DV/16 tiles x 2 MFMAs).
+// Split over keys (grid.y = split, keys [split * klen, +klen)) when the query tiles alone cannot
+// fill the chip: each split then writes its unnormalised fp32 output with its running max and
+// sum (opart / mpart / lpart), merged by attn_fwd_combine.
 template <int D, int DV>
 __global__ __launch_bounds__(kAttnT) void attn_fwd_kernel(
     const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v,
-    __bf16* __restrict__ o, float* __restrict__ lse2, int Lq, int Lk, float sl2) {
+    __bf16* __restrict__ o, float* __restrict__ lse2, int Lq, int Lk, float sl2, int klen,
+    float* __restrict__ opart, float* __restrict__ mpart, float* __restrict__ lpart) {
   constexpr int KB = 64, KP = D + 8, VP = KB + 8;
   __shared__ __attribute__((aligned(16))) __bf16 Ks[KB * KP];
   __shared__ __attribute__((aligned(16))) __bf16 Vt[DV * VP];
-  const int b = blockIdx.y;
+  const int b = blockIdx.z, sp = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l16 = lane & 15, g = lane >> 4;
   const int qi = blockIdx.x * 64 + wid * 16 + l16;  // this lane's query (the B/C column)
@@ -86,7 +91,8 @@ __global__ __launch_bounds__(kAttnT) void attn_fwd_kernel(
 #pragma unroll
   for (int i = 0; i < DV / 16; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = kNegBig, lsum = 0.f;
-  for (int k0 = 0; k0 < Lk; k0 += KB) {
+  const int kbeg = sp * klen, kend = min(Lk, kbeg + klen);
+  for (int k0 = kbeg; k0 < kend; k0 += KB) {
     __syncthreads();
     for (int e = tid; e < KB * D / 8; e += kAttnT) {
       const int r = e / (D / 8), c = (e - r * (D / 8)) * 8;
@@ -141,6 +147,18 @@ __global__ __launch_bounds__(kAttnT) void attn_fwd_kernel(
   }
   lsum += __shfl_xor(lsum, 16);
   lsum += __shfl_xor(lsum, 32);
+  if (opart) {  // split: unnormalised partial output + (max, sum) of this key range
+    const int64_t row = ((int64_t)sp * gridDim.z + b) * Lq + qi;
+    float* prow = opart + row * DV;
+#pragma unroll
+    for (int i = 0; i < DV / 16; ++i)
+      *reinterpret_cast<f32x4*>(prow + i * 16 + g * 4) = acc[i];
+    if (g == 0) {
+      mpart[row] = m;
+      lpart[row] = lsum;
+    }
+    return;
+  }
   const float inv = 1.f / lsum;
   __bf16* orow = o + ((int64_t)b * Lq + qi) * DV;
 #pragma unroll
@@ -153,6 +171,40 @@ __global__ __launch_bounds__(kAttnT) void attn_fwd_kernel(
   if (g == 0) lse2[(int64_t)b * Lq + qi] = m + log2f(lsum);
 }
 
+// merge NS key splits: M = max m_s, L = sum l_s 2^(m_s - M), O = sum O_s 2^(m_s - M) / L;
+// one wave per query row
+__global__ __launch_bounds__(256) void attn_fwd_combine(
+    const float* __restrict__ opart, const float* __restrict__ mpart,
+    const float* __restrict__ lpart, __bf16* __restrict__ o, float* __restrict__ lse2, int NS,
+    int64_t rows, int DV) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  float M = kNegBig;
+  for (int s = 0; s < NS; ++s) M = fmaxf(M, mpart[s * rows + row]);
+  float L = 0.f;
+  for (int s = 0; s < NS; ++s) L += lpart[s * rows + row] * exp2f(mpart[s * rows + row] - M);
+  const float inv = 1.f / L;
+  for (int c = lane; c < DV; c += 64) {
+    float acc = 0.f;
+    for (int s = 0; s < NS; ++s)
+      acc += opart[(s * rows + row) * DV + c] * exp2f(mpart[s * rows + row] - M);
+    o[row * DV + c] = (__bf16)(acc * inv);
+  }
+  if (lane == 0) lse2[row] = M + log2f(L);
+}
+
+// out[i] = bf16(sum_s part[s * n + i]) (the split backward's fp32 partial gradients)
+__global__ __launch_bounds__(256) void attn_sum_splits(const float* __restrict__ part,
+                                                       __bf16* __restrict__ out, int NS,
+                                                       int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float acc = 0.f;
+  for (int s = 0; s < NS; ++s) acc += part[s * n + i];
+  out[i] = (__bf16)acc;
+}
+
 // ---- backward: dK, dV ----------------------------------------------------------------------
 // workgroup: 64 keys (wave w: keys 16w..16w+15, held in registers as B operands) x all queries
 // in blocks of 32 staged in LDS both row-major (A operands of S, dP) and transposed (A operands
@@ -163,7 +215,8 @@ __global__ __launch_bounds__(kAttnT) void attn_bwd_dkv_kernel(
     const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v,
     const __bf16* __restrict__ dout, const float* __restrict__ lse2,
     const float* __restrict__ dsum, __bf16* __restrict__ dk, __bf16* __restrict__ dv, int Lq,
-    int Lk, float sl2, float scale) {
+    int Lk, float sl2, float scale, int qlen, float* __restrict__ dkpart,
+    float* __restrict__ dvpart) {
   constexpr int QB = 32, QP = D + 8, OP = DV + 8, TP = QB + 8;
   __shared__ __attribute__((aligned(16))) __bf16 Qs[QB * QP];
   __shared__ __attribute__((aligned(16))) __bf16 Qt[D * TP];
@@ -171,7 +224,7 @@ __global__ __launch_bounds__(kAttnT) void attn_bwd_dkv_kernel(
   __shared__ __attribute__((aligned(16))) __bf16 Ot[DV * TP];
   __shared__ __attribute__((aligned(16))) float Ls[QB];
   __shared__ __attribute__((aligned(16))) float Ds[QB];
-  const int b = blockIdx.y;
+  const int b = blockIdx.z, sp = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l16 = lane & 15, g = lane >> 4;
   const int ki = blockIdx.x * 64 + wid * 16 + l16;  // this lane's key (the B/C column)
@@ -189,7 +242,8 @@ __global__ __launch_bounds__(kAttnT) void attn_bwd_dkv_kernel(
   for (int i = 0; i < D / 16; ++i) dkt[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < DV / 16; ++i) dvt[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int q0 = 0; q0 < Lq; q0 += QB) {
+  const int qend = min(Lq, (sp + 1) * qlen);
+  for (int q0 = sp * qlen; q0 < qend; q0 += QB) {
     __syncthreads();
     for (int e = tid; e < QB * D / 8; e += kAttnT) {
       const int r = e / (D / 8), c = (e - r * (D / 8)) * 8;
@@ -239,6 +293,16 @@ __global__ __launch_bounds__(kAttnT) void attn_bwd_dkv_kernel(
     for (int i = 0; i < D / 16; ++i)
       dkt[i] = mfma16(read_a_split(&Qt[(i * 16 + l16) * TP], g), dsb, dkt[i]);
   }
+  if (dkpart) {  // query split: fp32 partial gradients, summed by attn_sum_splits
+    const int64_t row = ((int64_t)sp * gridDim.z + b) * Lk + ki;
+#pragma unroll
+    for (int i = 0; i < D / 16; ++i)
+      *reinterpret_cast<f32x4*>(dkpart + row * D + i * 16 + g * 4) = dkt[i];
+#pragma unroll
+    for (int i = 0; i < DV / 16; ++i)
+      *reinterpret_cast<f32x4*>(dvpart + row * DV + i * 16 + g * 4) = dvt[i];
+    return;
+  }
   __bf16* dkr = dk + ((int64_t)b * Lk + ki) * D;
   __bf16* dvr = dv + ((int64_t)b * Lk + ki) * DV;
 #pragma unroll
@@ -266,12 +330,12 @@ __global__ __launch_bounds__(kAttnT) void attn_bwd_dq_kernel(
     const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v,
     const __bf16* __restrict__ dout, const float* __restrict__ lse2,
     const float* __restrict__ dsum, __bf16* __restrict__ dq, int Lq, int Lk, float sl2,
-    float scale) {
+    float scale, int klen, float* __restrict__ dqpart) {
   constexpr int KB = 32, KP = D + 8, VP = DV + 8, TP = KB + 8;
   __shared__ __attribute__((aligned(16))) __bf16 Ks[KB * KP];
   __shared__ __attribute__((aligned(16))) __bf16 Kt[D * TP];
   __shared__ __attribute__((aligned(16))) __bf16 Vs[KB * VP];
-  const int b = blockIdx.y;
+  const int b = blockIdx.z, sp = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l16 = lane & 15, g = lane >> 4;
   const int qi = blockIdx.x * 64 + wid * 16 + l16;
@@ -288,7 +352,8 @@ __global__ __launch_bounds__(kAttnT) void attn_bwd_dq_kernel(
   f32x4 acc[D / 16];
 #pragma unroll
   for (int i = 0; i < D / 16; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < Lk; k0 += KB) {
+  const int kend = min(Lk, (sp + 1) * klen);
+  for (int k0 = sp * klen; k0 < kend; k0 += KB) {
     __syncthreads();
     for (int e = tid; e < KB * D / 8; e += kAttnT) {
       const int r = e / (D / 8), c = (e - r * (D / 8)) * 8;
@@ -326,6 +391,13 @@ __global__ __launch_bounds__(kAttnT) void attn_bwd_dq_kernel(
     for (int i = 0; i < D / 16; ++i)
       acc[i] = mfma16(read_a_split(&Kt[(i * 16 + l16) * TP], g), dsb, acc[i]);
   }
+  if (dqpart) {  // key split: fp32 partial dQ, summed by attn_sum_splits
+    const int64_t row = ((int64_t)sp * gridDim.z + b) * Lq + qi;
+#pragma unroll
+    for (int i = 0; i < D / 16; ++i)
+      *reinterpret_cast<f32x4*>(dqpart + row * D + i * 16 + g * 4) = acc[i];
+    return;
+  }
   __bf16* dqr = dq + ((int64_t)b * Lq + qi) * D;
 #pragma unroll
   for (int i = 0; i < D / 16; ++i) {
@@ -353,6 +425,8 @@ void check_attn(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v) {
   IAMD_CHECK(q.size(1) % 64 == 0 && k.size(1) % 64 == 0 && q.size(1) > 0 && k.size(1) > 0,
              "fused_attention: sequence lengths must be multiples of 64");
   IAMD_CHECK(q.size(0) < 65536, "fused_attention: batch too large");
+  IAMD_CHECK(q.size(0) * q.size(1) * std::max<int64_t>(v.size(2), q.size(2)) * 32 < (1ll << 40),
+             "fused_attention: too large");
 }
 
 // (D, DV) dispatch onto the launcher template FN<D, DV>(args...)
@@ -381,13 +455,39 @@ inline const __bf16* bp(const at::Tensor& t) {
 }
 inline __bf16* bpm(at::Tensor& t) { return reinterpret_cast<__bf16*>(t.data_ptr()); }
 
+// key / query splits so a launch has >= ~2 workgroups per CU: NS divides the sequence into
+// chunks of whole 64-row blocks
+inline int pick_splits(int64_t tiles, int64_t len) {
+  const int64_t want = (512 + tiles - 1) / tiles;
+  const int64_t maxs = len / 64;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(want, std::min<int64_t>(maxs, 32)));
+}
+inline int split_len(int64_t len, int ns) { return (int)((len / 64 + ns - 1) / ns * 64); }
+
 template <int D, int DV>
 void launch_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& out,
                 at::Tensor& lse, float sl2) {
   const int64_t B = q.size(0), Lq = q.size(1), Lk = k.size(1);
-  hipLaunchKernelGGL((attn_fwd_kernel<D, DV>), dim3((unsigned)(Lq / 64), (unsigned)B),
+  int ns = pick_splits(B * (Lq / 64), Lk);
+  const int klen = split_len(Lk, ns);
+  ns = (int)((Lk + klen - 1) / klen);
+  at::Tensor opart, mpart, lpart;
+  float *op = nullptr, *mp = nullptr, *lp = nullptr;
+  if (ns > 1) {
+    auto fo = q.options().dtype(at::kFloat);
+    opart = at::empty({ns, B, Lq, (int64_t)DV}, fo);
+    mpart = at::empty({ns, B, Lq}, fo);
+    lpart = at::empty({ns, B, Lq}, fo);
+    op = opart.data_ptr<float>();
+    mp = mpart.data_ptr<float>();
+    lp = lpart.data_ptr<float>();
+  }
+  hipLaunchKernelGGL((attn_fwd_kernel<D, DV>), dim3((unsigned)(Lq / 64), (unsigned)ns, (unsigned)B),
                      dim3(kAttnT), 0, stream(), bp(q), bp(k), bp(v), bpm(out),
-                     lse.data_ptr<float>(), (int)Lq, (int)Lk, sl2);
+                     lse.data_ptr<float>(), (int)Lq, (int)Lk, sl2, klen, op, mp, lp);
+  if (ns > 1)
+    hipLaunchKernelGGL(attn_fwd_combine, dim3((unsigned)((B * Lq + 3) / 4)), dim3(256), 0,
+                       stream(), op, mp, lp, bpm(out), lse.data_ptr<float>(), ns, B * Lq, DV);
 }
 
 template <int D, int DV>
@@ -395,14 +495,45 @@ void launch_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                 const at::Tensor& dout, const at::Tensor& lse, const at::Tensor& dsum,
                 at::Tensor& dq, at::Tensor& dk, at::Tensor& dv, float sl2, float sc) {
   const int64_t B = q.size(0), Lq = q.size(1), Lk = k.size(1);
-  hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, DV>), dim3((unsigned)(Lk / 64), (unsigned)B),
-                     dim3(kAttnT), 0, stream(), bp(q), bp(k), bp(v), bp(dout),
-                     lse.data_ptr<float>(), dsum.data_ptr<float>(), bpm(dk), bpm(dv), (int)Lq,
-                     (int)Lk, sl2, sc);
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, DV>), dim3((unsigned)(Lq / 64), (unsigned)B),
-                     dim3(kAttnT), 0, stream(), bp(q), bp(k), bp(v), bp(dout),
-                     lse.data_ptr<float>(), dsum.data_ptr<float>(), bpm(dq), (int)Lq, (int)Lk,
-                     sl2, sc);
+  auto fo = q.options().dtype(at::kFloat);
+  // dK / dV: key tiles x query splits
+  int nq = pick_splits(B * (Lk / 64), Lq);
+  const int qlen = split_len(Lq, nq);
+  nq = (int)((Lq + qlen - 1) / qlen);
+  at::Tensor dkp, dvp;
+  if (nq > 1) {
+    dkp = at::empty({nq, B, Lk, (int64_t)D}, fo);
+    dvp = at::empty({nq, B, Lk, (int64_t)DV}, fo);
+  }
+  hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, DV>),
+                     dim3((unsigned)(Lk / 64), (unsigned)nq, (unsigned)B), dim3(kAttnT), 0,
+                     stream(), bp(q), bp(k), bp(v), bp(dout), lse.data_ptr<float>(),
+                     dsum.data_ptr<float>(), bpm(dk), bpm(dv), (int)Lq, (int)Lk, sl2, sc, qlen,
+                     nq > 1 ? dkp.data_ptr<float>() : nullptr,
+                     nq > 1 ? dvp.data_ptr<float>() : nullptr);
+  if (nq > 1) {
+    const int64_t nk = B * Lk * D, nv = B * Lk * DV;
+    hipLaunchKernelGGL(attn_sum_splits, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0,
+                       stream(), dkp.data_ptr<float>(), bpm(dk), nq, nk);
+    hipLaunchKernelGGL(attn_sum_splits, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0,
+                       stream(), dvp.data_ptr<float>(), bpm(dv), nq, nv);
+  }
+  // dQ: query tiles x key splits
+  int nk2 = pick_splits(B * (Lq / 64), Lk);
+  const int klen = split_len(Lk, nk2);
+  nk2 = (int)((Lk + klen - 1) / klen);
+  at::Tensor dqp;
+  if (nk2 > 1) dqp = at::empty({nk2, B, Lq, (int64_t)D}, fo);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, DV>),
+                     dim3((unsigned)(Lq / 64), (unsigned)nk2, (unsigned)B), dim3(kAttnT), 0,
+                     stream(), bp(q), bp(k), bp(v), bp(dout), lse.data_ptr<float>(),
+                     dsum.data_ptr<float>(), bpm(dq), (int)Lq, (int)Lk, sl2, sc, klen,
+                     nk2 > 1 ? dqp.data_ptr<float>() : nullptr);
+  if (nk2 > 1) {
+    const int64_t n = B * Lq * D;
+    hipLaunchKernelGGL(attn_sum_splits, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       stream(), dqp.data_ptr<float>(), bpm(dq), nk2, n);
+  }
 }
 
 }  // namespace

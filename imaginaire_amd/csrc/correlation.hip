@@ -462,7 +462,7 @@ __global__ __launch_bounds__(256) void corr_bwd_k1(
   }
 }
 
-// Register-blocked variant of corr_bwd_k1 (the default for s2 in {1, 2} and 16-bit inputs): 96
+// Register-blocked variant of corr_bwd_k1 (opt-in, for s2 in {1, 2} and 16-bit inputs): 96
 // pixels x 64 channels per workgroup, each lane owns kRPX = 3 pixels of one parity class (s2
 // apart) x 8 channels. Pixel m at displacement ti reads strip row (m + ti) s2 for d(in1) and
 // (m + 2R - ti) s2 for d(in2), so stepping ti slides a 3-row register window by one row: one
@@ -707,11 +707,12 @@ std::vector<at::Tensor> correlation_backward(const at::Tensor& input1, const at:
   const size_t span = (size_t)(kBX + 2 * R * s2);
   const size_t lds = ((size_t)kBX * D + (span * D + 3) / 4 * 4 + 2 * span * kBCC) * sizeof(float);
   const char* tb = std::getenv("IMAGINAIRE_AMD_CORR_BWD_TILED");
-  // register-blocked tiled kernel (default; IMAGINAIRE_AMD_CORR_BWD_TILED=1 keeps corr_bwd_k1)
+  // register-blocked tiled kernel (IMAGINAIRE_AMD_CORR_BWD_TILED=2): measured 0.69-0.86x
+  // corr_bwd_k1 at the FlowNetC shapes (profiles/corr_bwd_probe_mi355x.txt), so not the default
   const size_t rspan = (size_t)(kRBX + 2 * R * s2);
   const size_t rlds = ((size_t)kRBX * D + (rspan * D + 3) / 4 * 4) * sizeof(float) +
                       2 * rspan * kBCC * a.element_size();
-  if ((tb == nullptr || tb[0] == '2') && ks == 1 && s1 == 1 && (s2 == 1 || s2 == 2) &&
+  if (tb != nullptr && tb[0] == '2' && ks == 1 && s1 == 1 && (s2 == 1 || s2 == 2) &&
       a.element_size() == 2 && C % kBCC == 0 && rlds <= 64 * 1024) {
     IAMD_DISPATCH_FLOAT_TYPES(a.scalar_type(), "correlation_bwd_k1r", [&] {
       dim3 grid(ceil_div(W, kRBX), H, N * (C / kBCC));

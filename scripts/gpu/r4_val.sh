@@ -14,7 +14,8 @@ step() {  # name, timeout, cmd...
 step tests 400 python -u -m pytest tests/test_kernels_gpu.py -m gpu -q --timeout 120 \
   --timeout-method thread -k "${TK:-fused_attention or correlation or spectral or sn_ or adam}"
 [ -z "$PROBES" ] || step attn 300 python scripts/probe/attn_probe.py
-[ -z "$PROBES" ] || step corr 300 python scripts/probe/corr_bwd_probe.py
+[ -z "$PROBES" ] || [ -n "$NOCORR" ] || step corr 300 python scripts/probe/corr_bwd_probe.py
+if [ -n "$FS" ]; then bash scripts/gpu/r4_fs.sh; rc=$?; [ $rc -eq 0 ] || exit $rc; fi
 [ -z "$BENCH" ] || step bench 300 python bench.py --steps 30 --warmup 6
 if [ -n "$TRACE" ]; then
   cd /tmp && export TMPDIR=/tmp

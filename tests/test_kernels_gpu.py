@@ -1745,10 +1745,13 @@ def test_spectral_norm_shadow_result_depends_on_weights_only():
     (2, 256, 256, 32, 66, 1.0),      # K = 1, small head dims (padded to 32 / 96)
     (1, 128, 384, 128, 256, 0.125),  # widest head dims, scaled scores
     (3, 64, 192, 20, 40, 0.5),       # ragged dims padded to 32 / 64
+    (8, 4096, 128, 32, 32, 1.0),     # enough query tiles: forward and dQ without key splits
 ])
 def test_fused_attention_matches_fp32_reference(B, Lq, Lk, d, dv, scale):
     """k16 (csrc/attention.hip): softmax(scale q k^T) v and its gradients against the explicit
-    fp32 formulation on the same bf16-rounded inputs; no attention matrix is materialised."""
+    fp32 formulation on the same bf16-rounded inputs; no attention matrix is materialised. The
+    shapes cover the key-split forward (+ combine), the split backward (+ partial sums) and the
+    unsplit launches."""
     from imaginaire_amd.ops import attention as A
     torch.manual_seed(31)
     q = torch.randn(B, Lq, d, device='cuda').to(torch.bfloat16)
@@ -1762,7 +1765,7 @@ def test_fused_attention_matches_fp32_reference(B, Lq, Lk, d, dv, scale):
     assert o.shape == ref.shape and o.dtype == torch.bfloat16
 
     def rel(a, b):
-        return float((a.float() - b).norm() / b.norm())
+        return float((a.detach().float() - b.detach()).norm() / b.detach().norm())
     assert rel(o, ref) < 1e-2, rel(o, ref)
     go = torch.randn_like(ref)
     o.backward(go.to(torch.bfloat16))
@@ -1788,3 +1791,23 @@ def test_nhwc_concat_into_matches_cat(dtype):
         ref = torch.cat([a, b, torch.zeros(n, cp - ca - cb, h, w, device='cuda', dtype=dtype)], 1)
         assert torch.equal(out[n:], ref)
         assert torch.isnan(out[:n]).all()  # the other half untouched
+
+
+@pytest.mark.gpu
+def test_correlation_backward_register_blocked_kernel(monkeypatch):
+    """The opt-in register-blocked correlation backward (IMAGINAIRE_AMD_CORR_BWD_TILED=2) equals
+    the default tiled kernel's gradients (both fp32 accumulation, different order)."""
+    from imaginaire_amd.ops import _ext
+    torch.manual_seed(34)
+    cl = torch.channels_last
+    for (N, C, H, W, params) in ((1, 128, 24, 200, (20, 1, 20, 1, 2)), (2, 64, 9, 37, (4, 1, 4, 1, 1))):
+        a = torch.randn(N, C, H, W, device='cuda').to(torch.bfloat16).contiguous(memory_format=cl)
+        b = torch.randn(N, C, H, W, device='cuda').to(torch.bfloat16).contiguous(memory_format=cl)
+        y = _ext.ext().correlation_forward(a, b, *params)
+        go = torch.randn(y.shape, device='cuda').contiguous(memory_format=cl)
+        monkeypatch.setenv('IMAGINAIRE_AMD_CORR_BWD_TILED', '1')
+        r1, r2 = _ext.ext().correlation_backward(a, b, go, *params)
+        monkeypatch.setenv('IMAGINAIRE_AMD_CORR_BWD_TILED', '2')
+        g1, g2 = _ext.ext().correlation_backward(a, b, go, *params)
+        for g, r in ((g1, r1), (g2, r2)):
+            assert float((g - r).abs().max()) <= 1e-4 * float(r.abs().max()) + 1e-6
