@@ -17,8 +17,9 @@
 // only the running max needs a 4-lane reduction (xor 16, 32).
 //
 // Shapes: q [B, Lq, D], k [B, Lk, D], v [B, Lk, DV] contiguous bf16; D in {32, 64, 128}, DV a
-// multiple of 32 up to 256 (the caller zero-pads: zero columns change no dot product), Lq and Lk
-// multiples of 64. Scores in the log2 domain: p = exp2(s * scale * log2(e) - lse2).
+// multiple of 32 up to 256, or 288 (the few-shot recipe's 128 + 128 + K value channels in one
+// pass; the caller zero-pads: zero columns change no dot product), Lq and Lk multiples of 64.
+// Every kernel's static LDS stays under 64 KB at D = 128, DV = 288. Scores in the log2 domain: p = exp2(s * scale * log2(e) - lse2).
 #include "common.h"
 
 #include <algorithm>
@@ -420,8 +421,8 @@ void check_attn(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v) {
              "fused_attention: shape mismatch");
   const int64_t d = q.size(2), dvv = v.size(2);
   IAMD_CHECK(d == 32 || d == 64 || d == 128, "fused_attention: head dim must be 32, 64 or 128");
-  IAMD_CHECK(dvv % 32 == 0 && dvv >= 32 && dvv <= 256 && dvv != 224,
-             "fused_attention: value dim must be 32..256 in steps of 32 (not 224)");
+  IAMD_CHECK(dvv % 32 == 0 && dvv >= 32 && dvv <= 288 && dvv != 224,
+             "fused_attention: value dim must be 32..256 in steps of 32 (not 224), or 288");
   IAMD_CHECK(q.size(1) % 64 == 0 && k.size(1) % 64 == 0 && q.size(1) > 0 && k.size(1) > 0,
              "fused_attention: sequence lengths must be multiples of 64");
   IAMD_CHECK(q.size(0) < 65536, "fused_attention: batch too large");
@@ -439,6 +440,7 @@ void check_attn(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v) {
     case 160: FN<DD, 160>(__VA_ARGS__); break;                    \
     case 192: FN<DD, 192>(__VA_ARGS__); break;                    \
     case 256: FN<DD, 256>(__VA_ARGS__); break;                    \
+    case 288: FN<DD, 288>(__VA_ARGS__); break;                    \
     default: IAMD_CHECK(false, "fused_attention: value dim");     \
   }
 #define IAMD_ATTN_DISPATCH(FN, ...)            \

@@ -9,9 +9,11 @@ per key block, dQ per query block; deterministic, no atomics).
 
 ``fused_attention(q, k, v, scale)`` takes q [B, Lq, d], k [B, Lk, d], v [B, Lk, dv] of any float
 dtype and returns [B, Lq, dv] (bf16 on the HIP path). Head dims are zero-padded to the kernel's
-sizes (d -> 32 / 64 / 128, dv -> a multiple of 32): zero columns change no dot product. Shapes
-the kernel does not take (sequence lengths not multiples of 64, d > 128, dv > 256) and CPU
-tensors run PyTorch's ``scaled_dot_product_attention``.
+sizes (d -> 32 / 64 / 128, dv -> a multiple of 32): zero columns change no dot product; value
+widths above 288 run as column chunks (the few-shot vid2vid recipe's 128 + 128 + K channels
+fit one 288-wide pass).
+Shapes the kernel does not take (sequence lengths not multiples of 64, d > 128) and CPU tensors
+run PyTorch's ``scaled_dot_product_attention``.
 
     IMAGINAIRE_AMD_FUSED_ATTN_KERNEL=0   PyTorch SDPA everywhere (A/B switch)
 """
@@ -36,13 +38,27 @@ def _pad_value(dv):
     c = (dv + 31) // 32 * 32
     if c == 224:
         c = 256
-    return c if c <= 256 else None
+    return c if c <= 288 else None
 
 
 def native_ok(q, k, v):
     return (_NATIVE and q.is_cuda and _ext.use_native(q) and q.dim() == 3 and
-            q.shape[1] % 64 == 0 and k.shape[1] % 64 == 0 and
-            _pad_head(q.shape[2]) is not None and _pad_value(v.shape[2]) is not None)
+            q.shape[1] % 64 == 0 and k.shape[1] % 64 == 0 and _pad_head(q.shape[2]) is not None)
+
+
+def _value_chunks(dv):
+    """Column chunks of a value width the kernel takes: one chunk up to 288 (the few-shot
+    recipe's 258), else full 256-wide chunks, then the remainder. Softmax(q k^T) is the same for every chunk and the backward is linear in the
+    chunks' dP (dS = P * (dP - rowsum(dO * O)) sums over them), so chunk outputs concatenate and
+    chunk gradients of q and k add up."""
+    if dv <= 288:
+        return [(0, dv)]
+    out, c0 = [], 0
+    while c0 < dv:
+        w = min(256, dv - c0)
+        out.append((c0, w))
+        c0 += w
+    return out
 
 
 class _FusedAttentionFn(torch.autograd.Function):
@@ -73,10 +89,15 @@ def fused_attention(q, k, v, scale=1.0):
             return F.scaled_dot_product_attention(q.unsqueeze(1), k.to(dt).unsqueeze(1),
                                                   v.to(dt).unsqueeze(1), scale=scale).squeeze(1)
     d, dv = q.shape[2], v.shape[2]
-    D, DV = _pad_head(d), _pad_value(dv)
+    D = _pad_head(d)
     with torch.autocast('cuda', enabled=False):
         qp = F.pad(q.to(torch.bfloat16), (0, D - d)).contiguous()
         kp = F.pad(k.to(torch.bfloat16), (0, D - d)).contiguous()
-        vp = F.pad(v.to(torch.bfloat16), (0, DV - dv)).contiguous()
-        o = _FusedAttentionFn.apply(qp, kp, vp, scale)
-    return o[:, :, :dv] if DV != dv else o
+        vb = v.to(torch.bfloat16)
+        outs = []
+        for c0, w in _value_chunks(dv):
+            DV = _pad_value(w)
+            vp = F.pad(vb[:, :, c0:c0 + w], (0, DV - w)).contiguous()
+            o = _FusedAttentionFn.apply(qp, kp, vp, scale)
+            outs.append(o[:, :, :w] if DV != w else o)
+    return outs[0] if len(outs) == 1 else torch.cat(outs, 2)

@@ -30,7 +30,7 @@ def sdpa(q, k, v):
 
 
 torch.manual_seed(0)
-for B, Lq, K, d, dv in ((1, 1024, 2, 64, 130), (1, 4096, 2, 64, 130), (2, 4096, 4, 128, 250),
+for B, Lq, K, d, dv in ((1, 1024, 2, 64, 130), (1, 4096, 2, 64, 130), (2, 4096, 4, 128, 250), (3, 16384, 2, 128, 258),
                         (1, 8192, 1, 64, 66)):
     Lk = Lq * K
     q = torch.randn(B, Lq, d, device='cuda').to(torch.bfloat16)

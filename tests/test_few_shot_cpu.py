@@ -63,8 +63,10 @@ def test_fused_attention_op_cpu_path_matches_reference():
     from imaginaire_amd.ops import attention as A
     assert [A._pad_head(d) for d in (1, 32, 33, 64, 100, 128, 129)] == [32, 32, 64, 64, 128, 128,
                                                                       None]
-    assert [A._pad_value(d) for d in (2, 32, 130, 200, 224, 256, 257)] == [32, 32, 160, 256, 256,
-                                                                         256, None]
+    assert [A._pad_value(d) for d in (2, 32, 130, 200, 224, 256, 258, 289)] == [
+        32, 32, 160, 256, 256, 256, 288, None]
+    assert A._value_chunks(258) == [(0, 258)] and A._value_chunks(600) == [(0, 256), (256, 256),
+                                                                          (512, 88)]
     torch.manual_seed(0)
     q, k, v = (torch.randn(2, 64, 20, dtype=torch.float64), torch.randn(2, 128, 20,
                                                                         dtype=torch.float64),
