@@ -65,14 +65,14 @@ __device__ __forceinline__ bf16x8 read_a_split(const __bf16* row, int g) {
 
 // ---- forward -----------------------------------------------------------------------------
 // workgroup: 64 queries (wave w: queries 16w..16w+15) x all keys in blocks of 64 staged in LDS
-// (K row-major, V transposed). Per block and wave: S^T (4 key tiles x D/32 MFMAs), the online
+// (K row-major, V^T from a host-transposed copy: 16-byte copies, no LDS transposition). Per block and wave: S^T (4 key tiles x D/32 MFMAs), the online
 // softmax, O^T += V^T P^T (DV/16 tiles x 2 MFMAs).
 // Split over keys (grid.y = split, keys [split * klen, +klen)) when the query tiles alone cannot
 // fill the chip: each split then writes its unnormalised fp32 output with its running max and
 // sum (opart / mpart / lpart), merged by attn_fwd_combine.
 template <int D, int DV>
 __global__ __launch_bounds__(kAttnT) void attn_fwd_kernel(
-    const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v,
+    const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ vt,
     __bf16* __restrict__ o, float* __restrict__ lse2, int Lq, int Lk, float sl2, int klen,
     float* __restrict__ opart, float* __restrict__ mpart, float* __restrict__ lpart) {
   constexpr int KB = 64, KP = D + 8, VP = KB + 8;
@@ -83,7 +83,7 @@ __global__ __launch_bounds__(kAttnT) void attn_fwd_kernel(
   const int l16 = lane & 15, g = lane >> 4;
   const int qi = blockIdx.x * 64 + wid * 16 + l16;  // this lane's query (the B/C column)
   const __bf16* kb = k + (int64_t)b * Lk * D;
-  const __bf16* vb = v + (int64_t)b * Lk * DV;
+  const __bf16* vtb = vt + (int64_t)b * DV * Lk;  // V^T [DV][Lk], transposed once on the host
   bf16x8 qf[D / 32];
 #pragma unroll
   for (int ks = 0; ks < D / 32; ++ks)
@@ -100,11 +100,10 @@ __global__ __launch_bounds__(kAttnT) void attn_fwd_kernel(
       *reinterpret_cast<bf16x8*>(&Ks[r * KP + c]) =
           *reinterpret_cast<const bf16x8*>(kb + (int64_t)(k0 + r) * D + c);
     }
-    for (int e = tid; e < KB * DV / 8; e += kAttnT) {
-      const int r = e / (DV / 8), c = (e - r * (DV / 8)) * 8;
-      const bf16x8 x = *reinterpret_cast<const bf16x8*>(vb + (int64_t)(k0 + r) * DV + c);
-#pragma unroll
-      for (int t = 0; t < 8; ++t) Vt[(c + t) * VP + r] = x[t];
+    for (int e = tid; e < DV * KB / 8; e += kAttnT) {  // 16-byte rows of V^T
+      const int r = e / (KB / 8), c = (e - r * (KB / 8)) * 8;
+      *reinterpret_cast<bf16x8*>(&Vt[r * VP + c]) =
+          *reinterpret_cast<const bf16x8*>(vtb + (int64_t)r * Lk + k0 + c);
     }
     __syncthreads();
     f32x4 s[4];
@@ -214,7 +213,8 @@ __global__ __launch_bounds__(256) void attn_sum_splits(const float* __restrict__
 template <int D, int DV>
 __global__ __launch_bounds__(kAttnT) void attn_bwd_dkv_kernel(
     const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v,
-    const __bf16* __restrict__ dout, const float* __restrict__ lse2,
+    const __bf16* __restrict__ dout, const __bf16* __restrict__ qt,
+    const __bf16* __restrict__ dott, const float* __restrict__ lse2,
     const float* __restrict__ dsum, __bf16* __restrict__ dk, __bf16* __restrict__ dv, int Lq,
     int Lk, float sl2, float scale, int qlen, float* __restrict__ dkpart,
     float* __restrict__ dvpart) {
@@ -231,6 +231,8 @@ __global__ __launch_bounds__(kAttnT) void attn_bwd_dkv_kernel(
   const int ki = blockIdx.x * 64 + wid * 16 + l16;  // this lane's key (the B/C column)
   const __bf16* qb = q + (int64_t)b * Lq * D;
   const __bf16* ob = dout + (int64_t)b * Lq * DV;
+  const __bf16* qtb = qt + (int64_t)b * D * Lq;
+  const __bf16* otb = dott + (int64_t)b * DV * Lq;
   bf16x8 kf[D / 32], vf[DV / 32];
 #pragma unroll
   for (int ks = 0; ks < D / 32; ++ks)
@@ -248,17 +250,23 @@ __global__ __launch_bounds__(kAttnT) void attn_bwd_dkv_kernel(
     __syncthreads();
     for (int e = tid; e < QB * D / 8; e += kAttnT) {
       const int r = e / (D / 8), c = (e - r * (D / 8)) * 8;
-      const bf16x8 x = *reinterpret_cast<const bf16x8*>(qb + (int64_t)(q0 + r) * D + c);
-      *reinterpret_cast<bf16x8*>(&Qs[r * QP + c]) = x;
-#pragma unroll
-      for (int t = 0; t < 8; ++t) Qt[(c + t) * TP + r] = x[t];
+      *reinterpret_cast<bf16x8*>(&Qs[r * QP + c]) =
+          *reinterpret_cast<const bf16x8*>(qb + (int64_t)(q0 + r) * D + c);
+    }
+    for (int e = tid; e < D * QB / 8; e += kAttnT) {  // Q^T rows (host-transposed copy)
+      const int r = e / (QB / 8), c = (e - r * (QB / 8)) * 8;
+      *reinterpret_cast<bf16x8*>(&Qt[r * TP + c]) =
+          *reinterpret_cast<const bf16x8*>(qtb + (int64_t)r * Lq + q0 + c);
     }
     for (int e = tid; e < QB * DV / 8; e += kAttnT) {
       const int r = e / (DV / 8), c = (e - r * (DV / 8)) * 8;
-      const bf16x8 x = *reinterpret_cast<const bf16x8*>(ob + (int64_t)(q0 + r) * DV + c);
-      *reinterpret_cast<bf16x8*>(&Os[r * OP + c]) = x;
-#pragma unroll
-      for (int t = 0; t < 8; ++t) Ot[(c + t) * TP + r] = x[t];
+      *reinterpret_cast<bf16x8*>(&Os[r * OP + c]) =
+          *reinterpret_cast<const bf16x8*>(ob + (int64_t)(q0 + r) * DV + c);
+    }
+    for (int e = tid; e < DV * QB / 8; e += kAttnT) {  // dO^T rows
+      const int r = e / (QB / 8), c = (e - r * (QB / 8)) * 8;
+      *reinterpret_cast<bf16x8*>(&Ot[r * TP + c]) =
+          *reinterpret_cast<const bf16x8*>(otb + (int64_t)r * Lq + q0 + c);
     }
     if (tid < QB) {
       Ls[tid] = lse2[(int64_t)b * Lq + q0 + tid];
@@ -329,8 +337,9 @@ __global__ __launch_bounds__(kAttnT) void attn_bwd_dkv_kernel(
 template <int D, int DV>
 __global__ __launch_bounds__(kAttnT) void attn_bwd_dq_kernel(
     const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v,
-    const __bf16* __restrict__ dout, const float* __restrict__ lse2,
-    const float* __restrict__ dsum, __bf16* __restrict__ dq, int Lq, int Lk, float sl2,
+    const __bf16* __restrict__ dout, const __bf16* __restrict__ kt,
+    const float* __restrict__ lse2, const float* __restrict__ dsum, __bf16* __restrict__ dq,
+    int Lq, int Lk, float sl2,
     float scale, int klen, float* __restrict__ dqpart) {
   constexpr int KB = 32, KP = D + 8, VP = DV + 8, TP = KB + 8;
   __shared__ __attribute__((aligned(16))) __bf16 Ks[KB * KP];
@@ -342,6 +351,7 @@ __global__ __launch_bounds__(kAttnT) void attn_bwd_dq_kernel(
   const int qi = blockIdx.x * 64 + wid * 16 + l16;
   const __bf16* kb = k + (int64_t)b * Lk * D;
   const __bf16* vb = v + (int64_t)b * Lk * DV;
+  const __bf16* ktb = kt + (int64_t)b * D * Lk;
   bf16x8 qf[D / 32], of[DV / 32];
 #pragma unroll
   for (int ks = 0; ks < D / 32; ++ks)
@@ -358,10 +368,13 @@ __global__ __launch_bounds__(kAttnT) void attn_bwd_dq_kernel(
     __syncthreads();
     for (int e = tid; e < KB * D / 8; e += kAttnT) {
       const int r = e / (D / 8), c = (e - r * (D / 8)) * 8;
-      const bf16x8 x = *reinterpret_cast<const bf16x8*>(kb + (int64_t)(k0 + r) * D + c);
-      *reinterpret_cast<bf16x8*>(&Ks[r * KP + c]) = x;
-#pragma unroll
-      for (int t = 0; t < 8; ++t) Kt[(c + t) * TP + r] = x[t];
+      *reinterpret_cast<bf16x8*>(&Ks[r * KP + c]) =
+          *reinterpret_cast<const bf16x8*>(kb + (int64_t)(k0 + r) * D + c);
+    }
+    for (int e = tid; e < D * KB / 8; e += kAttnT) {  // K^T rows (host-transposed copy)
+      const int r = e / (KB / 8), c = (e - r * (KB / 8)) * 8;
+      *reinterpret_cast<bf16x8*>(&Kt[r * TP + c]) =
+          *reinterpret_cast<const bf16x8*>(ktb + (int64_t)r * Lk + k0 + c);
     }
     for (int e = tid; e < KB * DV / 8; e += kAttnT) {
       const int r = e / (DV / 8), c = (e - r * (DV / 8)) * 8;
@@ -484,8 +497,9 @@ void launch_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, a
     mp = mpart.data_ptr<float>();
     lp = lpart.data_ptr<float>();
   }
+  const at::Tensor vt = v.transpose(1, 2).contiguous();  // [B, DV, Lk]
   hipLaunchKernelGGL((attn_fwd_kernel<D, DV>), dim3((unsigned)(Lq / 64), (unsigned)ns, (unsigned)B),
-                     dim3(kAttnT), 0, stream(), bp(q), bp(k), bp(v), bpm(out),
+                     dim3(kAttnT), 0, stream(), bp(q), bp(k), bp(vt), bpm(out),
                      lse.data_ptr<float>(), (int)Lq, (int)Lk, sl2, klen, op, mp, lp);
   if (ns > 1)
     hipLaunchKernelGGL(attn_fwd_combine, dim3((unsigned)((B * Lq + 3) / 4)), dim3(256), 0,
@@ -507,9 +521,10 @@ void launch_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
     dkp = at::empty({nq, B, Lk, (int64_t)D}, fo);
     dvp = at::empty({nq, B, Lk, (int64_t)DV}, fo);
   }
+  const at::Tensor qt = q.transpose(1, 2).contiguous(), dott = dout.transpose(1, 2).contiguous();
   hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, DV>),
                      dim3((unsigned)(Lk / 64), (unsigned)nq, (unsigned)B), dim3(kAttnT), 0,
-                     stream(), bp(q), bp(k), bp(v), bp(dout), lse.data_ptr<float>(),
+                     stream(), bp(q), bp(k), bp(v), bp(dout), bp(qt), bp(dott), lse.data_ptr<float>(),
                      dsum.data_ptr<float>(), bpm(dk), bpm(dv), (int)Lq, (int)Lk, sl2, sc, qlen,
                      nq > 1 ? dkp.data_ptr<float>() : nullptr,
                      nq > 1 ? dvp.data_ptr<float>() : nullptr);
@@ -526,9 +541,10 @@ void launch_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
   nk2 = (int)((Lk + klen - 1) / klen);
   at::Tensor dqp;
   if (nk2 > 1) dqp = at::empty({nk2, B, Lq, (int64_t)D}, fo);
+  const at::Tensor kt = k.transpose(1, 2).contiguous();
   hipLaunchKernelGGL((attn_bwd_dq_kernel<D, DV>),
                      dim3((unsigned)(Lq / 64), (unsigned)nk2, (unsigned)B), dim3(kAttnT), 0,
-                     stream(), bp(q), bp(k), bp(v), bp(dout), lse.data_ptr<float>(),
+                     stream(), bp(q), bp(k), bp(v), bp(dout), bp(kt), lse.data_ptr<float>(),
                      dsum.data_ptr<float>(), bpm(dq), (int)Lq, (int)Lk, sl2, sc, klen,
                      nk2 > 1 ? dqp.data_ptr<float>() : nullptr);
   if (nk2 > 1) {
