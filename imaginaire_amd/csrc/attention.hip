@@ -7,8 +7,8 @@
 // that recompute the probabilities from it (one owns key blocks and accumulates dK, dV; one owns
 // query blocks and accumulates dQ — no atomics, deterministic).
 //
-// MFMA v_mfma_f32_16x16x32_bf16 throughout, 64-wide waves, 16 queries (or keys) per wave, 4 waves
-// per workgroup sharing LDS tiles. Layout trick: scores are computed TRANSPOSED where the next
+// MFMA v_mfma_f32_16x16x32_bf16 throughout, 64-wide waves, 16 queries (or keys) per wave, 4 or 8
+// waves per workgroup sharing LDS tiles. Layout trick: scores are computed TRANSPOSED where the next
 // product needs the probabilities as its B operand — the C layout of one 16x16 tile (lane l holds
 // rows 4*(l/16)+e, column l%16) then feeds the B operand of the next MFMA directly (column l%16,
 // k = 8*(l/16)+t) once the 32-long k dimension is taken in the order {tile 0: rows 4g..4g+3,
@@ -32,7 +32,7 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
-constexpr int kAttnT = 256;  // 4 waves
+
 constexpr float kNegBig = -1.0e30f;
 
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
@@ -70,8 +70,8 @@ __device__ __forceinline__ bf16x8 read_a_split(const __bf16* row, int g) {
 // Split over keys (grid.y = split, keys [split * klen, +klen)) when the query tiles alone cannot
 // fill the chip: each split then writes its unnormalised fp32 output with its running max and
 // sum (opart / mpart / lpart), merged by attn_fwd_combine.
-template <int D, int DV>
-__global__ __launch_bounds__(kAttnT) void attn_fwd_kernel(
+template <int D, int DV, int NW>
+__global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(
     const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ vt,
     __bf16* __restrict__ o, float* __restrict__ lse2, int Lq, int Lk, float sl2, int klen,
     float* __restrict__ opart, float* __restrict__ mpart, float* __restrict__ lpart) {
@@ -81,7 +81,7 @@ __global__ __launch_bounds__(kAttnT) void attn_fwd_kernel(
   const int b = blockIdx.z, sp = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l16 = lane & 15, g = lane >> 4;
-  const int qi = blockIdx.x * 64 + wid * 16 + l16;  // this lane's query (the B/C column)
+  const int qi = blockIdx.x * (NW * 16) + wid * 16 + l16;  // this lane's query (B/C column)
   const __bf16* kb = k + (int64_t)b * Lk * D;
   const __bf16* vtb = vt + (int64_t)b * DV * Lk;  // V^T [DV][Lk], transposed once on the host
   bf16x8 qf[D / 32];
@@ -95,12 +95,12 @@ __global__ __launch_bounds__(kAttnT) void attn_fwd_kernel(
   const int kbeg = sp * klen, kend = min(Lk, kbeg + klen);
   for (int k0 = kbeg; k0 < kend; k0 += KB) {
     __syncthreads();
-    for (int e = tid; e < KB * D / 8; e += kAttnT) {
+    for (int e = tid; e < KB * D / 8; e += NW * 64) {
       const int r = e / (D / 8), c = (e - r * (D / 8)) * 8;
       *reinterpret_cast<bf16x8*>(&Ks[r * KP + c]) =
           *reinterpret_cast<const bf16x8*>(kb + (int64_t)(k0 + r) * D + c);
     }
-    for (int e = tid; e < DV * KB / 8; e += kAttnT) {  // 16-byte rows of V^T
+    for (int e = tid; e < DV * KB / 8; e += NW * 64) {  // 16-byte rows of V^T
       const int r = e / (KB / 8), c = (e - r * (KB / 8)) * 8;
       *reinterpret_cast<bf16x8*>(&Vt[r * VP + c]) =
           *reinterpret_cast<const bf16x8*>(vtb + (int64_t)r * Lk + k0 + c);
@@ -210,8 +210,8 @@ __global__ __launch_bounds__(256) void attn_sum_splits(const float* __restrict__
 // in blocks of 32 staged in LDS both row-major (A operands of S, dP) and transposed (A operands
 // of dV^T, dK^T). S = Q K^T and dP = dO V^T put the key in the lane's column, so P and dS feed
 // dV^T += dO^T P and dK^T += Q^T dS as B operands.
-template <int D, int DV>
-__global__ __launch_bounds__(kAttnT) void attn_bwd_dkv_kernel(
+template <int D, int DV, int NW>
+__global__ __launch_bounds__(NW * 64) void attn_bwd_dkv_kernel(
     const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v,
     const __bf16* __restrict__ dout, const __bf16* __restrict__ qt,
     const __bf16* __restrict__ dott, const float* __restrict__ lse2,
@@ -228,7 +228,7 @@ __global__ __launch_bounds__(kAttnT) void attn_bwd_dkv_kernel(
   const int b = blockIdx.z, sp = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l16 = lane & 15, g = lane >> 4;
-  const int ki = blockIdx.x * 64 + wid * 16 + l16;  // this lane's key (the B/C column)
+  const int ki = blockIdx.x * (NW * 16) + wid * 16 + l16;  // this lane's key (B/C column)
   const __bf16* qb = q + (int64_t)b * Lq * D;
   const __bf16* ob = dout + (int64_t)b * Lq * DV;
   const __bf16* qtb = qt + (int64_t)b * D * Lq;
@@ -248,22 +248,22 @@ __global__ __launch_bounds__(kAttnT) void attn_bwd_dkv_kernel(
   const int qend = min(Lq, (sp + 1) * qlen);
   for (int q0 = sp * qlen; q0 < qend; q0 += QB) {
     __syncthreads();
-    for (int e = tid; e < QB * D / 8; e += kAttnT) {
+    for (int e = tid; e < QB * D / 8; e += NW * 64) {
       const int r = e / (D / 8), c = (e - r * (D / 8)) * 8;
       *reinterpret_cast<bf16x8*>(&Qs[r * QP + c]) =
           *reinterpret_cast<const bf16x8*>(qb + (int64_t)(q0 + r) * D + c);
     }
-    for (int e = tid; e < D * QB / 8; e += kAttnT) {  // Q^T rows (host-transposed copy)
+    for (int e = tid; e < D * QB / 8; e += NW * 64) {  // Q^T rows (host-transposed copy)
       const int r = e / (QB / 8), c = (e - r * (QB / 8)) * 8;
       *reinterpret_cast<bf16x8*>(&Qt[r * TP + c]) =
           *reinterpret_cast<const bf16x8*>(qtb + (int64_t)r * Lq + q0 + c);
     }
-    for (int e = tid; e < QB * DV / 8; e += kAttnT) {
+    for (int e = tid; e < QB * DV / 8; e += NW * 64) {
       const int r = e / (DV / 8), c = (e - r * (DV / 8)) * 8;
       *reinterpret_cast<bf16x8*>(&Os[r * OP + c]) =
           *reinterpret_cast<const bf16x8*>(ob + (int64_t)(q0 + r) * DV + c);
     }
-    for (int e = tid; e < DV * QB / 8; e += kAttnT) {  // dO^T rows
+    for (int e = tid; e < DV * QB / 8; e += NW * 64) {  // dO^T rows
       const int r = e / (QB / 8), c = (e - r * (QB / 8)) * 8;
       *reinterpret_cast<bf16x8*>(&Ot[r * TP + c]) =
           *reinterpret_cast<const bf16x8*>(otb + (int64_t)r * Lq + q0 + c);
@@ -334,8 +334,8 @@ __global__ __launch_bounds__(kAttnT) void attn_bwd_dkv_kernel(
 // workgroup: 64 queries (registers: Q and dO rows as B operands) x all keys in blocks of 32
 // (K row-major and transposed, V row-major in LDS). S^T = K Q^T and dP^T = V dO^T put the query
 // in the lane's column; dQ^T += K^T dS^T.
-template <int D, int DV>
-__global__ __launch_bounds__(kAttnT) void attn_bwd_dq_kernel(
+template <int D, int DV, int NW>
+__global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(
     const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v,
     const __bf16* __restrict__ dout, const __bf16* __restrict__ kt,
     const float* __restrict__ lse2, const float* __restrict__ dsum, __bf16* __restrict__ dq,
@@ -348,7 +348,7 @@ __global__ __launch_bounds__(kAttnT) void attn_bwd_dq_kernel(
   const int b = blockIdx.z, sp = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l16 = lane & 15, g = lane >> 4;
-  const int qi = blockIdx.x * 64 + wid * 16 + l16;
+  const int qi = blockIdx.x * (NW * 16) + wid * 16 + l16;
   const __bf16* kb = k + (int64_t)b * Lk * D;
   const __bf16* vb = v + (int64_t)b * Lk * DV;
   const __bf16* ktb = kt + (int64_t)b * D * Lk;
@@ -366,17 +366,17 @@ __global__ __launch_bounds__(kAttnT) void attn_bwd_dq_kernel(
   const int kend = min(Lk, (sp + 1) * klen);
   for (int k0 = sp * klen; k0 < kend; k0 += KB) {
     __syncthreads();
-    for (int e = tid; e < KB * D / 8; e += kAttnT) {
+    for (int e = tid; e < KB * D / 8; e += NW * 64) {
       const int r = e / (D / 8), c = (e - r * (D / 8)) * 8;
       *reinterpret_cast<bf16x8*>(&Ks[r * KP + c]) =
           *reinterpret_cast<const bf16x8*>(kb + (int64_t)(k0 + r) * D + c);
     }
-    for (int e = tid; e < D * KB / 8; e += kAttnT) {  // K^T rows (host-transposed copy)
+    for (int e = tid; e < D * KB / 8; e += NW * 64) {  // K^T rows (host-transposed copy)
       const int r = e / (KB / 8), c = (e - r * (KB / 8)) * 8;
       *reinterpret_cast<bf16x8*>(&Kt[r * TP + c]) =
           *reinterpret_cast<const bf16x8*>(ktb + (int64_t)r * Lk + k0 + c);
     }
-    for (int e = tid; e < KB * DV / 8; e += kAttnT) {
+    for (int e = tid; e < KB * DV / 8; e += NW * 64) {
       const int r = e / (DV / 8), c = (e - r * (DV / 8)) * 8;
       *reinterpret_cast<bf16x8*>(&Vs[r * VP + c]) =
           *reinterpret_cast<const bf16x8*>(vb + (int64_t)(k0 + r) * DV + c);
@@ -479,11 +479,18 @@ inline int pick_splits(int64_t tiles, int64_t len) {
 }
 inline int split_len(int64_t len, int ns) { return (int)((len / 64 + ns - 1) / ns * 64); }
 
+// 8 waves per workgroup (128 rows sharing each staged tile: half the LDS staging per MFMA)
+// when the rows tile by 128 and that still leaves >= 512 workgroups, else 4
+inline int pick_waves(int64_t rows, int64_t other) {
+  return (rows % 128 == 0 && other * (rows / 128) >= 512) ? 8 : 4;
+}
+
 template <int D, int DV>
 void launch_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& out,
                 at::Tensor& lse, float sl2) {
   const int64_t B = q.size(0), Lq = q.size(1), Lk = k.size(1);
-  int ns = pick_splits(B * (Lq / 64), Lk);
+  const int nw = pick_waves(Lq, B);
+  int ns = pick_splits(B * (Lq / (nw * 16)), Lk);
   const int klen = split_len(Lk, ns);
   ns = (int)((Lk + klen - 1) / klen);
   at::Tensor opart, mpart, lpart;
@@ -498,9 +505,15 @@ void launch_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, a
     lp = lpart.data_ptr<float>();
   }
   const at::Tensor vt = v.transpose(1, 2).contiguous();  // [B, DV, Lk]
-  hipLaunchKernelGGL((attn_fwd_kernel<D, DV>), dim3((unsigned)(Lq / 64), (unsigned)ns, (unsigned)B),
-                     dim3(kAttnT), 0, stream(), bp(q), bp(k), bp(vt), bpm(out),
-                     lse.data_ptr<float>(), (int)Lq, (int)Lk, sl2, klen, op, mp, lp);
+  const dim3 grid((unsigned)(Lq / (nw * 16)), (unsigned)ns, (unsigned)B);
+  if (nw == 8)
+    hipLaunchKernelGGL((attn_fwd_kernel<D, DV, 8>), grid, dim3(512), 0, stream(), bp(q), bp(k),
+                       bp(vt), bpm(out), lse.data_ptr<float>(), (int)Lq, (int)Lk, sl2, klen, op,
+                       mp, lp);
+  else
+    hipLaunchKernelGGL((attn_fwd_kernel<D, DV, 4>), grid, dim3(256), 0, stream(), bp(q), bp(k),
+                       bp(vt), bpm(out), lse.data_ptr<float>(), (int)Lq, (int)Lk, sl2, klen, op,
+                       mp, lp);
   if (ns > 1)
     hipLaunchKernelGGL(attn_fwd_combine, dim3((unsigned)((B * Lq + 3) / 4)), dim3(256), 0,
                        stream(), op, mp, lp, bpm(out), lse.data_ptr<float>(), ns, B * Lq, DV);
@@ -513,7 +526,8 @@ void launch_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
   const int64_t B = q.size(0), Lq = q.size(1), Lk = k.size(1);
   auto fo = q.options().dtype(at::kFloat);
   // dK / dV: key tiles x query splits
-  int nq = pick_splits(B * (Lk / 64), Lq);
+  const int nwk = pick_waves(Lk, B);
+  int nq = pick_splits(B * (Lk / (nwk * 16)), Lq);
   const int qlen = split_len(Lq, nq);
   nq = (int)((Lq + qlen - 1) / qlen);
   at::Tensor dkp, dvp;
@@ -522,12 +536,21 @@ void launch_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
     dvp = at::empty({nq, B, Lk, (int64_t)DV}, fo);
   }
   const at::Tensor qt = q.transpose(1, 2).contiguous(), dott = dout.transpose(1, 2).contiguous();
-  hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, DV>),
-                     dim3((unsigned)(Lk / 64), (unsigned)nq, (unsigned)B), dim3(kAttnT), 0,
-                     stream(), bp(q), bp(k), bp(v), bp(dout), bp(qt), bp(dott), lse.data_ptr<float>(),
-                     dsum.data_ptr<float>(), bpm(dk), bpm(dv), (int)Lq, (int)Lk, sl2, sc, qlen,
-                     nq > 1 ? dkp.data_ptr<float>() : nullptr,
-                     nq > 1 ? dvp.data_ptr<float>() : nullptr);
+  {
+    const dim3 grid((unsigned)(Lk / (nwk * 16)), (unsigned)nq, (unsigned)B);
+    float* dkpp = nq > 1 ? dkp.data_ptr<float>() : nullptr;
+    float* dvpp = nq > 1 ? dvp.data_ptr<float>() : nullptr;
+    if (nwk == 8)
+      hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, DV, 8>), grid, dim3(512), 0, stream(), bp(q),
+                         bp(k), bp(v), bp(dout), bp(qt), bp(dott), lse.data_ptr<float>(),
+                         dsum.data_ptr<float>(), bpm(dk), bpm(dv), (int)Lq, (int)Lk, sl2, sc,
+                         qlen, dkpp, dvpp);
+    else
+      hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, DV, 4>), grid, dim3(256), 0, stream(), bp(q),
+                         bp(k), bp(v), bp(dout), bp(qt), bp(dott), lse.data_ptr<float>(),
+                         dsum.data_ptr<float>(), bpm(dk), bpm(dv), (int)Lq, (int)Lk, sl2, sc,
+                         qlen, dkpp, dvpp);
+  }
   if (nq > 1) {
     const int64_t nk = B * Lk * D, nv = B * Lk * DV;
     hipLaunchKernelGGL(attn_sum_splits, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0,
@@ -536,17 +559,25 @@ void launch_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                        stream(), dvp.data_ptr<float>(), bpm(dv), nq, nv);
   }
   // dQ: query tiles x key splits
-  int nk2 = pick_splits(B * (Lq / 64), Lk);
+  const int nwq = pick_waves(Lq, B);
+  int nk2 = pick_splits(B * (Lq / (nwq * 16)), Lk);
   const int klen = split_len(Lk, nk2);
   nk2 = (int)((Lk + klen - 1) / klen);
   at::Tensor dqp;
   if (nk2 > 1) dqp = at::empty({nk2, B, Lq, (int64_t)D}, fo);
   const at::Tensor kt = k.transpose(1, 2).contiguous();
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, DV>),
-                     dim3((unsigned)(Lq / 64), (unsigned)nk2, (unsigned)B), dim3(kAttnT), 0,
-                     stream(), bp(q), bp(k), bp(v), bp(dout), bp(kt), lse.data_ptr<float>(),
-                     dsum.data_ptr<float>(), bpm(dq), (int)Lq, (int)Lk, sl2, sc, klen,
-                     nk2 > 1 ? dqp.data_ptr<float>() : nullptr);
+  {
+    const dim3 grid((unsigned)(Lq / (nwq * 16)), (unsigned)nk2, (unsigned)B);
+    float* dqpp = nk2 > 1 ? dqp.data_ptr<float>() : nullptr;
+    if (nwq == 8)
+      hipLaunchKernelGGL((attn_bwd_dq_kernel<D, DV, 8>), grid, dim3(512), 0, stream(), bp(q),
+                         bp(k), bp(v), bp(dout), bp(kt), lse.data_ptr<float>(),
+                         dsum.data_ptr<float>(), bpm(dq), (int)Lq, (int)Lk, sl2, sc, klen, dqpp);
+    else
+      hipLaunchKernelGGL((attn_bwd_dq_kernel<D, DV, 4>), grid, dim3(256), 0, stream(), bp(q),
+                         bp(k), bp(v), bp(dout), bp(kt), lse.data_ptr<float>(),
+                         dsum.data_ptr<float>(), bpm(dq), (int)Lq, (int)Lk, sl2, sc, klen, dqpp);
+  }
   if (nk2 > 1) {
     const int64_t n = B * Lq * D;
     hipLaunchKernelGGL(attn_sum_splits, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,

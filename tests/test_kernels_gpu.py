@@ -1751,6 +1751,7 @@ def test_spectral_norm_shadow_result_depends_on_weights_only():
     (8, 4096, 128, 32, 32, 1.0),     # enough query tiles: forward and dQ without key splits
     (1, 256, 512, 128, 258, 1.0),    # the few-shot recipe's value width: one 288-wide pass
     (1, 128, 256, 64, 300, 1.0),     # above 288: two column chunks
+    (16, 4096, 8192, 32, 32, 1.0),   # 8-wave workgroups (128 rows per staged tile) everywhere
 ])
 def test_fused_attention_matches_fp32_reference(B, Lq, Lk, d, dv, scale):
     """k16 (csrc/attention.hip): softmax(scale q k^T) v and its gradients against the explicit
