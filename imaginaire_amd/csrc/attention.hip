@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 namespace iamd {
 namespace {
@@ -480,9 +481,14 @@ inline int pick_splits(int64_t tiles, int64_t len) {
 inline int split_len(int64_t len, int ns) { return (int)((len / 64 + ns - 1) / ns * 64); }
 
 // 8 waves per workgroup (128 rows sharing each staged tile: half the LDS staging per MFMA)
-// when the rows tile by 128 and that still leaves >= 512 workgroups, else 4
+// when the rows tile by 128 and that still leaves >= 256 workgroups, else 4 (at the few-shot
+// recipe shape the 384-workgroup 8-wave forward is 1.38x the 768-workgroup 4-wave one:
+// scripts/probe/attn_wave_ab.py)
 inline int pick_waves(int64_t rows, int64_t other) {
-  return (rows % 128 == 0 && other * (rows / 128) >= 512) ? 8 : 4;
+  // IMAGINAIRE_AMD_ATTN_MIN_WG: the smallest 8-wave grid taken (read per call, A/B)
+  const char* e = std::getenv("IMAGINAIRE_AMD_ATTN_MIN_WG");
+  const int64_t min_wg = e ? std::atoll(e) : 256;
+  return (rows % 128 == 0 && other * (rows / 128) >= min_wg) ? 8 : 4;
 }
 
 template <int D, int DV>
