@@ -19,7 +19,8 @@
 // Shapes: q [B, Lq, D], k [B, Lk, D], v [B, Lk, DV] contiguous bf16; D in {32, 64, 128}, DV a
 // multiple of 32 up to 256, or 288 (the few-shot recipe's 128 + 128 + K value channels in one
 // pass; the caller zero-pads: zero columns change no dot product), Lq and Lk multiples of 64.
-// Every kernel's static LDS stays under 64 KB at D = 128, DV = 288. Scores in the log2 domain: p = exp2(s * scale * log2(e) - lse2).
+// Every kernel's static LDS stays under 64 KB at D = 128, DV = 288. Scores in the log2 domain:
+// p = exp2(s * scale * log2(e) - lse2). Measured: profiles/fs_attention_k16_probe_mi355x.txt.
 #include "common.h"
 
 #include <algorithm>
