@@ -167,3 +167,27 @@ def test_fpse_pool_first_embedding_matches_reference_order():
     ref = d(img, seg)
     for a, b in zip(fast, ref):
         assert torch.allclose(a, b, atol=1e-5, rtol=1e-4)
+
+
+def test_shadow_weight_registry_resync():
+    """optimizers/fused_adam.py shadow registry: a parameter written outside the optimizer (its
+    version counter moves) has its bf16 shadow rewritten by resync_shadows() — what every graph
+    replay runs first — and one never synced (its first forward writes it) is left alone."""
+    from imaginaire_amd.optimizers import fused_adam as FA
+    p = torch.nn.Parameter(torch.randn(4, 3, 3, 3))
+    q = torch.nn.Parameter(torch.randn(5))
+    sp, sq = torch.zeros(4, 3, 3, 3, dtype=torch.bfloat16), torch.zeros(5, dtype=torch.bfloat16)
+    FA.register_shadow(p, sp)
+    FA.register_shadow(q, sq)
+    FA.sync_shadows([p])
+    assert FA.shadow_synced(p) and not FA.shadow_synced(q)
+    assert torch.equal(sp, p.detach().to(torch.bfloat16))
+    with torch.no_grad():
+        p.add_(1.0)  # outside the optimizer
+    assert not FA.shadow_synced(p)
+    assert FA.resync_shadows() == 1
+    assert FA.shadow_synced(p) and torch.equal(sp, p.detach().to(torch.bfloat16))
+    assert torch.equal(sq, torch.zeros(5, dtype=torch.bfloat16))  # never synced: untouched
+    FA.register_shadow(p, None)
+    FA.register_shadow(q, None)
+    assert FA.resync_shadows() == 0
