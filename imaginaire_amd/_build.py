@@ -155,8 +155,10 @@ def build(jobs=None, force=False, verbose=True):
     cmd = [_hipcc(), '-shared', '-fPIC', '--offload-arch=' + ARCH] + sorted(objs) + [
         '-L' + lib, '-lc10', '-lc10_hip', '-ltorch', '-ltorch_cpu', '-ltorch_hip',
         '-ltorch_python', '-Wl,-rpath,' + lib,
-        # RCCL: resolves to the librccl.so.1 torch already loaded (same SONAME)
-        '-L' + os.path.join(os.environ.get('ROCM_PATH', '/opt/rocm'), 'lib'), '-lrccl',
+        # RCCL is NOT linked: its nccl* symbols resolve at load time from the librccl.so that
+        # libtorch_hip already depends on (torch/lib). Linking -lrccl recorded a NEEDED
+        # librccl.so.1 that the loader found in /opt/rocm/lib — a second RCCL copy in the
+        # process whose exit-time destructors corrupted the heap (abort at interpreter exit)
         '-o', TARGET + '.tmp']
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
