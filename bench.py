@@ -286,6 +286,18 @@ def main():
                   'dis_loss', 'dis_back', 'dis_step'):
             print('[bench] phase %-9s %8.1f ms/step' % (
                 k, getattr(trainer, 'accu_%s_iter_time' % k) / n * 1e3), flush=True)
+    # correctness of what was timed: the last step's losses (every rank) and, at world > 1,
+    # whether the replicas still hold bitwise identical parameters (a rank-divergent replay or
+    # unused-parameter mask would desynchronise them silently)
+    losses = _last_losses(trainer)
+    finite = all(v == v and abs(v) != float('inf') for v in losses.values())
+    if world > 1:
+        fl = torch.tensor([0.0 if finite else 1.0], dtype=torch.float64,
+                          device=device if args.backend == 'nccl' and on_gpu else 'cpu')
+        dist.all_reduce(fl, op=dist.ReduceOp.MAX)
+        finite = float(fl.item()) == 0.0
+    in_sync = _replicas_in_sync(trainer, world, device if args.backend == 'nccl' and on_gpu
+                                else torch.device('cpu'))
     ms_per_step = elapsed / args.steps * 1e3
     value = world * bs * args.steps / elapsed
     mem_gb = torch.cuda.max_memory_allocated(device) / 2 ** 30 if on_gpu else 0.0
@@ -315,11 +327,56 @@ def main():
                        ('gloo' if world > 1 else None),
                        'device': args.device},
             'peak_mem_gb_rank0': round(mem_gb, 2),
+            'losses_rank0': losses,
+            'losses_finite': finite,
+            'replicas_in_sync': in_sync,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if not finite:
+        print('[bench] NON-FINITE losses after the timed steps: %s' % json.dumps(losses),
+              file=sys.stderr, flush=True)
+        sys.exit(3)
+    if in_sync is False:
+        print('[bench] replicas hold different parameters after the timed steps',
+              file=sys.stderr, flush=True)
+        sys.exit(4)
+
+
+def _last_losses(trainer):
+    """The last step's D and G losses (graph outputs after a replay) as floats."""
+    import torch
+    out = {}
+    for tag, src in (('G', getattr(trainer, 'gen_losses', {})),
+                     ('D', getattr(trainer, 'dis_losses', {}))):
+        for k, v in src.items():
+            if torch.is_tensor(v) and v.numel() == 1:
+                out['%s/%s' % (tag, k)] = round(float(v), 5)
+    return out
+
+
+def _replicas_in_sync(trainer, world, device):
+    """World > 1: True when every rank holds bitwise identical G and D parameters (one fp64
+    checksum per tensor of the fp32 bits, compared by a MIN / MAX all-reduce); None at world 1."""
+    if world <= 1:
+        return None
+    import torch
+    import torch.distributed as dist
+    sums = []
+    for net in (trainer.net_G, trainer.net_D):
+        if net is None:
+            continue
+        for p in net.parameters():
+            # the int32 view makes the checksum sensitive to every bit of every element
+            bits = p.detach().float().contiguous().view(torch.int32)
+            sums.append(bits.to(torch.float64).sum() + 1e-3 * bits[::7].to(torch.float64).sum())
+    v = torch.stack(sums).to(device)
+    hi, lo = v.clone(), v.clone()
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    return bool(torch.equal(hi, lo))
 
 
 if __name__ == '__main__':

@@ -582,8 +582,9 @@ class AttentionModule(nn.Module):
         v = torch.cat(vals, 2)
         dt = torch.get_autocast_dtype('cuda') if q.is_cuda and torch.is_autocast_enabled('cuda') \
             else q.dtype
-        if fused_attention_ops.native_ok(q, key, v):
+        if dt == torch.bfloat16 and fused_attention_ops.native_ok(q, key, v):
             # the k16 HIP kernel: online softmax over the K*HW keys, no attention matrix in HBM
+            # (bf16 compute only: an fp32 run keeps the fp32 SDPA path and its dtype)
             o = fused_attention_ops.fused_attention(q, key, v, 1.0)
         else:
             # one head dim for q, k and v (zero columns change no dot product)

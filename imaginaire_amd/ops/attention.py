@@ -8,7 +8,8 @@ a per-query log-sum-exp; the backward recomputes the probabilities from it in tw
 per key block, dQ per query block; deterministic, no atomics).
 
 ``fused_attention(q, k, v, scale)`` takes q [B, Lq, d], k [B, Lk, d], v [B, Lk, dv] of any float
-dtype and returns [B, Lq, dv] (bf16 on the HIP path). Head dims are zero-padded to the kernel's
+dtype and returns [B, Lq, dv] in the caller's compute dtype (autocast's, else q's; the kernel
+itself computes in bf16). Head dims are zero-padded to the kernel's
 sizes (d -> 32 / 64 / 128, dv -> a multiple of 32): zero columns change no dot product; value
 widths above 288 run as column chunks (the few-shot vid2vid recipe's 128 + 128 + K channels
 fit one 288-wide pass).
@@ -88,6 +89,9 @@ def fused_attention(q, k, v, scale=1.0):
         with torch.autocast(q.device.type, enabled=False):
             return F.scaled_dot_product_attention(q.unsqueeze(1), k.to(dt).unsqueeze(1),
                                                   v.to(dt).unsqueeze(1), scale=scale).squeeze(1)
+    # the kernel computes in bf16; the result comes back in the compute dtype of the caller
+    # (autocast's, else q's), so an fp32 caller never receives a bf16 tensor
+    out_dt = torch.get_autocast_dtype('cuda') if torch.is_autocast_enabled('cuda') else q.dtype
     d, dv = q.shape[2], v.shape[2]
     D = _pad_head(d)
     with torch.autocast('cuda', enabled=False):
@@ -100,4 +104,5 @@ def fused_attention(q, k, v, scale=1.0):
             vp = F.pad(vb[:, :, c0:c0 + w], (0, DV - w)).contiguous()
             o = _FusedAttentionFn.apply(qp, kp, vp, scale)
             outs.append(o[:, :, :w] if DV != w else o)
-    return outs[0] if len(outs) == 1 else torch.cat(outs, 2)
+    o = outs[0] if len(outs) == 1 else torch.cat(outs, 2)
+    return o if o.dtype == out_dt else o.to(out_dt)

@@ -48,11 +48,20 @@ class BaseTrainer(object):
     # (utils/trainer.py _find_unused_mode, utils/cuda_graph.py graph_supported)
     rank_uniform_control_flow = False
 
+    @classmethod
+    def rank_uniform(cls, cfg):
+        """Whether THIS configuration's iteration is rank-uniform (see above); families whose
+        uniformity depends on the config (the vid2vid family's optional hand discriminator)
+        override it. Read before the trainer exists (utils/trainer.py wraps the networks
+        first)."""
+        return cls.rank_uniform_control_flow
+
     def __init__(self, cfg, net_G, net_D, opt_G, opt_D, sch_G, sch_D, train_data_loader,
                  val_data_loader):
         super().__init__()
         print('Setup trainer.')
         self.cfg = cfg
+        self.rank_uniform_control_flow = type(self).rank_uniform(cfg)
         self.net_G = net_G
         if cfg.trainer.model_average:
             self.net_G_module = self.net_G.module.module

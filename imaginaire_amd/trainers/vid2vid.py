@@ -58,6 +58,18 @@ class Trainer(BaseTrainer):
     # batch shape does; tests/test_graph_families_gpu.py)
     graph_capturable = True
 
+    @classmethod
+    def rank_uniform(cls, cfg):
+        """Rank-uniform unless the config adds the data-dependent discriminators: the
+        reference's ``additional_discriminators`` (the pose recipes' hand / face crops,
+        reference discriminators/fs_vid2vid.py:58-150) run only on batches whose labels hold
+        that part, so ranks can differ in which D parameters get gradients. Without them every
+        rank calls the same networks on every frame (the temporal D / flow nets follow the
+        sequence length, which the epoch schedule sets identically on all ranks): DDP uses the
+        rank-local unused mask and the multi-rank step is captured."""
+        dis = getattr(cfg, 'dis', None)
+        return getattr(dis, 'additional_discriminators', None) is None
+
     def __init__(self, cfg, net_G, net_D, opt_G, opt_D, sch_G, sch_D, train_data_loader,
                  val_data_loader):
         super().__init__(cfg, net_G, net_D, opt_G, opt_D, sch_G, sch_D, train_data_loader,

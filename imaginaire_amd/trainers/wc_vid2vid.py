@@ -26,6 +26,11 @@ class Trainer(Vid2VidTrainer):
     # the world-consistent renderer keeps host-side point-cloud state between frames
     graph_capturable = False
 
+    @classmethod
+    def rank_uniform(cls, cfg):
+        # the guidance renderer's per-sequence host state decides which inputs exist per rank
+        return False
+
     def __init__(self, cfg, net_G, net_D, opt_G, opt_D, sch_G, sch_D, train_data_loader,
                  val_data_loader):
         super().__init__(cfg, net_G, net_D, opt_G, opt_D, sch_G, sch_D, train_data_loader,

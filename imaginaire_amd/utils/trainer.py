@@ -114,9 +114,10 @@ def _calculate_model_size(model):
 def _find_unused_mode(cfg):
     """DDP unused-parameter mode: ``trainer.ddp_find_unused`` when set, else 'local' for the
     trainers whose iteration runs the same networks on every rank
-    (``Trainer.rank_uniform_control_flow``: SPADE, pix2pixHD, MUNIT, UNIT, FUNIT, COCO-FUNIT; no
-    host sync per backward, capturable) and 'global' for the rest (the vid2vid family's hand
-    discriminator runs only on batches with hand pixels)."""
+    (``Trainer.rank_uniform(cfg)``: SPADE, pix2pixHD, MUNIT, UNIT, FUNIT, COCO-FUNIT, and vid2vid /
+    few-shot vid2vid without additional discriminators; no host sync per backward, capturable)
+    and 'global' for the rest (the pose recipes' hand / face discriminators run only on batches
+    with those pixels; wc-vid2vid)."""
     mode = getattr(cfg.trainer, 'ddp_find_unused', None)
     if mode in ('local', 'global'):
         return mode
@@ -124,6 +125,8 @@ def _find_unused_mode(cfg):
         cls = import_module(cfg.trainer.type).Trainer
     except (ImportError, AttributeError):
         return 'global'
+    if hasattr(cls, 'rank_uniform'):
+        return 'local' if cls.rank_uniform(cfg) else 'global'
     return 'local' if getattr(cls, 'rank_uniform_control_flow', False) else 'global'
 
 

@@ -42,6 +42,20 @@ def main():
     p.add_argument('--conv-log', action='store_true',
                    help='after the timed steps, time every conv kernel call of one more '
                         'iteration and print time / TF/s per (kind, shape, kernel) to stderr')
+    p.add_argument('--print-losses', action='store_true',
+                   help='print every iteration\'s D and G losses to stderr (divergence hunts)')
+    p.add_argument('--diag', action='store_true',
+                   help='after every iteration: non-finite parameters / gradients per network and '
+                        'spectral-norm bf16 shadows that differ from bf16(param), on stderr')
+    p.add_argument('--poison', action='store_true',
+                   help='fill every uninitialised allocation with NaN (deterministic mode\'s '
+                        'fill_uninitialized_memory): a kernel reading memory nobody wrote shows')
+    p.add_argument('--flag-probe', action='store_true',
+                   help='with --graph: record isfinite() of every leaf module output / output '
+                        'gradient into the captured graph and print the first non-finite ones '
+                        'after each replay (locates a replay-only NaN)')
+    p.add_argument('--allow-nonfinite', action='store_true',
+                   help='exit 0 even when a final loss is NaN/Inf (default: exit 3)')
     p.add_argument('--set', nargs='*', default=[], metavar='KEY=VALUE',
                    help='dotted config overrides, e.g. gen.num_filters=64 '
                         'data.train.augmentations.random_crop_h_w=256,256 (scale a unit-test '
@@ -55,6 +69,9 @@ def main():
     from imaginaire_amd.utils.trainer import get_model_optimizer_and_scheduler, get_trainer
 
     real_stdout, sys.stdout = sys.stdout, sys.stderr
+    if args.poison:
+        torch.use_deterministic_algorithms(True, warn_only=True)
+        torch.utils.deterministic.fill_uninitialized_memory = True
     device = torch.device('cpu' if args.cpu else 'cuda', 0)
     if device.type == 'cuda':
         torch.cuda.set_device(0)
@@ -122,6 +139,7 @@ def main():
             return [fresh(v) for v in x]
         return x
 
+    probe = _FlagProbe(trainer) if args.flag_probe else None
     graphed = None
     if args.graph:
         from imaginaire_amd.utils.cuda_graph import make_trainer_step
@@ -137,7 +155,11 @@ def main():
     def step(it):
         data = fresh(pool[it % len(pool)])
         data = trainer.start_of_iteration(data, it)
+        if probe is not None:
+            probe.reset()
         train_step(data)
+        if probe is not None:
+            probe.report(it)
         return data
 
     def sync():
@@ -148,6 +170,11 @@ def main():
     for it in range(args.warmup):
         data = step(it)
         print('[bench_families] warmup %d done' % it, flush=True)
+        if args.print_losses:
+            print('[bench_families] it %d losses %s' % (it, json.dumps(_losses(trainer))),
+                  flush=True)
+        if args.diag:
+            _diag(trainer, it)
     sync()
     if device.type == 'cuda':
         try:  # steady-state marker for scripts/gpu/summarize_kernels.py (after warm-up/autotune)
@@ -164,6 +191,11 @@ def main():
         data = step(args.warmup + it)
         sync()
         times.append(time.perf_counter() - t1)
+        if args.print_losses:
+            print('[bench_families] it %d losses %s' % (args.warmup + it,
+                                                       json.dumps(_losses(trainer))), flush=True)
+        if args.diag:
+            _diag(trainer, args.warmup + it)
     dt = (time.perf_counter() - t0) / args.steps
     st = sorted(times)
     med = st[len(st) // 2] if len(st) % 2 else 0.5 * (st[len(st) // 2 - 1] + st[len(st) // 2])
@@ -194,6 +226,9 @@ def main():
         frames = img.shape[1] if torch.is_tensor(img) and img.dim() == 5 else \
             (args.seq_len or 1)
     h, w = ds.h, ds.w
+    losses = _losses(trainer)
+    finite = all(v == v and abs(v) != float('inf')
+                 for part in losses.values() for v in part.values())
     sys.stdout = real_stdout
     print(json.dumps({
         'config': os.path.relpath(args.config),
@@ -212,8 +247,111 @@ def main():
         'peak_mem_gb': round(torch.cuda.max_memory_allocated() / 2 ** 30, 2)
         if device.type == 'cuda' else None,
         'hipgraph': bool(graphed is not None and graphed.graph is not None),
-        'losses': {k: round(float(v), 5) for k, v in trainer.gen_losses.items()
-                   if torch.is_tensor(v) and v.numel() == 1}}), flush=True)
+        'losses': losses['gen'], 'dis_losses': losses['dis'],
+        'losses_finite': finite}), flush=True)
+    if not finite and not args.allow_nonfinite:
+        print('[bench_families] NON-FINITE final losses: %s' % json.dumps(losses),
+              file=sys.stderr, flush=True)
+        sys.exit(3)
+
+
+class _FlagProbe(object):
+    """isfinite() flags of every leaf module's outputs (forward) and output gradients (tensor
+    hooks: no extra autograd nodes) recorded INSIDE the captured graph, read after each replay."""
+
+    MAXF = 1 << 17
+
+    def __init__(self, trainer):
+        import torch
+        self.flags = torch.ones(self.MAXF, dtype=torch.bool, device='cuda')
+        self.labels = []
+        self.slot = 0
+        for net, tag in ((trainer.net_G, 'G'), (trainer.net_D, 'D')):
+            if net is None:
+                continue
+            for n, m in net.named_modules():
+                if len(list(m.children())) == 0:
+                    m._probe_name = tag + '.' + n.replace('module.module.', '')
+                    m.register_forward_hook(self._fwd)
+
+    def _record(self, kind, name, t):
+        import torch
+        if not torch.cuda.is_current_stream_capturing() or not torch.is_tensor(t) or \
+                not t.is_floating_point() or t.numel() == 0 or self.slot >= self.MAXF:
+            return
+        i = self.slot
+        self.slot += 1
+        self.labels.append((kind, name, tuple(t.shape)))
+        self.flags[i:i + 1].copy_(torch.isfinite(t.detach()).all().reshape(1))
+
+    def _fwd(self, mod, inp, out):
+        import torch
+        for o in (out if isinstance(out, (tuple, list)) else [out]):
+            self._record('fwd', mod._probe_name, o)
+            if torch.cuda.is_current_stream_capturing() and torch.is_tensor(o) and \
+                    o.requires_grad:
+                nm = mod._probe_name
+                o.register_hook(lambda g, nm=nm: self._record('dout', nm, g))
+
+    def reset(self):
+        self.flags.fill_(True)
+
+    def report(self, it):
+        if not self.slot:
+            return
+        f = self.flags[:self.slot].cpu()
+        bad = [i for i in range(self.slot) if not bool(f[i])]
+        print('[flag-probe] it %d: %d checks, %d non-finite' % (it, self.slot, len(bad)),
+              flush=True)
+        for i in bad[:12]:
+            print('[flag-probe]    #%d %s %s %s' % ((i,) + self.labels[i]), flush=True)
+
+
+def _diag(trainer, it):
+    """Divergence hunt: non-finite parameters / gradients of every network and spectral-norm
+    shadows (optimizers/fused_adam.py) that no longer equal bf16(param)."""
+    import torch
+    from imaginaire_amd.optimizers import fused_adam as FA
+    out = []
+    for tag in ('net_G', 'net_D'):
+        net = getattr(trainer, tag, None)
+        if net is None:
+            continue
+        bad_p, bad_g, bad_s, n_s = [], [], [], 0
+        gn, pmax, top = 0.0, 0.0, ('', 0.0)
+        for name, p in net.named_parameters():
+            pmax = max(pmax, p.detach().abs().max().item())
+            if p.grad is not None:
+                g2 = p.grad.detach().float().norm().item()
+                gn += g2 * g2
+                if g2 > top[1]:
+                    top = (name, g2)
+            if not torch.isfinite(p).all():
+                bad_p.append(name)
+            if p.grad is not None and not torch.isfinite(p.grad).all():
+                bad_g.append(name)
+            sh = FA.shadow_of(p)
+            if sh is not None:
+                n_s += 1
+                d = (sh.float() - p.detach().to(torch.bfloat16).float()).abs().max().item()
+                if not d == 0.0:
+                    bad_s.append('%s:%.3g' % (name, d))
+        out.append('%s |g| %.3g (max %s %.3g) max|p| %.3g nonfinite params %d %s grads %d %s '
+                   'shadows %d/%d off %s' % (
+                       tag, gn ** 0.5, top[0][-48:], top[1], pmax, len(bad_p), bad_p[:2],
+                       len(bad_g), bad_g[:2], len(bad_s), n_s, bad_s[:3]))
+    print('[bench_families] it %d diag: %s' % (it, ' | '.join(out)), flush=True)
+
+
+def _losses(trainer):
+    """The last iteration's D and G losses as floats ({'gen': {...}, 'dis': {...}})."""
+    import torch
+    out = {}
+    for part, src in (('gen', getattr(trainer, 'gen_losses', {})),
+                      ('dis', getattr(trainer, 'dis_losses', {}))):
+        out[part] = {k: round(float(v), 5) for k, v in src.items()
+                     if torch.is_tensor(v) and v.numel() == 1}
+    return out
 
 
 def _routing():

@@ -1493,6 +1493,39 @@ def test_fused_few_shot_attention_k2_gpu():
     assert (gx2.float() - gx).abs().max() / gx.abs().max() < 5e-2
 
 
+def test_fused_few_shot_attention_fp32_keeps_dtype_gpu():
+    """without bf16 autocast (amp O0) the few-shot attention must return fp32
+    features (the k16 kernel is bf16-only, so this run takes the fp32 path) that match the
+    reference formulation tightly; and ops.attention.fused_attention on fp32 inputs hands back
+    fp32 even when it runs the bf16 kernel."""
+    import types
+    from imaginaire_amd.generators.fs_vid2vid import AttentionModule
+    from imaginaire_amd.layers import Conv2dBlock
+    from imaginaire_amd.ops import attention as attn_ops
+    torch.manual_seed(24)
+    k, b, c, h, w = 2, 2, 64, 16, 16
+    atn_cfg = types.SimpleNamespace(num_downsamples=1)
+    data_cfg = types.SimpleNamespace(initial_few_shot_K=k, num_input_channels=3)
+
+    def block(cin, cout, stride=1):
+        return Conv2dBlock(cin, cout, 3, stride, 1, nonlinearity='leakyrelu')
+    m = AttentionModule(atn_cfg, data_cfg, block, [32, c]).cuda()
+    label = torch.randn(b, 3, 2 * h, 2 * w, device='cuda')
+    ref_label = torch.randn(b * k, 3, 2 * h, 2 * w, device='cuda')
+    x = torch.randn(b * k, c, h, w, device='cuda')
+    out, atn, _ = m(x, label, ref_label)
+    outs, vis = m.fused([x], label, ref_label)
+    assert outs[0].dtype == torch.float32 and vis.dtype == torch.float32
+    assert (outs[0] - out).abs().max().item() <= 1e-3 * out.abs().max().item()
+    q = torch.randn(2, 128, 64, device='cuda')
+    kk = torch.randn(2, 256, 64, device='cuda')
+    v = torch.randn(2, 256, 96, device='cuda')
+    o = attn_ops.fused_attention(q, kk, v, 0.125)
+    assert o.dtype == torch.float32
+    ref = attn_ops.attention_reference(q, kk, v, 0.125)
+    assert (o - ref).abs().max().item() <= 3e-2 * ref.abs().max().item()
+
+
 def test_mt_conv_weight_flip_t_matches_single():
     """The one-launch multi-tensor flip (views of one flat buffer and separate tensors) equals
     conv_weight_flip_t per weight, bitwise; and a conv whose weight was registered with its
