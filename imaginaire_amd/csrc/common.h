@@ -28,6 +28,13 @@ bool stream_capturing();
 // the copy is deferred to flush_deferred_uploads() (multi_tensor.hip).
 at::Tensor stage_to_device(const void* src, size_t bytes, const at::Device& dev);
 int64_t flush_deferred_uploads();
+// Under hipGraph capture: keep ``t``'s storage alive for the life of the process. Every cached
+// device object (multi-tensor table, spectral-norm plan, flip plan, workspace) a capture USES
+// goes through this — including ones made eagerly before the capture and merely hit by it: a
+// later cache eviction would otherwise free memory the graph still reads, and the caching
+// allocator would hand it to the next eager allocation (a replay then reads garbage tables).
+// No-op outside a capture.
+void keep_for_graph(const at::Tensor& t);
 
 #define IAMD_CHECK(cond, ...) TORCH_CHECK(cond, "imaginaire_amd: ", __VA_ARGS__)
 #define IAMD_HIP_CHECK(expr)                                                     \

@@ -633,6 +633,8 @@ std::vector<at::Tensor> mt_conv_weight_flip_t(const std::vector<at::Tensor>& ws)
       it = g_flip_cache.emplace(h, std::move(p)).first;
     }
     pp = &it->second;
+    keep_for_graph(pp->ents);
+    keep_for_graph(pp->blocks);
   }
   auto flat = at::empty({pp->total}, ws[0].options());
   hipLaunchKernelGGL(mt_flip_kernel, dim3(pp->nblocks), dim3(kT), 0, stream(),

@@ -19,6 +19,7 @@
 
 #include <mutex>
 #include <unordered_map>
+#include <unordered_set>
 
 namespace iamd {
 namespace {
@@ -111,6 +112,14 @@ at::Tensor stage_to_device(const void* src, size_t bytes, const at::Device& dev)
   return h.to(dev, /*non_blocking=*/true);
 }
 
+void keep_for_graph(const at::Tensor& t) {
+  if (!t.defined() || !stream_capturing()) return;
+  static std::unordered_set<const void*> kept;
+  std::lock_guard<std::mutex> lk(g_def_mu);
+  const void* key = t.storage().unsafeGetStorageImpl();
+  if (kept.insert(key).second) g_graph_keep.push_back(t);
+}
+
 int64_t flush_deferred_uploads() {
   std::lock_guard<std::mutex> lk(g_def_mu);
   const int64_t n = (int64_t)g_deferred.size();
@@ -148,7 +157,11 @@ Table& get_table(const std::vector<std::vector<at::Tensor>>& lists, const at::De
   }
   std::lock_guard<std::mutex> lk(g_mu);
   auto it = g_cache.find(h);
-  if (it != g_cache.end()) return it->second;
+  if (it != g_cache.end()) {
+    keep_for_graph(it->second.entries);
+    keep_for_graph(it->second.blocks);
+    return it->second;
+  }
   std::vector<TensorEntry> ents(T);
   std::vector<int32_t> bm;
   for (size_t i = 0; i < T; ++i) {
@@ -550,7 +563,13 @@ at::Tensor mt_sn_sigma(const std::vector<at::Tensor>& weights, const std::vector
   {
     std::lock_guard<std::mutex> lk(ws_mu);
     at::Tensor& ws = ws_map[weights[0].get_device()];
-    if (!ws.defined() || ws.numel() < total) ws = at::empty({total}, weights[0].options());
+    if (!ws.defined() || ws.numel() < total) {
+      // the old workspace may be named by a captured graph: never free it
+      static std::vector<at::Tensor> retired;
+      if (ws.defined()) retired.push_back(ws);
+      ws = at::empty({total}, weights[0].options());
+    }
+    keep_for_graph(ws);
     int64_t off = 0;
     for (auto& w : weights) {
       const int64_t cols = w.numel() / std::max<int64_t>(1, w.size(0));

@@ -283,6 +283,12 @@ struct SnPlan {
 std::mutex g_sn_mu;
 std::unordered_map<uint64_t, SnPlan> g_sn_cache;
 
+void keep_plan(const SnPlan& p) {
+  for (const at::Tensor* t : {&p.ents, &p.col_blocks, &p.sum_blocks, &p.row_blocks, &p.t_ws,
+                              &p.s_ws, &p.tp_ws})
+    keep_for_graph(*t);
+}
+
 SnPlan& get_plan(const std::vector<at::Tensor>& W, const std::vector<at::Tensor>& U,
                  const std::vector<at::Tensor>& V, const std::vector<at::Tensor>& WB) {
   uint64_t hsh = 0x51ed270b0b6e3a6dULL;
@@ -296,7 +302,10 @@ SnPlan& get_plan(const std::vector<at::Tensor>& W, const std::vector<at::Tensor>
   }
   std::lock_guard<std::mutex> lk(g_sn_mu);
   auto it = g_sn_cache.find(hsh);
-  if (it != g_sn_cache.end()) return it->second;
+  if (it != g_sn_cache.end()) {
+    keep_plan(it->second);
+    return it->second;
+  }
   const int L = (int)W.size();
   int64_t tot_w = 0, tot_h = 0, tot_p = 0;
   for (int i = 0; i < L; ++i) {
@@ -373,6 +382,7 @@ SnPlan& get_plan(const std::vector<at::Tensor>& W, const std::vector<at::Tensor>
   p.n_col_blocks = (int)(cb.size() / 3);
   p.n_row_blocks = (int)(rb.size() / 2);
   p.L = L;
+  keep_plan(p);
   if (g_sn_cache.size() > 64) g_sn_cache.clear();
   return g_sn_cache.emplace(hsh, std::move(p)).first->second;
 }
@@ -509,7 +519,11 @@ ScPlan& get_sc_plan(const std::vector<at::Tensor>& W, const std::vector<at::Tens
   for (auto& t : S) h ^= reinterpret_cast<uint64_t>(t.data_ptr()) * 0x100000001b3ULL + (h << 7);
   std::lock_guard<std::mutex> lk(g_sc_mu);
   auto it = g_sc_cache.find(h);
-  if (it != g_sc_cache.end()) return it->second;
+  if (it != g_sc_cache.end()) {
+    keep_for_graph(it->second.ents);
+    keep_for_graph(it->second.blocks);
+    return it->second;
+  }
   ScPlan p;
   std::vector<ScEntry> ents;
   std::vector<int32_t> bm;

@@ -299,6 +299,7 @@ def _flip_t(w):
 # reused by another tensor while the entry lives.
 _WFLIP = {}
 _WFLIP_FROZEN = {}
+_GRAPH_KEEP = {}  # cached tensors a captured graph uses (kept for the process lifetime)
 
 
 def register_dgrad_weights(weights, flipped, old_keys=()):
@@ -328,6 +329,9 @@ def _dgrad_weight(wb):
             if len(_WFLIP_FROZEN) > 256:
                 _WFLIP_FROZEN.clear()
             ent = _WFLIP_FROZEN[key] = (wb, _ext.ext().conv_weight_flip_t(wb, 1, 0, 0, 1))
+        if torch.cuda.is_current_stream_capturing():
+            # a captured graph reads this copy on every replay: never let an eviction free it
+            _GRAPH_KEEP[id(ent[1])] = ent
         return ent[1]
     return None
 
@@ -898,6 +902,10 @@ def _pending_union():
     return sorted([(kind, k, v) for (kind, k), v in union.items()], key=lambda e: repr(e[:2]))
 
 
+_TUNE_STATE = {'calls': 0, 'empty': 0}
+_TUNE_QUIET_PERIOD = 64
+
+
 def tune_pending():
     """Resolve the per-shape kernel choices first seen since the last call (wgrad k11 variants /
     k11 vs MIOpen; FlowNet2 deconv k10 phases vs MIOpen): time each candidate on scratch tensors
@@ -910,9 +918,18 @@ def tune_pending():
     multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
     if not multi and not (_WGRAD_PENDING or _DECONV_PENDING):
         return 0
+    if multi:
+        # the union is a collective + host sync: once it has come back empty a few calls in a
+        # row, only every _TUNE_QUIET_PERIOD-th call runs it. Every rank makes the same calls
+        # and sees the same union, so the schedule stays rank-uniform.
+        _TUNE_STATE['calls'] += 1
+        if _TUNE_STATE['empty'] >= 3 and _TUNE_STATE['calls'] % _TUNE_QUIET_PERIOD:
+            return 0
     entries = _pending_union()
     if not entries:
+        _TUNE_STATE['empty'] += 1
         return 0
+    _TUNE_STATE['empty'] = 0
     times = {}
     dev = torch.device('cuda', torch.cuda.current_device())
     cl = torch.channels_last

@@ -45,8 +45,11 @@ class Trainer(BaseTrainer):
         calls a hipGraph capture does not record — replays of the captured MUNIT step then
         differed from each other and from the eager step (D conv bias gradients,
         scripts/probe/graph_eager_diff_probe.py). PyTorch's own convolutions (im2col + rocBLAS)
-        are capture-safe and twice differentiable."""
-        if 'gp' not in self.weights:
+        are capture-safe and twice differentiable. Only a step that is (or must match) a
+        captured one needs that: outside :class:`~imaginaire_amd.utils.cuda_graph.graph_routing`
+        (plain eager loops, tests) MIOpen stays on."""
+        from imaginaire_amd.ops import conv as conv_ops
+        if 'gp' not in self.weights or not conv_ops._GRAPH_ROUTING[0]:
             return super().dis_update(data)
         was = torch.backends.cudnn.enabled
         torch.backends.cudnn.enabled = False

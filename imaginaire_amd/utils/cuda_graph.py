@@ -184,6 +184,9 @@ class graph_routing(object):
         conv._GRAPH_ROUTING[0] -= 1
 
 
+_WARNED = [False]
+
+
 class GraphedStep(object):
     """Runs ``step_fn(data)`` eagerly for ``warmup`` iterations (on a side stream, as
     stream capture requires), then captures it and replays the graph from then on.
@@ -273,6 +276,11 @@ class GraphedStep(object):
 
     def _capture_and_run(self, ent, data):
         from imaginaire_amd.ops import _ext
+        if os.environ.get('DEBUG_CLR_GRAPH_PACKET_CAPTURE', '0') != '0' and not _WARNED[0]:
+            _WARNED[0] = True
+            print('[graph] warning: DEBUG_CLR_GRAPH_PACKET_CAPTURE=%s — long captured steps have '
+                  'replayed with stale operands in this mode (imaginaire_amd/__init__.py)' %
+                  os.environ['DEBUG_CLR_GRAPH_PACKET_CAPTURE'])
         torch.cuda.synchronize()
         t0 = time.time()
         # private copies: the batch source may hand out views of its own pool

@@ -54,15 +54,41 @@ def main():
                    help='with --graph: record isfinite() of every leaf module output / output '
                         'gradient into the captured graph and print the first non-finite ones '
                         'after each replay (locates a replay-only NaN)')
+    p.add_argument('--static-batch', action='store_true',
+                   help='prepare each pooled batch once and hand the same tensors to every '
+                        'iteration (no host-side allocation between graph replays)')
+    p.add_argument('--ab-eager', action='store_true',
+                   help='with --graph: every timed iteration runs twice from one saved state — '
+                        'graph replay, then the eager step — and prints where their losses and '
+                        'gradients part; training continues from the eager result')
+    p.add_argument('--op-probe', action='store_true',
+                   help='like --flag-probe, plus the outputs (and in-place operands) of every HIP '
+                        'extension call, labelled with the enclosing module')
     p.add_argument('--allow-nonfinite', action='store_true',
                    help='exit 0 even when a final loss is NaN/Inf (default: exit 3)')
+    p.add_argument('--gpus', type=int, default=1,
+                   help='ranks (one process per GPU, DDP over RCCL). Without a launcher (no '
+                        'WORLD_SIZE) the script starts them itself through torch.distributed.run; '
+                        'weak scaling: every rank trains its own batch of --batch samples')
+    p.add_argument('--backend', default='nccl',
+                   help='process-group backend for --gpus > 1 (nccl = RCCL; gloo for rehearsals)')
+    p.add_argument('--share-gpu', action='store_true',
+                   help='testing only: every rank uses cuda:0 (needs --backend gloo)')
     p.add_argument('--set', nargs='*', default=[], metavar='KEY=VALUE',
                    help='dotted config overrides, e.g. gen.num_filters=64 '
                         'data.train.augmentations.random_crop_h_w=256,256 (scale a unit-test '
                         'config up to a recipe without another YAML)')
     args = p.parse_args()
+    world_env = os.environ.get('WORLD_SIZE')
+    if world_env is None and args.gpus > 1:
+        sys.exit(_launch_ranks(args, sys.argv[1:]))
+    if world_env is not None and int(world_env) != args.gpus:
+        sys.exit('bench_families.py: --gpus %d but WORLD_SIZE=%s' % (args.gpus, world_env))
+    if args.share_gpu and args.gpus > 1 and args.backend == 'nccl':
+        sys.exit('bench_families.py: --share-gpu needs --backend gloo')
 
     import torch
+    import torch.distributed as dist
     from torch.utils.data import default_collate
     from imaginaire_amd.config import Config
     from imaginaire_amd.datasets.synthetic import Dataset
@@ -72,9 +98,17 @@ def main():
     if args.poison:
         torch.use_deterministic_algorithms(True, warn_only=True)
         torch.utils.deterministic.fill_uninitialized_memory = True
-    device = torch.device('cpu' if args.cpu else 'cuda', 0)
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local_rank = 0 if args.share_gpu else int(os.environ.get('LOCAL_RANK', '0'))
+    device = torch.device('cpu') if args.cpu else torch.device('cuda', local_rank)
     if device.type == 'cuda':
-        torch.cuda.set_device(0)
+        torch.cuda.set_device(local_rank)  # before the process group: rank r -> GPU r
+    if world > 1:
+        from imaginaire_amd.utils.distributed import init_dist
+        init_dist(local_rank, backend=args.backend if device.type == 'cuda' else 'gloo')
+    coll_dev = device if (world > 1 and args.backend == 'nccl' and device.type == 'cuda') \
+        else torch.device('cpu')
     cfg = Config(args.config)
     cfg.logdir = '/tmp/imaginaire_amd_bench_families'
     for kv in args.set:
@@ -127,7 +161,9 @@ def main():
             return [to_dev(v) for v in x]
         return x
 
-    pool = [to_dev(default_collate([ds[(i * bs + j) % max(1, len(ds))] for j in range(bs)]))
+    # every rank trains its own samples (weak scaling)
+    off = rank * bs * args.pool
+    pool = [to_dev(default_collate([ds[(off + i * bs + j) % max(1, len(ds))] for j in range(bs)]))
             for i in range(args.pool)]
 
     def fresh(x):  # some pre-processing (DensePose label remap) edits the batch in place
@@ -139,7 +175,8 @@ def main():
             return [fresh(v) for v in x]
         return x
 
-    probe = _FlagProbe(trainer) if args.flag_probe else None
+    probe = _FlagProbe(trainer, ops=args.op_probe) if (args.flag_probe or args.op_probe) \
+        else None
     graphed = None
     if args.graph:
         from imaginaire_amd.utils.cuda_graph import make_trainer_step
@@ -152,15 +189,28 @@ def main():
         from imaginaire_amd.utils.cuda_graph import make_trainer_step
         train_step, graphed = make_trainer_step(trainer, enabled=False)
 
+    prepared = {}
+
+    def prepare(it):
+        if args.static_batch:
+            k = it % len(pool)
+            if k not in prepared:
+                prepared[k] = trainer.start_of_iteration(fresh(pool[k]), it)
+            trainer.current_iteration = it
+            return prepared[k]
+        return trainer.start_of_iteration(fresh(pool[it % len(pool)]), it)
+
     def step(it):
-        data = fresh(pool[it % len(pool)])
-        data = trainer.start_of_iteration(data, it)
+        data = prepare(it)
         if probe is not None:
             probe.reset()
         train_step(data)
         if probe is not None:
             probe.report(it)
         return data
+
+    step.prepare = prepare
+    step.probe = probe
 
     def sync():
         if device.type == 'cuda':
@@ -185,10 +235,15 @@ def main():
     # per-iteration wall times (synchronised each iteration) -> median and spread; the mean over
     # the whole timed window is reported too (what a throughput number over K steps means)
     times = []
+    if world > 1:
+        dist.barrier()
     t0 = time.perf_counter()
     for it in range(args.steps):
         t1 = time.perf_counter()
-        data = step(args.warmup + it)
+        if args.ab_eager and graphed is not None and graphed.graph is not None:
+            data = _ab_step(trainer, graphed, step, args.warmup + it)
+        else:
+            data = step(args.warmup + it)
         sync()
         times.append(time.perf_counter() - t1)
         if args.print_losses:
@@ -196,7 +251,13 @@ def main():
                                                        json.dumps(_losses(trainer))), flush=True)
         if args.diag:
             _diag(trainer, args.warmup + it)
+    if world > 1:
+        dist.barrier()
     dt = (time.perf_counter() - t0) / args.steps
+    if world > 1:  # the job is as fast as its slowest rank
+        t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
     st = sorted(times)
     med = st[len(st) // 2] if len(st) % 2 else 0.5 * (st[len(st) // 2 - 1] + st[len(st) // 2])
     if args.op_sites and device.type == 'cuda':
@@ -225,64 +286,169 @@ def main():
         img = data.get('images') if isinstance(data, dict) else None
         frames = img.shape[1] if torch.is_tensor(img) and img.dim() == 5 else \
             (args.seq_len or 1)
-    h, w = ds.h, ds.w
     losses = _losses(trainer)
     finite = all(v == v and abs(v) != float('inf')
                  for part in losses.values() for v in part.values())
+    in_sync = None
+    if world > 1:
+        fl = torch.tensor([0.0 if finite else 1.0], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(fl, op=dist.ReduceOp.MAX)
+        finite = float(fl.item()) == 0.0
+        sys.path.insert(0, os.path.dirname(HERE))
+        from bench import _replicas_in_sync
+        in_sync = _replicas_in_sync(trainer, world, coll_dev)
     sys.stdout = real_stdout
+    if rank == 0:
+        _print_row(args, cfg, ds, bs, frames, dt, med, st, device, graphed, losses, finite,
+                   world, in_sync)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if not finite and not args.allow_nonfinite:
+        print('[bench_families] NON-FINITE final losses: %s' % json.dumps(losses),
+              file=sys.stderr, flush=True)
+        sys.exit(3)
+    if in_sync is False:
+        print('[bench_families] replicas hold different parameters', file=sys.stderr, flush=True)
+        sys.exit(4)
+
+
+def _print_row(args, cfg, ds, bs, frames, dt, med, st, device, graphed, losses, finite, world,
+               in_sync):
+    import torch
+    h, w = ds.h, ds.w
     print(json.dumps({
         'config': os.path.relpath(args.config),
         'family': cfg.trainer.type.split('.')[-1],
         'resolution': '%dx%d' % (h, w), 'batch': bs, 'frames_per_sample': frames,
+        'n_gpus': world, 'parallelism': 'dp%d' % world,
         'ms_per_iteration': round(dt * 1e3, 2),
-        'samples_per_s': round(bs / dt, 3), 'frames_per_s': round(bs * frames / dt, 3),
+        # whole-job throughput (every rank trains its own batch)
+        'samples_per_s': round(world * bs / dt, 3),
+        'frames_per_s': round(world * bs * frames / dt, 3),
         'timed_iterations': args.steps, 'warmup': args.warmup,
         'median_ms': round(med * 1e3, 2), 'min_ms': round(st[0] * 1e3, 2),
         'max_ms': round(st[-1] * 1e3, 2),
         'spread_pct': round(100.0 * (st[-1] - st[0]) / med, 2),
-        'median_frames_per_s': round(bs * frames / med, 3),
+        'median_frames_per_s': round(world * bs * frames / med, 3),
         'routing': _routing(),
-        'device': torch.cuda.get_device_name(0) if device.type == 'cuda' else 'cpu',
+        'device': torch.cuda.get_device_name(device) if device.type == 'cuda' else 'cpu',
+        'backend': args.backend if world > 1 else None,
+        'replicas_in_sync': in_sync,
         'data': 'synthetic, random-init weights',
         'peak_mem_gb': round(torch.cuda.max_memory_allocated() / 2 ** 30, 2)
         if device.type == 'cuda' else None,
         'hipgraph': bool(graphed is not None and graphed.graph is not None),
         'losses': losses['gen'], 'dis_losses': losses['dis'],
         'losses_finite': finite}), flush=True)
-    if not finite and not args.allow_nonfinite:
-        print('[bench_families] NON-FINITE final losses: %s' % json.dumps(losses),
-              file=sys.stderr, flush=True)
-        sys.exit(3)
+
+
+def _launch_ranks(args, argv):
+    """``--gpus N`` without a launcher: N ranks through a CHILD torch.distributed.run (nothing
+    has touched the GPU yet; no exec from a process holding a HIP context)."""
+    import socket
+    import subprocess
+    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           '--nproc-per-node=%d' % args.gpus, '--master-addr=127.0.0.1',
+           '--master-port=%d' % port, os.path.abspath(__file__)] + argv
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    env.setdefault('OMP_NUM_THREADS', '4')
+    print('[bench_families] launching %d ranks' % args.gpus, file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env)
 
 
 class _FlagProbe(object):
     """isfinite() flags of every leaf module's outputs (forward) and output gradients (tensor
     hooks: no extra autograd nodes) recorded INSIDE the captured graph, read after each replay."""
 
-    MAXF = 1 << 17
+    MAXF = 1 << 18
 
-    def __init__(self, trainer):
+    def __init__(self, trainer, ops=False):
         import torch
         self.flags = torch.ones(self.MAXF, dtype=torch.bool, device='cuda')
         self.labels = []
         self.slot = 0
+        self.stack = []
         for net, tag in ((trainer.net_G, 'G'), (trainer.net_D, 'D')):
             if net is None:
                 continue
             for n, m in net.named_modules():
+                m._probe_name = tag + '.' + n.replace('module.module.', '')
                 if len(list(m.children())) == 0:
-                    m._probe_name = tag + '.' + n.replace('module.module.', '')
                     m.register_forward_hook(self._fwd)
+                if ops:
+                    m.register_forward_pre_hook(self._push)
+                    m.register_forward_hook(self._pop)
+        self.ops = ops
+        # (a capture with tens of thousands of check nodes crashed graph instantiation: the
+        # op probe stops after the first few thousand checks, i.e. within the first frame)
+        self.limit = int(os.environ.get('IAMD_PROBE_LIMIT', '6000' if ops else str(self.MAXF)))
+        if ops:
+            self._install_op_hooks()
 
-    def _record(self, kind, name, t):
+    def _push(self, mod, inp):
+        self.stack.append(mod._probe_name)
+
+    def _pop(self, mod, inp, out):
+        if self.stack:
+            self.stack.pop()
+
+    def _where(self):
+        return self.stack[-1] if self.stack else '-'
+
+    def _install_op_hooks(self):
+        import torch
+        from imaginaire_amd.ops import _ext
+        probe = self
+
+        def rec_all(kind, out, pop=True):
+            if torch.is_tensor(out):
+                probe._record(kind, probe._where(), out, pop)
+            elif isinstance(out, (list, tuple)):
+                for o in out:
+                    if torch.is_tensor(o):
+                        probe._record(kind, probe._where(), o, pop)
+
+        X = _ext.ext()
+        arg_names = set(os.environ.get('IAMD_PROBE_ARGS', '').split(','))
+        for name in dir(X):
+            fn = getattr(X, name)
+            if name.startswith('_') or not callable(fn) or name in (
+                    'stream_capturing', 'flush_deferred_uploads', 'profile_marker'):
+                continue
+
+            def wrap(fn=fn, name=name):
+                def w(*a, **k):
+                    out = fn(*a, **k)
+                    if torch.cuda.is_current_stream_capturing():
+                        if name in arg_names:  # the operands too (IAMD_PROBE_ARGS=f1,f2)
+                            for ai, t in enumerate(a):
+                                if torch.is_tensor(t):
+                                    probe._record('arg%d:%s' % (ai, name), probe._where(), t)
+                        rec_all('ext:' + name, out)
+                    return out
+                return w
+            setattr(X, name, wrap())
+
+    def _record(self, kind, name, t, pop=True):
         import torch
         if not torch.cuda.is_current_stream_capturing() or not torch.is_tensor(t) or \
-                not t.is_floating_point() or t.numel() == 0 or self.slot >= self.MAXF:
+                not t.is_floating_point() or t.numel() == 0 or self.slot >= self.limit or \
+                getattr(self, '_busy', False):
             return
-        i = self.slot
-        self.slot += 1
-        self.labels.append((kind, name, tuple(t.shape)))
-        self.flags[i:i + 1].copy_(torch.isfinite(t.detach()).all().reshape(1))
+        self._busy = True
+        try:
+            i = self.slot
+            self.slot += 1
+            self.labels.append((kind, name, tuple(t.shape)))
+            self.flags[i:i + 1].copy_(torch.isfinite(t.detach()).all().reshape(1))
+        finally:
+            self._busy = False
 
     def _fwd(self, mod, inp, out):
         import torch
@@ -305,6 +471,96 @@ class _FlagProbe(object):
               flush=True)
         for i in bad[:12]:
             print('[flag-probe]    #%d %s %s %s' % ((i,) + self.labels[i]), flush=True)
+        if bad and getattr(self, 'ops', False):
+            # context around the first non-finite checks
+            fl = f.tolist()
+            for b in bad[:3]:
+                for i in range(max(0, b - 6), min(self.slot, b + 5)):
+                    print('[flag-probe]    %s #%d %s %s %s' % (
+                        ('ok ' if fl[i] else 'BAD', i) + self.labels[i]), flush=True)
+
+
+def _ab_state(tr):
+    ts = list(tr.net_G.parameters()) + list(tr.net_G.buffers())
+    ts += list(tr.net_D.parameters()) + list(tr.net_D.buffers())
+    for o in (tr.opt_G, tr.opt_D):
+        for st in o.state.values():
+            ts += [v for v in st.values() if torch_is_tensor(v)]
+        ts += [g['_hyper'] for g in o.param_groups if '_hyper' in g]
+    return ts
+
+
+def torch_is_tensor(v):
+    import torch
+    return torch.is_tensor(v)
+
+
+def _ab_step(trainer, graphed, step, it, _refs={}):
+    """One iteration run as the eager step and as a graph replay from the same saved state,
+    continuing along the REPLAY trajectory; prints the loss differences and the parameters whose
+    last-frame gradients differ most. The graph's own output tensors (loss dicts, parameter
+    gradients) are grabbed once after a replay and re-installed after every eager run (an eager
+    step rebinds them to fresh tensors)."""
+    import torch
+    from imaginaire_amd.utils.cuda_graph import graph_routing
+    nets = (('G', trainer.net_G), ('D', trainer.net_D))
+    if not _refs:
+        _refs['gen'] = dict(trainer.gen_losses)
+        _refs['dis'] = dict(trainer.dis_losses)
+        _refs['grad'] = [(p, p.grad) for _, net in nets for p in net.parameters()]
+    state = _ab_state(trainer)
+    saved = [t.detach().clone() for t in state]
+
+    def grads():
+        out = {}
+        for tag, net in nets:
+            for n, p in net.named_parameters():
+                if p.grad is not None:
+                    out[tag + '.' + n.replace('module.', '')] = p.grad.detach().float().clone()
+        return out
+
+    data = step.prepare(it)
+    with graph_routing():
+        graphed.step_fn(data)
+    torch.cuda.synchronize()
+    le, ge = _losses(trainer), grads()
+    with torch.no_grad():
+        for t, c in zip(state, saved):
+            t.copy_(c)
+    trainer.gen_losses.clear()
+    trainer.gen_losses.update(_refs['gen'])
+    trainer.dis_losses.clear()
+    trainer.dis_losses.update(_refs['dis'])
+    for p, g in _refs['grad']:
+        p.grad = g
+    probe = getattr(step, 'probe', None)
+    if probe is not None:
+        probe.reset()
+    graphed(data)
+    torch.cuda.synchronize()
+    if probe is not None:
+        probe.report(it)
+    lr, gr = _losses(trainer), grads()
+    dl = {p + '/' + k: (lr[p][k], le[p][k]) for p in lr for k in lr[p]
+          if k in le.get(p, {}) and lr[p][k] != le[p][k]}
+    rows = []
+    for n, b in ge.items():
+        a = gr.get(n)
+        if a is None:
+            rows.append((float('inf'), n + ' (no replay grad)', float(b.norm())))
+            continue
+        d = float((a - b).norm())
+        bn = float(b.norm())
+        if not d == 0.0:
+            rows.append((d / max(bn, 1e-30) if d == d else float('nan'), n, bn))
+    nan_rows = [r for r in rows if r[0] != r[0]]
+    rows = sorted((r for r in rows if r[0] == r[0]), key=lambda r: -r[0])
+    print('[ab] it %d: losses replay vs eager %s | grads differing %d of %d, NaN %d' % (
+        it, sorted(dl.items())[:8], len(rows) + len(nan_rows), len(ge), len(nan_rows)),
+        flush=True)
+    for r in nan_rows[:6] + rows[:8]:
+        print('[ab]    rel %.3g  |eager| %.4g  %s' % (r[0], r[2], r[1][-90:]), flush=True)
+    return data
 
 
 def _diag(trainer, it):

@@ -326,3 +326,53 @@ def test_native_rccl_comm_eager_and_long_capture():
             p.kill()
     assert p.exitcode == 0
     assert res == {'eager': True, 'captured': True}, res
+
+
+@pytest.mark.gpu
+def test_cached_tables_survive_eviction_after_capture():
+    """Round-5 root cause of the few-shot vid2vid replay NaN: a device table / plan made EAGERLY
+    (warm-up) and merely HIT by a capture was freed by a later cache eviction; the next eager
+    allocation then reused its memory and every replay read garbage pointers. Here: EMA table
+    and spectral-norm plans made eagerly, captured, caches overflowed (>256 multi-tensor
+    tables, >64 SN plans), freed memory re-allocated and filled with NaN, then replayed — the
+    replay must still compute the right EMA and sigma."""
+    from imaginaire_amd.ops import _ext
+    X = _ext.ext()
+    torch.manual_seed(5)
+    dev = 'cuda'
+    tg = [torch.randn(257 * (i + 1), device=dev) for i in range(6)]
+    src = [torch.randn_like(t) for t in tg]
+    ws = [torch.randn(64, 48, device=dev) for _ in range(4)]
+    us = [torch.nn.functional.normalize(torch.randn(64, device=dev), dim=0) for _ in ws]
+    vs = [torch.nn.functional.normalize(torch.randn(48, device=dev), dim=0) for _ in ws]
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):  # eager: the tables / plans are made here, outside the graph
+        X.mt_ema(tg, src, 0.5)
+        sig0 = X.mt_sn_power(ws, us, vs, False, 1e-12).clone()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        X.mt_ema(tg, src, 0.5)
+        sig = X.mt_sn_power(ws, us, vs, False, 1e-12)
+    X.flush_deferred_uploads()
+    torch.cuda.synchronize()
+    # overflow both caches with transient operands, then recycle the freed memory as NaN
+    for i in range(300):
+        a = [torch.randn(64 + i, device=dev)]
+        X.mt_ema(a, [torch.randn_like(a[0])], 0.5)
+    for i in range(70):
+        w = [torch.randn(8 + i, 16, device=dev)]
+        X.mt_sn_power(w, [torch.randn(8 + i, device=dev)], [torch.randn(16, device=dev)],
+                      False, 1e-12)
+    torch.cuda.synchronize()
+    junk = [torch.full((1 << 16,), float('nan'), device=dev) for _ in range(64)]
+    torch.cuda.synchronize()
+    before = [t.clone() for t in tg]
+    g.replay()
+    torch.cuda.synchronize()
+    for t, b, sv in zip(tg, before, src):
+        assert torch.allclose(t, 0.5 * b + 0.5 * sv, atol=1e-6), 'EMA replay read a stale table'
+    assert torch.isfinite(sig).all() and torch.equal(sig, sig0), (sig, sig0)
+    del junk
