@@ -376,3 +376,82 @@ def test_cached_tables_survive_eviction_after_capture():
         assert torch.allclose(t, 0.5 * b + 0.5 * sv, atol=1e-6), 'EMA replay read a stale table'
     assert torch.isfinite(sig).all() and torch.equal(sig, sig0), (sig, sig0)
     del junk
+
+
+def _video_dist_capture_worker(port, q, tmp):
+    """vid2vid street at world 1 with the distributed wrappers forced on and NO
+    graph override: the trainer declares rank-uniform control flow for this config, so DDP takes
+    the rank-local unused mask on the native RCCL communicator and the whole per-frame D / G
+    sequence update — with its bucket all-reduces after every per-frame backward — is captured
+    and replays like the eager iteration from the same state."""
+    import faulthandler
+    import sys
+    faulthandler.dump_traceback_later(170, exit=True, file=sys.__stderr__)
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK='0', WORLD_SIZE='1',
+                      LOCAL_RANK='0', IMAGINAIRE_AMD_FORCE_DIST='1')
+    os.environ.pop('IMAGINAIRE_AMD_GRAPH', None)
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group('nccl', rank=0, world_size=1, device_id=torch.device('cuda', 0))
+    sys.path.insert(0, os.path.join(ROOT, 'tests'))
+    from test_graph_families_gpu import _build, _fresh, _losses, _state
+    from imaginaire_amd.parallel import DistributedDataParallel
+    from imaginaire_amd.utils.cuda_graph import graph_routing, make_trainer_step
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    cfg, tr, batches = _build('vid2vid_street', 3)
+    ddps = [m for n in (tr.net_G, tr.net_D) for m in [n] + list(n.modules())
+            if isinstance(m, DistributedDataParallel)]
+    info = {'n_ddp': len(ddps), 'modes': sorted({m.find_unused for m in ddps}),
+            'native': all(m._native is not None for m in ddps),
+            'rank_uniform': bool(tr.rank_uniform_control_flow)}
+    step, graphed = make_trainer_step(tr, warmup=2, enabled=True)
+    for i in range(3):
+        torch.manual_seed(3)
+        step(tr.start_of_iteration(_fresh(batches[i % 2]), i))
+    torch.cuda.synchronize()
+    info['captured'] = graphed is not None and graphed.graph is not None and not graphed.failed
+    state = _state(tr)
+    saved = [t.detach().clone() for t in state]
+    d = tr.start_of_iteration(_fresh(batches[1]), 3)
+    graphed(d)
+    torch.cuda.synchronize()
+    lg = _losses(tr)
+    with torch.no_grad():
+        for t, c in zip(state, saved):
+            t.copy_(c)
+    d = tr.start_of_iteration(_fresh(batches[1]), 3)
+    with graph_routing():
+        graphed.step_fn(d)
+    torch.cuda.synchronize()
+    info['lg'], info['le'] = lg, _losses(tr)
+    q.put(info)
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_vid2vid_capture_with_rccl_collectives(tmp_path):
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    p = ctx.Process(target=_video_dist_capture_worker, args=(port, q, str(tmp_path)))
+    p.start()
+    try:
+        info = q.get(timeout=175)
+    finally:
+        p.join(30)
+        if p.is_alive():
+            p.kill()
+    assert p.exitcode == 0
+    assert info['rank_uniform'] and info['n_ddp'] >= 2, info
+    assert info['modes'] == ['local'] and info['native'], info
+    assert info['captured'], 'the video step with collectives was not captured'
+    lg, le = info['lg'], info['le']
+    assert lg.keys() == le.keys() and lg
+    for k in le:
+        assert lg[k] == lg[k], k
+        assert abs(lg[k] - le[k]) <= 1e-3 * max(1.0, abs(le[k])), (k, lg[k], le[k])
