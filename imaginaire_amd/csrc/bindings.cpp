@@ -105,19 +105,22 @@ std::vector<at::Tensor> resample2d_backward(const at::Tensor& in1, const at::Ten
 // conv_mfma.hip (k10)
 at::Tensor channel_softmax_fwd(const at::Tensor& x);
 at::Tensor conv2d_dgrad_strided(const at::Tensor& dy, const at::Tensor& w, int64_t s, int64_t ph,
-                                int64_t pw, int64_t H, int64_t W, int64_t ncv);
+                                int64_t pw, int64_t H, int64_t W, int64_t ncv,
+                                const c10::optional<at::Tensor>& ascale);
 std::vector<at::Tensor> mt_conv_weight_flip_t(const std::vector<at::Tensor>& ws);
 at::Tensor channel_softmax_bwd(const at::Tensor& y, const at::Tensor& dy);
 at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                        int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
                        double slope, int64_t nb, int64_t ncv,
-                       const c10::optional<at::Tensor>& residual);
+                       const c10::optional<at::Tensor>& residual,
+                       const c10::optional<at::Tensor>& ascale);
 at::Tensor conv2d_dgrad_mfma(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int64_t pw,
-                             int64_t ncv);
+                             int64_t ncv, const c10::optional<at::Tensor>& ascale);
 at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t KH, int64_t KW,
                              int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh,
                              int64_t dw, int64_t out_cout, int64_t out_cin, bool out_bf16,
-                             int64_t nb, int64_t variant);
+                             int64_t nb, int64_t variant,
+                             const c10::optional<std::vector<at::Tensor>>& sn);
 bool conv2d_wgrad_v2_eligible(const at::Tensor& dy, const at::Tensor& x, int64_t KH, int64_t KW,
                               int64_t sh, int64_t sw, int64_t dh, int64_t dw, int64_t nb);
 // conv_tapsplit.hip
@@ -188,15 +191,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv2d_mfma", &iamd::conv2d_mfma, "MFMA implicit-GEMM NHWC conv + bias + act (k10)",
         py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("sh"), py::arg("sw"), py::arg("ph"),
         py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("slope"), py::arg("nb") = 1,
-        py::arg("ncv") = -1, py::arg("residual") = py::none());
+        py::arg("ncv") = -1, py::arg("residual") = py::none(), py::arg("ascale") = py::none());
   m.def("conv2d_dgrad_mfma", &iamd::conv2d_dgrad_mfma,
         "stride-1 conv data gradient from the forward weight (k10 v4 transposed-weight path)",
-        py::arg("dy"), py::arg("w"), py::arg("ph"), py::arg("pw"), py::arg("ncv") = -1);
+        py::arg("dy"), py::arg("w"), py::arg("ph"), py::arg("pw"), py::arg("ncv") = -1,
+        py::arg("ascale") = py::none());
   m.def("conv2d_wgrad_mfma", &iamd::conv2d_wgrad_mfma, "MFMA conv weight gradient (k11)",
         py::arg("dy"), py::arg("x"), py::arg("KH"), py::arg("KW"), py::arg("sh"), py::arg("sw"),
         py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("out_cout") = -1,
         py::arg("out_cin") = -1, py::arg("out_bf16") = false, py::arg("nb") = 1,
-        py::arg("variant") = 0);
+        py::arg("variant") = 0, py::arg("sn") = py::none());
   m.def("conv2d_wgrad_v2_eligible", &iamd::conv2d_wgrad_v2_eligible,
         "whether the k11 v2 (one wave per SIMD) kernel can run this weight gradient",
         py::arg("dy"), py::arg("x"), py::arg("KH"), py::arg("KW"), py::arg("sh"), py::arg("sw"),
@@ -209,7 +213,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv2d_dgrad_strided", &iamd::conv2d_dgrad_strided,
         "strided-conv data gradient: all s*s phase convs in one k10 launch, stored in place",
         py::arg("dy"), py::arg("w"), py::arg("s"), py::arg("ph"), py::arg("pw"), py::arg("H"),
-        py::arg("W"), py::arg("ncv") = -1);
+        py::arg("W"), py::arg("ncv") = -1, py::arg("ascale") = py::none());
   m.def("conv_tap_sum", &iamd::conv_tap_sum, "tap-split conv: sum of per-tap partials (+bias)");
   m.def("conv_tap_gather", &iamd::conv_tap_gather, "tap-split conv backward: dy -> per-tap dZ");
   m.def("conv_phase_scatter", &iamd::conv_phase_scatter,

@@ -134,6 +134,74 @@ wgrad_finalize_kernel(const float* __restrict__ part, T* __restrict__ out, int S
   }
 }
 
+// As wgrad_finalize_kernel (fp32 out, real dims), with the spectral-norm backward applied:
+//   dW[co][t][ci] = G / sigma - (<G, W> / sigma^2) u[co] v[ci * KK + t]
+// where <G, W> = sum of the k11 blocks' partials dotp[0 .. ndot) (every block sums them itself,
+// in a fixed order) and v is in the reference's logical column order (ci, kh, kw).
+template <bool VEC>
+__global__ void __launch_bounds__(kT)
+wgrad_finalize_sn_kernel(const float* __restrict__ part, float* __restrict__ out, int S, int Cop,
+                         int Cip, int Cout, int Cin, int KK, int G,
+                         const float* __restrict__ dotp, int ndot, const float* __restrict__ u,
+                         const float* __restrict__ v, const float* __restrict__ sigma) {
+  __shared__ float4 red[kT];
+  __shared__ float dsh[kT / 64];
+  const int opb = kT / G;
+  const int tid = threadIdx.x, o = tid % opb, g = tid / opb;
+  float dd = 0.f;
+  for (int k = tid; k < ndot; k += kT) dd += dotp[k];
+  dd = wave_sum(dd);
+  if ((tid & 63) == 0) dsh[tid >> 6] = dd;
+  __syncthreads();
+  float dot = 0.f;
+#pragma unroll
+  for (int k = 0; k < kT / 64; ++k) dot += dsh[k];
+  const float inv = 1.f / sigma[0];
+  const float cf = dot * inv * inv;  // <G, W> / sigma^2
+  const int per = VEC ? Cin / 4 : Cin;
+  const int64_t n = (int64_t)Cout * KK * per;
+  const int64_t slab = (int64_t)Cop * KK * Cip;
+  for (int64_t i0 = (int64_t)blockIdx.x * opb; i0 < n; i0 += (int64_t)gridDim.x * opb) {
+    const int64_t i = i0 + o;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int64_t rt = 0, src = 0;
+    int c = 0, t = 0, co = 0;
+    if (i < n) {
+      c = (int)(i % per);
+      rt = i / per;  // co * KK + t
+      t = (int)(rt % KK);
+      co = (int)(rt / KK);
+      src = ((int64_t)co * KK + t) * Cip + (VEC ? c * 4 : c);
+      for (int sl = g; sl < S; sl += G) {
+        if constexpr (VEC) {
+          const float4 w4 = *reinterpret_cast<const float4*>(part + sl * slab + src);
+          acc.x += w4.x; acc.y += w4.y; acc.z += w4.z; acc.w += w4.w;
+        } else {
+          acc.x += part[sl * slab + src];
+        }
+      }
+    }
+    red[tid] = acc;
+    __syncthreads();
+    if (g == 0 && i < n) {
+      for (int k = 1; k < G; ++k) {
+        const float4 w4 = red[k * opb + o];
+        acc.x += w4.x; acc.y += w4.y; acc.z += w4.z; acc.w += w4.w;
+      }
+      const float cu = cf * u[co];
+      if constexpr (VEC) {
+        const float* vv = v + (int64_t)c * 4 * KK + t;
+        *reinterpret_cast<float4*>(out + rt * Cin + c * 4) =
+            make_float4(fmaf(acc.x, inv, -cu * vv[0]), fmaf(acc.y, inv, -cu * vv[KK]),
+                        fmaf(acc.z, inv, -cu * vv[2 * KK]), fmaf(acc.w, inv, -cu * vv[3 * KK]));
+      } else {
+        out[rt * Cin + c] = fmaf(acc.x, inv, -cu * v[(int64_t)c * KK + t]);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // padded index o -> source index along one axis (mode 0 reflect, 1 replicate)
 __device__ __forceinline__ int pad_src(int o, int p, int n, int mode) {
   int i = o - p;
@@ -685,6 +753,42 @@ at::Tensor wgrad_finalize(const at::Tensor& part, int64_t S, int64_t Cop, int64_
   if (dtype == at::kBFloat16) launch(__hip_bfloat16());
   else if (dtype == at::kFloat) launch(float());
   else IAMD_CHECK(false, "wgrad_finalize: bf16 or fp32 output expected");
+  IAMD_LAUNCH_CHECK();
+  return out;
+}
+
+at::Tensor wgrad_finalize_sn(const at::Tensor& part, int64_t S, int64_t Cop, int64_t Cip,
+                             int64_t Cout, int64_t Cin, int64_t KH, int64_t KW,
+                             const at::Tensor& dotp, const at::Tensor& u, const at::Tensor& v,
+                             const at::Tensor& sigma) {
+  IAMD_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() &&
+                 part.numel() >= S * Cop * KH * KW * Cip && Cout <= Cop && Cin <= Cip,
+             "wgrad_finalize_sn: slab shape");
+  IAMD_CHECK(dotp.scalar_type() == at::kFloat && u.scalar_type() == at::kFloat &&
+                 v.scalar_type() == at::kFloat && sigma.scalar_type() == at::kFloat &&
+                 u.numel() == Cout && v.numel() == Cin * KH * KW && sigma.numel() == 1 &&
+                 u.is_contiguous() && v.is_contiguous() && dotp.is_contiguous(),
+             "wgrad_finalize_sn: u / v / sigma / partials");
+  auto out = at::empty({Cout, Cin, KH, KW},
+                       part.options().dtype(at::kFloat).memory_format(at::MemoryFormat::ChannelsLast));
+  const int KK = (int)(KH * KW);
+  const bool vec = Cin % 4 == 0 && Cip % 4 == 0;
+  const int64_t n = Cout * KK * (vec ? Cin / 4 : Cin);
+  if (n == 0) return out;
+  int G = 1;
+  while (G < 16 && G < S && (n * G * 2 <= (int64_t)256 * 4096 || G * 8 < S)) G *= 2;
+  const int opb = kT / G;
+  const int blocks = (int)std::min<int64_t>((n + opb - 1) / opb, 8192);
+  if (vec)
+    hipLaunchKernelGGL((wgrad_finalize_sn_kernel<true>), dim3(blocks), dim3(kT), 0, stream(),
+                       part.data_ptr<float>(), out.data_ptr<float>(), (int)S, (int)Cop, (int)Cip,
+                       (int)Cout, (int)Cin, KK, G, dotp.data_ptr<float>(), (int)dotp.numel(),
+                       u.data_ptr<float>(), v.data_ptr<float>(), sigma.data_ptr<float>());
+  else
+    hipLaunchKernelGGL((wgrad_finalize_sn_kernel<false>), dim3(blocks), dim3(kT), 0, stream(),
+                       part.data_ptr<float>(), out.data_ptr<float>(), (int)S, (int)Cop, (int)Cip,
+                       (int)Cout, (int)Cin, KK, G, dotp.data_ptr<float>(), (int)dotp.numel(),
+                       u.data_ptr<float>(), v.data_ptr<float>(), sigma.data_ptr<float>());
   IAMD_LAUNCH_CHECK();
   return out;
 }

@@ -74,7 +74,16 @@ struct ConvArgs {
   // residual block whose branch ends in this conv (reference layers/residual.py:150
   // ``x_shortcut + dx``) lands in the epilogue instead of a separate full-tensor add
   const __hip_bfloat16* res;
+  // spectrally normalised weight (layers/spectral_norm.py): the operand w is bf16(W) and the
+  // epilogue scales the accumulator by 1 / *ascale (sigma, a device scalar written by the power
+  // iteration in the same graph) before the bias: conv(x, W / sigma) without a W / sigma copy.
+  // nullptr: no scale.
+  const float* ascale = nullptr;
 };
+
+__device__ __forceinline__ float ascale_of(const ConvArgs& a) {
+  return a.ascale ? 1.f / a.ascale[0] : 1.f;
+}
 
 // y[off .. off + 8) = v (+ res[off .. off + 8) when the conv carries a residual), one 16-byte
 // store. The residual is added to the bf16-rounded conv output and rounded again: the same
@@ -293,6 +302,7 @@ __device__ __forceinline__ void conv_v1_impl(const ConvArgs& a, int bid, int spl
   // ---- epilogue: bias + activation -> bf16 tile in LDS -> 16-byte row stores --------------
   __syncthreads();
   char* E = smem;
+  const float asc = ascale_of(a);
   __hip_bfloat16* yz = a.y + (size_t)zb * a.ybs;
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
@@ -303,7 +313,7 @@ __device__ __forceinline__ void conv_v1_impl(const ConvArgs& a, int bid, int spl
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int rl = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-        float v = acc[i][j][r] + bv;
+        float v = fmaf(acc[i][j][r], asc, bv);
         v = v > 0.f ? v : v * a.slope;
         *reinterpret_cast<__hip_bfloat16*>(E + rl * kEpiStride + cl * 2) = __float2bfloat16(v);
       }
@@ -511,6 +521,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v2(ConvArgs a) {
 
   __syncthreads();  // every wave is done reading the ring: reuse it for the epilogue tile
   char* E = smem;
+  const float asc = ascale_of(a);
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
     const int cl = wn * 64 + j * 16 + (lane & 15);
@@ -520,7 +531,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v2(ConvArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int rl = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-        float v = acc[i][j][r] + bv;
+        float v = fmaf(acc[i][j][r], asc, bv);
         v = v > 0.f ? v : v * a.slope;
         *reinterpret_cast<__hip_bfloat16*>(E + rl * kEpiStride + cl * 2) = __float2bfloat16(v);
       }
@@ -762,6 +773,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v3(ConvArgs a) {
 
   // ---- epilogue: 128-column slices through LDS, 16-byte row stores ------------------------
   char* E = smem;
+  const float asc = ascale_of(a);
 #pragma unroll
   for (int half = 0; half < BN / 128; ++half) {
     if ((wn >> 1) == half) {
@@ -775,7 +787,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v3(ConvArgs a) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int rl = wm * 128 + i * 16 + (lane >> 4) * 4 + r;
-            float v = acc[i][j][r] + bv;
+            float v = fmaf(acc[i][j][r], asc, bv);
             v = v > 0.f ? v : v * a.slope;
             *reinterpret_cast<__hip_bfloat16*>(E + rl * kEpiStride + cl * 2) = __float2bfloat16(v);
           }
@@ -1094,6 +1106,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v4(ConvArgs a) {
     return;
   }
   char* E = smem;
+  const float asc = ascale_of(a);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int cl = wn * 64 + j * 16 + (lane & 15);
@@ -1103,7 +1116,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v4(ConvArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int rl = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-        float v = acc[i][j][r] + bv;
+        float v = fmaf(acc[i][j][r], asc, bv);
         v = v > 0.f ? v : v * a.slope;
         *reinterpret_cast<__hip_bfloat16*>(E + rl * kEpiStride + cl * 2) = __float2bfloat16(v);
       }
@@ -1342,6 +1355,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v5(ConvArgs a) {
     return;
   }
   char* E = smem;
+  const float asc = ascale_of(a);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int cl = wn * 64 + j * 16 + (lane & 15);
@@ -1351,7 +1365,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v5(ConvArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int rl = wm * 128 + i * 16 + (lane >> 4) * 4 + r;
-        float v = acc[i][j][r] + bv;
+        float v = fmaf(acc[i][j][r], asc, bv);
         v = v > 0.f ? v : v * a.slope;
         *reinterpret_cast<__hip_bfloat16*>(E + rl * kEpi + cl * 2) = __float2bfloat16(v);
       }
@@ -1375,6 +1389,7 @@ __global__ void __launch_bounds__(256)
 conv_splitk_reduce(const float* __restrict__ part, const float* __restrict__ bias,
                    __hip_bfloat16* __restrict__ y, int S, int64_t MC, int C, float slope,
                    ConvArgs map) {
+  const float asc = ascale_of(map);
   for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < MC / 8;
        v += (int64_t)gridDim.x * blockDim.x) {
     const int64_t e = v * 8;
@@ -1394,7 +1409,7 @@ conv_splitk_reduce(const float* __restrict__ part, const float* __restrict__ bia
     const int zb = (int)(e / ((int64_t)map.M * C));  // sample of a batched launch
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      float t = acc[k] + (bias ? bias[zb * map.bbs + c + k] : 0.f);
+      float t = fmaf(acc[k], asc, bias ? bias[zb * map.bbs + c + k] : 0.f);
       acc[k] = t > 0.f ? t : t * slope;
     }
     const int64_t m = e / C - (int64_t)zb * map.M;
@@ -1675,13 +1690,22 @@ void run_conv(ConvArgs& a, const at::Tensor& x) {
 
 }  // namespace
 
+// The optional epilogue scale operand: a 1-element fp32 CUDA tensor (sigma) or nothing.
+static const float* ascale_ptr(const c10::optional<at::Tensor>& t, const char* who) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  IAMD_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->numel() == 1, who,
+             ": ascale must be a 1-element fp32 CUDA tensor");
+  return t->data_ptr<float>();
+}
+
 // y[B, Cout, Ho, Wo] (channels-last) = act(conv2d(x, w) + bias), x/w channels-last bf16.
 // nb > 1: a batch of nb independent convs with per-sample weights, w [nb * Cout, Cin, KH, KW]
 // (sample-major), bias [nb * Cout]: y[b] = act(conv2d(x[b], w[b]) + bias[b]).
 at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                        int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw,
                        double slope, int64_t nb, int64_t ncv,
-                       const c10::optional<at::Tensor>& residual) {
+                       const c10::optional<at::Tensor>& residual,
+                       const c10::optional<at::Tensor>& ascale) {
   IAMD_CHECK(x.is_cuda() && w.is_cuda(), "conv2d_mfma: CUDA tensors expected");
   IAMD_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16,
              "conv2d_mfma: bf16 operands expected");
@@ -1745,6 +1769,8 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
                "like the output (single-weight convs only)");
     a.res = reinterpret_cast<const __hip_bfloat16*>(r.data_ptr());
   }
+  a.ascale = ascale_ptr(ascale, "conv2d_mfma");
+  IAMD_CHECK(a.ascale == nullptr || nb == 1, "conv2d_mfma: ascale is for single-weight convs");
   run_conv(a, x);
   return y;
 }
@@ -1768,7 +1794,7 @@ static bool dgrad_bt_enabled() {
 // path the forward weight is read directly (tap-flipped, k-major, transposing LDS reads): no
 // flipped copy of the weight per backward; other shapes flip once and run the k10 routing.
 at::Tensor conv2d_dgrad_mfma(const at::Tensor& dy, const at::Tensor& w, int64_t ph, int64_t pw,
-                             int64_t ncv) {
+                             int64_t ncv, const c10::optional<at::Tensor>& ascale) {
   IAMD_CHECK(dy.is_cuda() && w.is_cuda() && dy.scalar_type() == at::kBFloat16 &&
                  w.scalar_type() == at::kBFloat16 && dy.dim() == 4 && w.dim() == 4,
              "conv2d_dgrad_mfma: 4-D bf16 CUDA tensors expected");
@@ -1793,7 +1819,8 @@ at::Tensor conv2d_dgrad_mfma(const at::Tensor& dy, const at::Tensor& w, int64_t 
                   (int64_t)B * a.Ho * a.Wo * N < (1ll << 31) && dgrad_bt_enabled();
   if (!ok) {
     const at::Tensor wt = conv_weight_flip_t(w, 1, 0, 0, 1);
-    return conv2d_mfma(dy, wt, c10::nullopt, 1, 1, tph, tpw, 1, 1, 1.0, 1, ncv, c10::nullopt);
+    return conv2d_mfma(dy, wt, c10::nullopt, 1, 1, tph, tpw, 1, 1, 1.0, 1, ncv, c10::nullopt,
+                       ascale);
   }
   if (ncv < 0) ncv = N;
   IAMD_CHECK(ncv == N || (ncv > 0 && ncv < N && ncv % 8 == 0),
@@ -1814,6 +1841,7 @@ at::Tensor conv2d_dgrad_mfma(const at::Tensor& dy, const at::Tensor& w, int64_t 
   a.slope = 1.f;
   a.oH = a.Ho; a.oW = a.Wo; a.osy = 1; a.osx = 1; a.ory = 0; a.orx = 0;
   a.res = nullptr;
+  a.ascale = ascale_ptr(ascale, "conv2d_dgrad_mfma");
   run_v4(a, dy, true);
   return y;
 }
@@ -1827,7 +1855,8 @@ at::Tensor conv2d_dgrad_mfma(const at::Tensor& dy, const at::Tensor& w, int64_t 
 // phase starts inside dy). Replaces per phase one launch + one scatter pass
 // (ops/conv.py _strided_dgrad). ncv: channels of dx stored (<= Cin, multiple of 8).
 at::Tensor conv2d_dgrad_strided(const at::Tensor& dy, const at::Tensor& w, int64_t s, int64_t ph,
-                                int64_t pw, int64_t H, int64_t W, int64_t ncv) {
+                                int64_t pw, int64_t H, int64_t W, int64_t ncv,
+                                const c10::optional<at::Tensor>& ascale) {
   IAMD_CHECK(dy.is_cuda() && w.is_cuda() && dy.scalar_type() == at::kBFloat16 &&
                  w.scalar_type() == at::kBFloat16 && dy.dim() == 4 && w.dim() == 4,
              "conv2d_dgrad_strided: 4-D bf16 CUDA tensors expected");
@@ -1889,6 +1918,7 @@ at::Tensor conv2d_dgrad_strided(const at::Tensor& dy, const at::Tensor& w, int64
       a.ory = ry; a.orx = rx;
       a.xbs = a.wbs = a.ybs = 0; a.bbs = 0; a.nz = 1;
       a.ldy = (int)ncv;
+      a.ascale = ascale_ptr(ascale, "conv2d_dgrad_strided");
       phases.push_back(a);
     }
   }

@@ -54,7 +54,39 @@ struct WgradArgs {
   // batch of independent weight gradients (per-sample weights), one per blockIdx.y: operand
   // strides in elements between samples; slabs are [S][nz][Cout][KK][Cin]
   int64_t dybs, xbs;
+  // spectrally normalised weight (layers/spectral_norm.py): the epilogue also sums G * W over
+  // the block's outputs (W = the bf16 shadow, real dims [wsn_cout][KK][wsn_cin]) into
+  // dotp[blockIdx.x]; their total is <G, W> for the SN backward, folded into wgrad_finalize_sn
+  const __hip_bfloat16* wsn = nullptr;
+  float* dotp = nullptr;
+  int wsn_cout = 0, wsn_cin = 0;
 };
+
+// one output's share of <G, W> (outputs in the zero-padded channel tail contribute nothing).
+// Branch-free: the load always runs (clamped into the real weight in the tail) so the compiler can issue
+// every load of the epilogue back to back; a load under a per-element branch got its own
+// vmcnt(0) wait, serialising ~100 round trips per thread.
+__device__ __forceinline__ float sn_term(const WgradArgs& a, int n, int tap, int ci, float gv) {
+  const int nn = min(n, a.wsn_cout - 1), cc = min(ci, a.wsn_cin - 1);
+  const float w = __bfloat162float(a.wsn[(nn * a.KK + tap) * a.wsn_cin + cc]);
+  return (n < a.wsn_cout && ci < a.wsn_cin) ? gv * w : 0.f;
+}
+
+// block total of the per-thread <G, W> shares -> dotp[blockIdx.x] (fixed order: deterministic).
+// The epilogues sum their shares BEFORE writing the slab: with the slab stores interleaved, every
+// W load's wait would also wait for the stores issued before it (vmcnt counts both on CDNA).
+__device__ void sn_dot_store(const WgradArgs& a, float d) {
+  __shared__ float red[kThreads / 64];
+  d = wave_sum(d);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = d;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < kThreads / 64; ++k) t += red[k];
+    a.dotp[blockIdx.x] = t;
+  }
+}
 
 // 16-byte chunk swizzle of a [64 pixel rows][RB bytes] image: the 8 rows read by one 32-lane
 // half of a transposed fragment read land in distinct 32-byte bank windows.
@@ -280,6 +312,18 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_mfma(WgradArgs a) {
 
   // ---- fp32 partial slab: row n (4 per lane), column ci (16 lanes contiguous) -------------
   float* o = a.out + ((size_t)split * gridDim.y + zb) * a.Cout * a.KK * a.Cin;
+  if (a.wsn) {  // <G, W> share first (see sn_dot_store)
+    float sd = 0.f;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          sd += sn_term(a, n0 + wm * (BNO / 2) + i * 16 + g * 4 + r, tap,
+                        c0 + wn * (BC / 2) + j * 16 + (lane & 15), acc[i][j][r]);
+    sn_dot_store(a, sd);
+  }
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -570,6 +614,20 @@ __global__ __launch_bounds__(kThreads, (NT == 5 && BNO == 64) ? 3 : 2) void conv
   }
 
   float* o = a.out + ((size_t)split * gridDim.y + zb) * a.Cout * a.KK * a.Cin;
+  if (a.wsn) {  // <G, W> share first (see sn_dot_store)
+    float sd = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            sd += sn_term(a, n0 + wm * (BNO / 2) + i * 16 + g * 4 + r, ky * a.KW + t,
+                          c0 + wn * (BC / 2) + j * 16 + (lane & 15), acc[t][i][j][r]);
+    sn_dot_store(a, sd);
+  }
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int tap = ky * a.KW + t;
@@ -803,6 +861,20 @@ __global__ __launch_bounds__(kThreads, 1) void conv_wgrad_mfma_w4(WgradArgs a) {
 
   // ---- fp32 partial slab [S][Cout][KK][Cin]: row n (4 per lane), column ci (16 lanes) ------
   float* o = a.out + (size_t)split * a.Cout * a.KK * a.Cin;
+  if (a.wsn) {  // <G, W> share first (see sn_dot_store)
+    float sd = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            sd += sn_term(a, n0 + wm * 64 + i * 16 + g * 4 + r, ky * a.KW + t,
+                          c0 + wn * (BC / 2) + j * 16 + (lane & 15), acc[t][i][j][r]);
+    sn_dot_store(a, sd);
+  }
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int tap = ky * a.KW + t;
@@ -826,6 +898,11 @@ __global__ __launch_bounds__(kThreads, 1) void conv_wgrad_mfma_w4(WgradArgs a) {
 at::Tensor wgrad_finalize(const at::Tensor& part, int64_t S, int64_t Cop, int64_t Cip,
                           int64_t Cout, int64_t Cin, int64_t KH, int64_t KW,
                           at::ScalarType dtype);
+// ... and the spectral-norm backward folded into the same pass (fp32 dW of W)
+at::Tensor wgrad_finalize_sn(const at::Tensor& part, int64_t S, int64_t Cop, int64_t Cip,
+                             int64_t Cout, int64_t Cin, int64_t KH, int64_t KW,
+                             const at::Tensor& dotp, const at::Tensor& u, const at::Tensor& v,
+                             const at::Tensor& sigma);
 
 // dW [out_cout, out_cin, KH, KW] (channels-last memory = [Cout][KH][KW][Cin]) in fp32, or bf16
 // when out_bf16; out_cout / out_cin < 0 keep the (padded) channel counts of dy / x. Cropping
@@ -851,7 +928,8 @@ bool conv2d_wgrad_v2_eligible(const at::Tensor& dy, const at::Tensor& x, int64_t
 at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t KH, int64_t KW,
                              int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh,
                              int64_t dw, int64_t out_cout, int64_t out_cin, bool out_bf16,
-                             int64_t nb, int64_t variant) {
+                             int64_t nb, int64_t variant,
+                             const c10::optional<std::vector<at::Tensor>>& sn) {
   IAMD_CHECK(dy.is_cuda() && x.is_cuda(), "conv2d_wgrad_mfma: CUDA tensors expected");
   IAMD_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16,
              "conv2d_wgrad_mfma: bf16 operands expected");
@@ -956,7 +1034,34 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
   S = ceil_div(a.nks, a.kps);  // no empty split
   const int64_t oc = out_cout < 0 ? Cout : out_cout, oi = out_cin < 0 ? Cin : out_cin;
   IAMD_CHECK(oc <= Cout && oi <= Cin, "conv2d_wgrad_mfma: crop larger than the operands");
-  const bool direct = S == 1 && !out_bf16 && oc == Cout && oi == Cin;
+  // sn = {shadow bf16 [oc, oi, KH, KW] channels-last, u [oc], v [oi * KH * KW], sigma [1]}: the
+  // weight is spectrally normalised and dW is the gradient w.r.t. the fp32 parameter W of
+  // W / sigma (reference torch.nn.utils.spectral_norm, u / v constant):
+  //   dW = G / sigma - (<G, W> / sigma^2) u v^T,  G = the k11 gradient w.r.t. W / sigma,
+  // with <G, W> summed in the k11 epilogue (one partial per block) and the rest applied by
+  // wgrad_finalize_sn in the pass that sums the split-K slabs: no bf16 G round trip and no
+  // separate <G, W> / apply passes (layers/spectral_norm.py _SNScale.backward)
+  const bool use_sn = sn.has_value() && !sn->empty();
+  at::Tensor dotp;
+  if (use_sn) {
+    IAMD_CHECK(nb == 1 && sn->size() == 4, "conv2d_wgrad_mfma: sn = [shadow, u, v, sigma]");
+    const at::Tensor& shw = (*sn)[0];
+    IAMD_CHECK(shw.is_cuda() && shw.scalar_type() == at::kBFloat16 && shw.dim() == 4 &&
+                   shw.size(0) == oc && shw.size(1) == oi && shw.size(2) == KH &&
+                   shw.size(3) == KW && shw.is_contiguous(at::MemoryFormat::ChannelsLast),
+               "conv2d_wgrad_mfma: the SN shadow must be the bf16 weight [out_cout, out_cin, KH, "
+               "KW] channels-last");
+    IAMD_CHECK((*sn)[1].numel() == oc && (*sn)[2].numel() == oi * KH * KW &&
+                   (*sn)[3].numel() == 1 && (*sn)[1].scalar_type() == at::kFloat &&
+                   (*sn)[2].scalar_type() == at::kFloat && (*sn)[3].scalar_type() == at::kFloat,
+               "conv2d_wgrad_mfma: SN u / v / sigma sizes");
+    a.wsn = reinterpret_cast<const __hip_bfloat16*>(shw.data_ptr());
+    a.wsn_cout = (int)oc;
+    a.wsn_cin = (int)oi;
+    dotp = at::empty({(int64_t)tiles * S}, x.options().dtype(at::kFloat));
+    a.dotp = dotp.data_ptr<float>();
+  }
+  const bool direct = !use_sn && S == 1 && !out_bf16 && oc == Cout && oi == Cin;
   at::Tensor dW, part;
   if (direct) {
     dW = at::empty({nb * Cout, Cin, KH, KW},
@@ -1053,6 +1158,9 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
   else launch(I64(), I64());
   IAMD_LAUNCH_CHECK();
   if (direct) return dW;
+  if (use_sn)
+    return wgrad_finalize_sn(part, S, Cout, Cin, oc, oi, KH, KW, dotp, (*sn)[1].contiguous(),
+                             (*sn)[2].contiguous(), (*sn)[3]);
   if (nb > 1)  // slabs [S][nb][Cout][KK][Cin]: one [nb * Cout] output, no crop
     return wgrad_finalize(part, S, nb * Cout, Cin, nb * Cout, Cin, KH, KW,
                           out_bf16 ? at::kBFloat16 : at::kFloat);

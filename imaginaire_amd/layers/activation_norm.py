@@ -372,6 +372,10 @@ class SpatiallyAdaptiveNorm(nn.Module):
                                               weight_norm_type=weight_norm_type))
                 self.betas.append(conv_block(mlp_ch, num_features, kernel_size, padding=padding,
                                              weight_norm_type=weight_norm_type))
+                # γ and β run as ONE conv over their concatenated weights (_gb): their spectral
+                # norm group materialises bf16(W / sigma) for them back to back (zero-copy cat)
+                for blk in (self.gammas[-1], self.betas[-1]):
+                    blk.layers.conv._iamd_sn_materialize = True
             else:
                 mlp += [conv_block(mlp_ch, num_features * 2, kernel_size, padding=padding,
                                    weight_norm_type=weight_norm_type)]

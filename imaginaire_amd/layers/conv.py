@@ -29,7 +29,8 @@ from .nonlinearity import act_slope
 
 def _plain_conv_weight(conv):
     from .weight_norm import get_weight
-    return get_weight(conv)
+    # (an ops.conv.SNWeight for a batched spectral-norm conv: the conv ops take it as is)
+    return get_weight(conv, ref=isinstance(conv, nn.Conv2d))
 
 
 def _fusible_conv(layer):
@@ -42,6 +43,8 @@ def _fusible_conv(layer):
 
 def _conv_nobias(layer, x):
     w = _plain_conv_weight(layer)
+    if isinstance(w, nhwc_conv.SNWeight) and not isinstance(layer, nn.Conv2d):
+        w = w.materialize()
     if isinstance(layer, nn.Linear):
         return F.linear(x, w, None)
     if isinstance(layer, nn.Conv2d):

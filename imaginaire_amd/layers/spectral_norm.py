@@ -35,6 +35,13 @@ _SN_FLIP = os.environ.get('IMAGINAIRE_AMD_SN_FLIP', '1') == '1'
 # IMAGINAIRE_AMD_SN_SHADOW=0: the power iteration and the W / sigma cast read the fp32 weights
 # (default: a bf16 copy of each weight that the optimizer step writes in its own pass)
 _SN_SHADOW = os.environ.get('IMAGINAIRE_AMD_SN_SHADOW', '1') == '1'
+# IMAGINAIRE_AMD_SN_FUSED=0: every SN conv gets a materialised bf16(W / sigma) (the k5c cast)
+# and the separate <G, W> / apply backward passes. Default (with shadows): a plain SN conv that
+# runs on k10 / k11 takes its bf16 shadow directly, 1 / sigma rides in the conv epilogues
+# (forward and data gradient) and the SN backward in the weight gradient's split-K sum
+# (ops/conv.py _MfmaConv2d with an SNWeight): no W / sigma copy, no bf16 G round trip, no per-layer SN
+# backward launches.
+_SN_FUSED = os.environ.get('IMAGINAIRE_AMD_SN_FUSED', '1') == '1'
 
 
 class _SNScale(torch.autograd.Function):
@@ -80,17 +87,39 @@ def w_shape(w):
     return tuple(w.shape)
 
 
+def materialize_scaled(weight, sigma, shadow):
+    """bf16(W / sigma) of ONE layer from its shadow (the fused group left it unmaterialised
+    and a consumer needs the tensor: a linear layer, the tap-split head, an eager MIOpen conv)."""
+    with torch.no_grad():
+        return _ext.ext().mt_sn_scale_cast([weight], sigma.reshape(1), [shadow], 1)[0]
+
+
 def _autocast_bf16(dev):
     return torch.is_autocast_enabled(dev) and torch.get_autocast_dtype(dev) == torch.bfloat16
 
 
 class SpectralNorm(_TorchSN):
+    def weight_ref(self, module):
+        """The pending batched iteration's result as an ``ops.conv.SNWeight`` (unmaterialised
+        W / sigma) for a plain conv whose group left it to the fused conv path; else None."""
+        batched = getattr(self, '_batched', None)
+        if batched is None or batched[3] is not None or batched[4] is None or \
+                type(module) is not torch.nn.Conv2d or module.groups != 1 or \
+                not _autocast_bf16(batched[4].device.type):
+            return None
+        self._batched = None
+        from imaginaire_amd.ops.conv import SNWeight
+        u, v, sigma, _, shadow = batched
+        return SNWeight(getattr(module, self.name + '_orig'), shadow, u, v, sigma, self, module)
+
     def compute_weight(self, module, do_power_iteration):
         batched = getattr(self, '_batched', None)
         if batched is not None:
             self._batched = None  # consumed: a second call this forward iterates itself
             weight = getattr(module, self.name + '_orig')
             u, v, sigma, w16, shadow = batched
+            if w16 is None and shadow is not None and _autocast_bf16(weight.device.type):
+                w16 = materialize_scaled(weight, sigma, shadow)
             if w16 is not None and _autocast_bf16(weight.device.type):
                 return _SNScaleCast.apply(weight, u, v, sigma, w16, shadow)
             return _SNScale.apply(weight, u, v, sigma)
@@ -179,6 +208,7 @@ class _SNGroup:
         bf16 = _autocast_bf16(w0.device.type)
         with torch.no_grad():
             shadows = self._shadows(ws) if (bf16 and net.training and _SN_SHADOW) else None
+            fused = False
             if shadows is not None:
                 # the optimizer's step writes bf16(W) with the update: the GEMV passes and the
                 # W / sigma cast read half the bytes. Stale shadows (first step, a loaded or
@@ -186,15 +216,35 @@ class _SNGroup:
                 # an eager step and a graph replay from the same state agree bitwise.
                 self._sync_stale(ws)
                 sigma = X.mt_sn_power(ws, us, vs, True, eps, shadows)
-                w16 = X.mt_sn_scale_cast(ws, sigma, shadows, 1)
+                if _SN_FUSED:
+                    # only the layers that must hand a tensor on (the SPADE γ|β pairs, one conv
+                    # over their concatenated weights) get bf16(W / sigma), back to back in one
+                    # launch; the others stay unmaterialised for the fused conv path
+                    fused = True
+                    pre = self._pre_materialize()
+                    w16 = [None] * len(ws)
+                    if pre:
+                        sub = X.mt_sn_scale_cast([ws[i] for i in pre],
+                                                 sigma.index_select(0, self._pre_index(sigma)),
+                                                 [shadows[i] for i in pre], 1)
+                        for i, t in zip(pre, sub):
+                            w16[i] = t
+                else:
+                    w16 = X.mt_sn_scale_cast(ws, sigma, shadows, 1)
             else:
                 sigma = X.mt_sn_power(ws, us, vs, bool(net.training), eps)
                 w16 = X.mt_sn_scale_cast(ws, sigma) if bf16 else [None] * len(ws)
             # snapshots of u, v for the backward (the next forward updates them in place)
             u_all = torch.cat(us)
             v_all = torch.cat(vs)
-        if w16[0] is not None and torch.is_grad_enabled() and net.training and _SN_FLIP:
-            self._flip_for_dgrad(w16)
+        if torch.is_grad_enabled() and net.training and _SN_FLIP:
+            if fused:
+                # the fused convs' data gradients run on the flipped SHADOW (1 / sigma in the
+                # epilogue); the γ|β pairs flip their concatenated weight in the backward
+                self._flip_for_dgrad([shadows[i] if w16[i] is None else None
+                                      for i in range(len(ws))])
+            elif w16[0] is not None:
+                self._flip_for_dgrad(w16)
         ou = ov = 0
         for i, (m, h) in enumerate(self.entries):
             nu, nv = us[i].numel(), vs[i].numel()
@@ -202,6 +252,26 @@ class _SNGroup:
                           shadows[i] if shadows is not None else None)
             ou += nu
             ov += nv
+
+    def _pre_materialize(self):
+        """Entries whose module asks for a materialised bf16(W / sigma) (``_iamd_sn_
+        materialize``: the SPADE γ / β convs), in entry order; cached per group."""
+        pre = getattr(self, '_pre', None)
+        if pre is None or len(pre[1]) != len(self.entries):
+            # (and every non-Conv2d SN layer — linear / 1-D / 3-D / transposed: no fused path)
+            idx = [i for i, (m, _) in enumerate(self.entries)
+                   if getattr(m, '_iamd_sn_materialize', False) or type(m) is not torch.nn.Conv2d
+                   or m.groups != 1]
+            pre = self._pre = (idx, list(self.entries))
+            self._pre_t = None
+        return pre[0]
+
+    def _pre_index(self, like):
+        t = getattr(self, '_pre_t', None)
+        if t is None or t.device != like.device:
+            t = self._pre_t = torch.tensor(self._pre_materialize(), dtype=torch.long,
+                                           device=like.device)
+        return t
 
     def _shadows(self, ws):
         """bf16 copies of the group's weights, one per parameter and shared by every group that
@@ -235,7 +305,8 @@ class _SNGroup:
         (instead of one flip per conv in the backward: ~220 small launches per SPADE step)."""
         from imaginaire_amd.ops import conv as nhwc_conv
         sel = [i for i, (m, _) in enumerate(self.entries)
-               if type(m) is torch.nn.Conv2d and tuple(m.stride) == (1, 1) and
+               if w16[i] is not None and
+               type(m) is torch.nn.Conv2d and tuple(m.stride) == (1, 1) and
                tuple(m.dilation) == (1, 1) and m.groups == 1 and w16[i].dim() == 4 and
                w16[i].shape[0] % 64 == 0 and w16[i].shape[1] % 64 == 0 and
                w16[i].is_contiguous(memory_format=torch.channels_last)]

@@ -33,14 +33,23 @@ def _wn_hook(module):
     return None
 
 
-def get_weight(module):
+def get_weight(module, ref=False):
     """Effective weight of a conv/linear, running one SN power iteration in training.
 
     Mirrors what the module's own forward would use; call at most once per
     forward pass per module (the power iteration updates ``weight_u``).
+    ``ref=True`` (callers that hand the weight straight to ``ops.conv.conv2d`` /
+    ``conv2d_act``): a spectrally normalised plain Conv2d whose batched iteration left its
+    W / sigma unmaterialised comes back as an ``ops.conv.SNWeight`` — the conv then runs on the
+    bf16 shadow with 1 / sigma in its epilogue and the SN backward folded into its weight
+    gradient (layers/spectral_norm.py).
     """
     hook = _sn_hook(module)
     if hook is not None:
+        if ref and hasattr(hook, 'weight_ref'):
+            r = hook.weight_ref(module)
+            if r is not None:
+                return r
         w = hook.compute_weight(module, do_power_iteration=module.training)
         setattr(module, hook.name, w)
         return w

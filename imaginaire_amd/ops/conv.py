@@ -353,13 +353,14 @@ _STRIDED_DGRAD_MIN_PIX = int(os.environ.get('IMAGINAIRE_AMD_STRIDED_DGRAD_MIN_PI
 _STRIDED_ONE_LAUNCH = os.environ.get('IMAGINAIRE_AMD_STRIDED_ONE_LAUNCH', '1') == '1'
 
 
-def _strided_dgrad(dy, wb, H, W, s, padding, wts=None, ncv=-1):
+def _strided_dgrad(dy, wb, H, W, s, padding, wts=None, ncv=-1, ascale=None):
     """Data gradient of a stride-``s`` conv (weight ``wb`` [Cout, Cin, KH, KW], channels-last
     bf16) as s*s stride-1 phase convolutions on k10. Input row i = s*q + r receives
     dy[q + c0 - j] * w[kh0 + s*j] for kh0 = (r + p) mod s, c0 = (r + p - kh0) / s: a J-tap
     correlation of dy with the flipped phase sub-kernel (``conv_weight_flip_t(w, s, kh0, kw0)``),
     whose output rows [m0, m0 + Q) are scattered into the parity sub-grid of dx
-    (``conv_phase_scatter``). Same FLOPs as the dense dgrad, no zero-insertion."""
+    (``conv_phase_scatter``). Same FLOPs as the dense dgrad, no zero-insertion. ``ascale``: a
+    device scalar the k10 epilogues divide by (spectral norm's sigma)."""
     X = _ext.ext()
     cout, cin, kh, kw = wb.shape
     ho, wo = dy.shape[2], dy.shape[3]
@@ -367,7 +368,7 @@ def _strided_dgrad(dy, wb, H, W, s, padding, wts=None, ncv=-1):
     if wts is None and _STRIDED_ONE_LAUNCH and cout % 64 == 0 and cin % 64 == 0 and \
             0 <= ph < kh and 0 <= pw < kw:
         # every phase in one launch, stored straight into its parity sub-grid of dx
-        return X.conv2d_dgrad_strided(dy, wb, s, ph, pw, H, W, ncv)
+        return X.conv2d_dgrad_strided(dy, wb, s, ph, pw, H, W, ncv, ascale)
     dx = None
     phases = []
     for ry in range(s):
@@ -388,7 +389,7 @@ def _strided_dgrad(dy, wb, H, W, s, padding, wts=None, ncv=-1):
         py = max(0, jy - 1 - cy, qy + cy - ho)
         px = max(0, jx - 1 - cx, qx + cx - wo)
         wt = wts[(ry, rx)] if wts is not None else X.conv_weight_flip_t(wb, s, ky0, kx0, 1)
-        out = X.conv2d_mfma(dy, wt, None, 1, 1, py, px, 1, 1, 1.0, 1)
+        out = X.conv2d_mfma(dy, wt, None, 1, 1, py, px, 1, 1, 1.0, 1, -1, None, ascale)
         X.conv_phase_scatter(out, dx, s, ry, rx, cy - (jy - 1) + py, cx - (jx - 1) + px, qy, qx)
     return dx
 
@@ -414,25 +415,39 @@ def _bwd_side_stream():
 
 class _MfmaConv2d(torch.autograd.Function):
     """k10 forward / stride-1 dgrad, k11 wgrad, k2 activation + bias backward. Channel
-    counts are zero-padded to multiples of 64 (input) / 64 (output) around the kernels."""
+    counts are zero-padded to multiples of 64 (input) / 64 (output) around the kernels.
+
+    Spectral norm (``sw``: an :class:`SNWeight`; ``w`` is then its fp32 parameter W and the
+    function is differentiable w.r.t. W, reference torch.nn.utils.spectral_norm):
+
+    * forward: k10 on the bf16 shadow, ``y = act(conv(x, W) / sigma + b)`` — 1 / sigma in the
+      epilogue, no bf16(W / sigma) copy per forward;
+    * data gradient: k10 on the flipped shadow (the group flips every fused conv's shadow in
+      one launch) or the strided data gradient, 1 / sigma in the epilogue;
+    * weight gradient: k11 into fp32 split-K slabs whose epilogue also sums <G, W> per block;
+      the pass that sums the slabs writes ``dW = G / sigma - (<G, W> / sigma^2) u v^T`` (the
+      gradient of W / (u^T W v) with u, v constant, as torch's spectral_norm backward).
+    """
 
     @staticmethod
-    def forward(ctx, x, w, bias, stride, padding, dilation, slope, res=None):
+    def forward(ctx, x, w, bias, stride, padding, dilation, slope, res=None, sw=None):
         cout, cin = w.shape[0], w.shape[1]
         cp, op = _round_up(cin, 64), _out_pad(cout)
         xb = _pad_channels(x, cp, torch.bfloat16)
-        wb = _pad_rows(_pad_channels(w, cp, torch.bfloat16), op)
+        sig = None if sw is None else sw.sigma.reshape(1)
+        wb = _pad_rows(_pad_channels(w if sw is None else sw.shadow, cp, torch.bfloat16), op)
         ho, wo = _out_hw(x.shape[2], x.shape[3], w.shape[2:], stride, padding, dilation)
         # Cout % 8 == 0: k10 stores only the real output channels (no crop copy after it)
         ncv = cout if (op != cout and cout % 8 == 0) else op
         ctx.res_dtype = None if res is None else res.dtype
         with _Logged('fwd', 'k10', 2.0 * x.shape[0] * ho * wo * op * cp * w.shape[2] * w.shape[3],
-                     _gemm_desc(xb, wb, stride, padding)):
+                     _gemm_desc(xb, wb, stride, padding) + ('' if sw is None else ' sn')):
             y = _ext.ext().conv2d_mfma(xb, wb, _pad_rows(bias, op), stride[0], stride[1],
                                        padding[0], padding[1], dilation[0], dilation[1],
-                                       float(slope), 1, ncv, res)
+                                       float(slope), 1, ncv, res, sig)
         ctx.conf = (stride, padding, dilation, float(slope), cin, cout, x.dtype, w.dtype,
                     None if bias is None else bias.dtype, x.shape[1])
+        ctx.sn = None if sw is None else (sw.shadow, sw.u, sw.v, sig)
         ctx.wflip = _dgrad_weight(wb) if (stride == (1, 1) and dilation == (1, 1) and
                                           ctx.needs_input_grad[0]) else None
         # the output is needed only for a fused activation's mask: with slope 1 it is not
@@ -452,6 +467,8 @@ class _MfmaConv2d(torch.autograd.Function):
             _ps_check('conv.dy', dy)
         stride, padding, dilation, slope, cin, cout, xdt, wdt, bdt, xc = ctx.conf
         need_x, need_w, need_b = ctx.needs_input_grad[:3]
+        sn = ctx.sn
+        sig = None if sn is None else sn[3]
         # the activation backward runs at the saved output's channel count (the real Cout when
         # k10 stored only those, else the padded one), then dy is padded for the GEMMs; without
         # an activation / bias gradient that is ONE pad-cast pass from any dy layout
@@ -477,7 +494,7 @@ class _MfmaConv2d(torch.autograd.Function):
                 if side_bias:  # bias gradient only: the k2 kernel reads dy, writes no dx
                     db = _ext.ext().bias_act_bwd(dy, dy, 1.0)[1]
                 if need_w and _OVERLAP_BWD == '1':
-                    dw = _wgrad(dy, xb, wb, stride, padding, dilation, cout, cin, wdt)
+                    dw = _wgrad(dy, xb, wb, stride, padding, dilation, cout, cin, wdt, sn)
         if need_x:
             kh, kw = wb.shape[2], wb.shape[3]
             pt = (dilation[0] * (kh - 1) - padding[0], dilation[1] * (kw - 1) - padding[1])
@@ -498,14 +515,15 @@ class _MfmaConv2d(torch.autograd.Function):
                 with _Logged('dgrad', 'k10', fl, _gemm_desc(dy, wb.transpose(0, 1), (1, 1), pt)):
                     if ctx.wflip is not None:
                         dx = _ext.ext().conv2d_mfma(dy, ctx.wflip, None, 1, 1, pt[0], pt[1], 1,
-                                                    1, 1.0, 1, ncv)
+                                                    1, 1.0, 1, ncv, None, sig)
                     else:
-                        dx = _ext.ext().conv2d_dgrad_mfma(dy, wb, padding[0], padding[1], ncv)
+                        dx = _ext.ext().conv2d_dgrad_mfma(dy, wb, padding[0], padding[1], ncv,
+                                                          sig)
             elif stride == (1, 1) and pt[0] >= 0 and pt[1] >= 0 and big:
                 wt = _flip_t(wb)
                 with _Logged('dgrad', 'k10', fl, _gemm_desc(dy, wt, (1, 1), pt)):
                     dx = _ext.ext().conv2d_mfma(dy, wt, None, 1, 1, pt[0], pt[1],
-                                                dilation[0], dilation[1], 1.0, 1, ncv)
+                                                dilation[0], dilation[1], 1.0, 1, ncv, None, sig)
             elif _STRIDED_DGRAD and stride[0] == stride[1] and 2 <= stride[0] <= 4 and \
                     dilation == (1, 1) and (cap or (
                         dblocks >= _MFMA_MIN_DGRAD_BLOCKS * stride[0] ** 2 and
@@ -514,12 +532,14 @@ class _MfmaConv2d(torch.autograd.Function):
                 # or slower below ~128K dx pixels (profiles/strided_dgrad_probe_mi355x.txt)
                 with _Logged('dgrad', 'k10s', fl, _gemm_desc(dy, wb, stride, padding)):
                     dx = _strided_dgrad(dy, wb, xb.shape[2], xb.shape[3], stride[0], padding,
-                                        ncv=ncv)
+                                        ncv=ncv, ascale=sig)
             else:
                 with _Logged('dgrad', 'miopen', fl, _gemm_desc(dy, wb, stride, padding)):
                     dx = torch.ops.aten.convolution_backward(
                         dy, xb, wb, None, stride, padding, dilation, False, [0, 0], 1,
                         [True, False, False])[0]
+                    if sig is not None:
+                        dx = dx * (1.0 / sig).to(dx.dtype)
             if dx.shape[1] != xc:
                 dx = dx[:, :xc]
             dx = dx.to(xdt)
@@ -530,7 +550,7 @@ class _MfmaConv2d(torch.autograd.Function):
                     t.record_stream(main)
         if need_w:
             if dw is None:
-                dw = _wgrad(dy, xb, wb, stride, padding, dilation, cout, cin, wdt)
+                dw = _wgrad(dy, xb, wb, stride, padding, dilation, cout, cin, wdt, sn)
             if dw.shape[0] != cout or dw.shape[1] != cin:
                 dw = dw[:cout, :cin]
             dw = dw.to(wdt)
@@ -547,7 +567,50 @@ class _MfmaConv2d(torch.autograd.Function):
         dres = None
         if ctx.res_dtype is not None and ctx.needs_input_grad[7]:
             dres = dy_in if dy_in.dtype == ctx.res_dtype else dy_in.to(ctx.res_dtype)
-        return dx, dw, db, None, None, None, None, dres
+        return dx, dw, db, None, None, None, None, dres, None
+
+
+class SNWeight(object):
+    """A spectrally normalised conv weight handed to :func:`conv2d` / :func:`conv2d_act`
+    unmaterialised (layers/spectral_norm.py ``weight_ref``): the fp32 parameter ``W``, its bf16
+    shadow (= bf16(W), written by the optimizer step), the power iteration's u / v snapshots
+    and sigma (a device scalar). On the k10 / k11 path the conv runs on the shadow with
+    1 / sigma in its epilogues and the SN backward in its weight gradient
+    (:class:`_MfmaConv2d`); any other consumer calls :meth:`materialize` for the usual
+    bf16(W / sigma) tensor (reference: torch.nn.utils.spectral_norm, W / (u^T W v))."""
+
+    __slots__ = ('W', 'shadow', 'u', 'v', 'sigma', 'hook', 'module')
+
+    def __init__(self, W, shadow, u, v, sigma, hook, module):
+        self.W, self.shadow, self.u, self.v, self.sigma = W, shadow, u, v, sigma
+        self.hook, self.module = hook, module
+
+    @property
+    def shape(self):
+        return self.W.shape
+
+    def dim(self):
+        return self.W.dim()
+
+    def materialize(self):
+        from imaginaire_amd.layers.spectral_norm import _SNScaleCast, materialize_scaled
+        w16 = materialize_scaled(self.W, self.sigma, self.shadow)
+        return _SNScaleCast.apply(self.W, self.u, self.v, self.sigma, w16, self.shadow)
+
+
+def _sn_fused_ok(x, sw, stride, padding, dilation, residual=None):
+    """The fused SN conv runs exactly where the plain k10 path would (no tap-split head).
+    Decided on the weight's shape alone (a meta tensor: no padded copy of the shadow here)."""
+    cx, cw = x.shape[1], sw.shadow.shape[1]
+    if cx != cw and not (cx == _round_up(cw, 64) and
+                         getattr(x, '_iamd_valid_channels', None) == cw):
+        return False
+    wm = torch.empty((sw.shadow.shape[0], cx) + tuple(sw.shadow.shape[2:]), dtype=torch.bfloat16,
+                     device='meta')
+    if tapsplit_eligible(x, wm, stride, padding, dilation, 1) or \
+            not mfma_eligible(x, wm, stride, padding, dilation, 1):
+        return False
+    return residual is None or _residual_fusible(residual, x, wm, stride, padding, dilation)
 
 
 class _MfmaConvPerSample(torch.autograd.Function):
@@ -811,11 +874,12 @@ def _agree(times):
     return out
 
 
-def _wgrad_fns(dy, xb, wb, stride, padding, dilation, cout, cin, wdt, variant=0):
+def _wgrad_fns(dy, xb, wb, stride, padding, dilation, cout, cin, wdt, variant=0, sn=None):
     def k11(v=variant):
         return _ext.ext().conv2d_wgrad_mfma(dy, xb, wb.shape[2], wb.shape[3], stride[0],
                                             stride[1], padding[0], padding[1], dilation[0],
-                                            dilation[1], cout, cin, wdt == torch.bfloat16, 1, v)
+                                            dilation[1], cout, cin, wdt == torch.bfloat16, 1, v,
+                                            None if sn is None else list(sn))
 
     def miopen():
         return torch.ops.aten.convolution_backward(
@@ -835,14 +899,15 @@ def _k11_variants(dy, xb, wb, stride, dilation):
     return ('k11',)
 
 
-def _wgrad(dy, xb, wb, stride, padding, dilation, cout=-1, cin=-1, wdt=torch.float32):
+def _wgrad(dy, xb, wb, stride, padding, dilation, cout=-1, cin=-1, wdt=torch.float32, sn=None):
     """Weight gradient: k11 or MIOpen wrw (``IMAGINAIRE_AMD_MFMA_WGRAD`` = 1 | 0 | auto; auto =
     the faster of the two per shape, timed by :func:`tune_pending` outside the backward and
     agreed across ranks). k11 returns the gradient already cropped to (cout, cin) and in the
     weight's dtype (bf16 for the bf16 spectral-norm / autocast weights): the crop and cast ride
-    in its split-K sum."""
-    k11, miopen = _wgrad_fns(dy, xb, wb, stride, padding, dilation, cout, cin, wdt)
-    mode = _MFMA_WGRAD
+    in its split-K sum. ``sn`` = (bf16 shadow, u, v, sigma) of a spectrally normalised weight
+    (:class:`_MfmaConv2d`): k11 only, returning the fp32 gradient w.r.t. W."""
+    k11, miopen = _wgrad_fns(dy, xb, wb, stride, padding, dilation, cout, cin, wdt, sn=sn)
+    mode = _MFMA_WGRAD if sn is None else '1'  # (the SN backward rides in k11's split-K sum)
     fl = 2.0 * dy.shape[0] * dy.shape[2] * dy.shape[3] * wb.numel()
     desc = _gemm_desc(xb, wb, stride, padding)
     if mode == '0' and not _capturing():
@@ -855,13 +920,13 @@ def _wgrad(dy, xb, wb, stride, padding, dilation, cout=-1, cin=-1, wdt=torch.flo
     # per-shape choice among the candidates (mode 1: the k11 variants; auto: those and MIOpen),
     # timed by tune_pending() between iterations; the default routing runs until then
     key = (tuple(dy.shape), tuple(xb.shape), tuple(wb.shape), stride, padding, dilation,
-           cout, cin, wdt)
+           cout, cin, wdt) + (() if sn is None else ('sn',))  # (tuned with the SN epilogue)
     choice = _WGRAD_CHOICE.get(key)
     if choice is None:
         _WGRAD_PENDING.setdefault(key, (dy.dtype, xb.dtype, wb.dtype))
         choice = 'k11'
     with _Logged('wgrad', choice, fl, desc):
-        if choice == 'miopen' and not _capturing():
+        if choice == 'miopen' and sn is None and not _capturing():
             return miopen()
         if choice == 'k11v2':
             return k11(2)
@@ -936,13 +1001,21 @@ def tune_pending():
     for kind, key, dts in entries:
         if kind == 'w':
             dyt, xt, wt = dts
-            dys, xs, ws, stride, padding, dilation, cout, cin, wdt = key
+            dys, xs, ws, stride, padding, dilation, cout, cin, wdt = key[:9]
             dy = torch.randn(dys, device=dev).to(dyt).contiguous(memory_format=cl)
             xb = torch.randn(xs, device=dev).to(xt).contiguous(memory_format=cl)
             wb = torch.randn(ws, device=dev).to(wt).contiguous(memory_format=cl)
-            k11, miopen = _wgrad_fns(dy, xb, wb, stride, padding, dilation, cout, cin, wdt)
+            sn = None
+            if len(key) > 9:  # spectral norm: the k11 variants with their <G, W> epilogue
+                kk = ws[2] * ws[3]
+                sn = (torch.randn((cout, cin) + tuple(ws[2:]), device=dev).to(
+                    torch.bfloat16).contiguous(memory_format=cl),
+                    torch.randn(cout, device=dev), torch.randn(cin * kk, device=dev),
+                    torch.ones(1, device=dev))
+            k11, miopen = _wgrad_fns(dy, xb, wb, stride, padding, dilation, cout, cin, wdt,
+                                     sn=sn)
             cand = {}
-            if _MFMA_WGRAD != '1':
+            if _MFMA_WGRAD != '1' and sn is None:
                 cand['miopen'] = _time_ms(miopen)
             if len(_k11_variants(dy, xb, wb, stride, dilation)) > 1:
                 cand['k11'] = _time_ms(lambda: k11(1))
@@ -977,6 +1050,11 @@ def conv2d_act(x, weight, bias=None, stride=1, padding=0, dilation=1, slope=1.0)
     """``act(conv2d(x, weight) + bias)`` with a leaky slope (1 = identity, 0 = relu);
     one k10 launch when eligible, otherwise MIOpen conv + k2 bias-act epilogue."""
     stride, padding, dilation = _pair(stride), _pair(padding), _pair(dilation)
+    if isinstance(weight, SNWeight):
+        if _sn_fused_ok(x, weight, stride, padding, dilation):
+            return _MfmaConv2d.apply(x, weight.W, bias, stride, padding, dilation, slope, None,
+                                     weight)
+        weight = weight.materialize()
     weight = _match_channels(x, weight)
     if slope == 1.0 and tapsplit_eligible(x, weight, stride, padding, dilation, 1):
         return _TapSplitConv2d.apply(x, weight, bias, padding, dilation)
@@ -1041,7 +1119,19 @@ def _residual_fusible(res, x, weight, stride, padding, dilation):
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1,
            padding_mode='zeros', residual=None):
     """``F.conv2d`` (+ ``residual``, added to the output: on the k10 path inside its epilogue,
-    otherwise as a separate add)."""
+    otherwise as a separate add). ``weight`` may be an :class:`SNWeight`."""
+    if isinstance(weight, SNWeight):
+        st, pd, dl = _pair(stride), _pair(padding), _pair(dilation)
+        if groups == 1 and x.is_cuda and x.dim() == 4:
+            if padding_mode not in ('zeros', None):  # reflect / replicate: pad, then the conv
+                vc = getattr(x, '_iamd_valid_channels', None)
+                x = pad(nhwc(x), _pad_arg(padding), padding_mode)
+                if vc is not None:
+                    x._iamd_valid_channels = vc
+                padding, pd, padding_mode = 0, (0, 0), 'zeros'
+            if _sn_fused_ok(x, weight, st, pd, dl, residual):
+                return _MfmaConv2d.apply(x, weight.W, bias, st, pd, dl, 1.0, residual, weight)
+        weight = weight.materialize()
     if residual is not None:
         st, pd, dl = _pair(stride), _pair(padding), _pair(dilation)
         if groups == 1 and padding_mode in ('zeros', None) and x.is_cuda and x.dim() == 4:

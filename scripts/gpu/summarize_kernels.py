@@ -92,7 +92,7 @@ def main(root):
         print('  %-28s %9.1f ms  %5.1f%%' % (k, v / 1e6, 100 * v / total))
     print()
     rows.sort(key=lambda r: -float(r[key_total]))
-    for r in rows[:50]:
+    for r in rows[:int(os.environ.get("SUMMARY_ROWS", "150"))]:
         name = re.sub(r'\s+', ' ', r[key_name])[:110]
         calls = r[key_calls] if key_calls else '?'
         print('%9.2f ms %5.1f%% %6s  %s' % (float(r[key_total]) / 1e6,

@@ -35,6 +35,12 @@ def _fresh(x):
     return x
 
 
+def _grads(net):
+    """Every parameter's gradient as a CPU fp32 copy (unit-test configs: a few MB)."""
+    return {name: p.grad.detach().float().cpu().clone() for name, p in net.named_parameters()
+            if p.grad is not None}
+
+
 def _grad_norms(net, exclude=()):
     sq = 0.0
     n = 0
@@ -45,7 +51,7 @@ def _grad_norms(net, exclude=()):
     return math.sqrt(sq), n
 
 
-def _iteration(config, amp, eager, tmp, seq_len=None, overrides=(), grad_exclude=()):
+def _iteration(config, amp, eager, tmp, seq_len=None, overrides=(), grad_exclude=(), cudnn=None):
     from torch.utils.data import default_collate
     from imaginaire_amd.config import Config
     from imaginaire_amd.datasets.synthetic import Dataset
@@ -56,7 +62,9 @@ def _iteration(config, amp, eager, tmp, seq_len=None, overrides=(), grad_exclude
     # of MIOpen's fp32 backward solvers faulted (illegal memory access) on the pix2pixHD
     # reference iteration of one box (gpurun_out r4t, round 4)
     old_cudnn = torch.backends.cudnn.enabled
-    torch.backends.cudnn.enabled = not eager
+    # (``cudnn``: force MIOpen on / off — a second bf16 PyTorch run with other conv algorithms,
+    # i.e. other roundings, measures how far bf16 alone moves each gradient)
+    torch.backends.cudnn.enabled = (not eager) if cudnn is None else cudnn
     try:
         cfg = Config(os.path.join(ROOT, 'configs', 'unit_test', config))
         cfg.logdir = str(tmp)
@@ -98,12 +106,15 @@ def _iteration(config, amp, eager, tmp, seq_len=None, overrides=(), grad_exclude
         torch.manual_seed(2)
         tr.dis_update(data)
         d_norm = _grad_norms(tr.net_D)
+        d_grads = _grads(tr.net_D)
         torch.manual_seed(3)
         tr.gen_update(data)
         g_norm = _grad_norms(tr.net_G, grad_exclude)
+        g_grads = _grads(tr.net_G)
         torch.cuda.synchronize()
         dl = {k: float(v) for k, v in tr.dis_losses.items() if torch.is_tensor(v)}
         gl = {k: float(v) for k, v in tr.gen_losses.items() if torch.is_tensor(v)}
+        _LAST_GRADS[0] = (d_grads, g_grads)
         return dl, gl, d_norm, g_norm
     finally:
         torch.backends.cudnn.enabled = old_cudnn
@@ -113,15 +124,45 @@ def _iteration(config, amp, eager, tmp, seq_len=None, overrides=(), grad_exclude
             os.environ['IMAGINAIRE_AMD_EAGER'] = old
 
 
+_LAST_GRADS = [None]
+
+
+def _cosine_report(hip, ref, floor_frac, loose=(), loose_min=None):
+    """Per-parameter-tensor cosine similarity of the HIP-bf16 gradients against the fp32
+    reference for every tensor whose reference norm is at least ``floor_frac`` of the largest
+    one. Returns [(cos, name, |ref|)] sorted worst first, and the tensors under the floor."""
+    norms = {n: float(g.norm()) for n, g in ref.items()}
+    top = max(norms.values()) if norms else 0.0
+    rows, skipped = [], 0
+    for n, g in ref.items():
+        if norms[n] < floor_frac * top or n not in hip:
+            skipped += 1
+            continue
+        a = hip[n].reshape(-1)
+        b = g.reshape(-1)
+        cos = float(torch.dot(a, b) / (a.norm() * b.norm()).clamp_min(1e-30))
+        rows.append((cos, n, norms[n]))
+    rows.sort()
+    return rows, skipped
+
+
 def _close(a, b, rtol, atol):
     # losses are O(1); a near-zero term (the hinge G loss -mean(D(fake)) of an untrained D)
     # is compared on the absolute scale
     return abs(a - b) <= atol + rtol * abs(b)
 
 
-def _compare(tmp_path, config, rtol=0.05, atol=1e-2, **kw):
+def _compare(tmp_path, config, rtol=0.05, atol=1e-2, floor_frac=1e-3, **kw):
     hip = _iteration(config, 'O1', False, tmp_path / 'hip', **kw)
+    hip_grads = _LAST_GRADS[0]
     ref = _iteration(config, 'O0', True, tmp_path / 'ref', **kw)
+    ref_grads = _LAST_GRADS[0]
+    # PyTorch's own ops under the same bf16 autocast, twice (im2col + rocBLAS convolutions, and
+    # MIOpen's): how far bf16 rounding alone moves each gradient
+    _iteration(config, 'O1', True, tmp_path / 'eager16', **kw)
+    e16_grads = _LAST_GRADS[0]
+    _iteration(config, 'O1', True, tmp_path / 'eager16b', cudnn=True, **kw)
+    e16b_grads = _LAST_GRADS[0]
     (dl, gl, dn, gn), (rdl, rgl, rdn, rgn) = hip, ref
     report = ['%s: hip %s | fp32 eager %s' % (config, hip, ref)]
     print('\n'.join(report))
@@ -136,7 +177,34 @@ def _compare(tmp_path, config, rtol=0.05, atol=1e-2, **kw):
     for name, a, b in (('|grad D|', dn[0], rdn[0]), ('|grad G|', gn[0], rgn[0])):
         if not _close(a, b, 2 * rtol, 1e-6):
             bad.append('%s hip %.5g vs fp32 %.5g' % (name, a, b))
-    assert not bad, '; '.join(bad)
+    # per-parameter-tensor direction, EVERY tensor above the norm floor (no
+    # exclusions): the HIP path's gradient may deviate from fp32 no more than PyTorch's own ops
+    # under the same bf16 autocast do, (1 - cos_hip) <= 3 (1 - cos_torch_bf16) + 0.02, where
+    # cos_torch_bf16 is the worst of the two PyTorch bf16 runs against fp32 and against each
+    # other (their spread is the measured bf16 sensitivity of that tensor). On these unit
+    # configs bf16 alone turns some gradients far (PyTorch bf16 vs fp32: SPADE head convs cos
+    # 0.89, MUNIT content encoder 0.59, vid2vid encoder -0.06 — the random FlowNet2 flow target
+    # and 4x8-pixel instance norms amplify rounding; scripts/probe/parity_cos_probe.py; the
+    # unscaled few-shot attention's key / query towers, profiles/fs_attention_bf16_probe), so an
+    # absolute bound would only measure the model's conditioning; a kernel defect (a reversed
+    # or wrong gradient) lands far outside the bf16 envelope where that envelope is tight.
+    for tag, i in (('D', 0), ('G', 1)):
+        rows, skipped = _cosine_report(hip_grads[i], ref_grads[i], floor_frac)
+        e16 = {n: c for c, n, _ in _cosine_report(e16_grads[i], ref_grads[i], floor_frac)[0]}
+        for extra in (_cosine_report(e16b_grads[i], ref_grads[i], floor_frac)[0],
+                      _cosine_report(e16b_grads[i], e16_grads[i], floor_frac)[0]):
+            for c, n, _ in extra:
+                e16[n] = min(e16.get(n, 1.0), c)
+        print('%s %s grads: %d tensors compared (%d under the floor); worst cos %s' % (
+            config, tag, len(rows), skipped,
+            ['%.4f (torch-bf16 %.4f) %s' % (c, e16.get(n, float('nan')), n)
+             for c, n, _ in rows[:4]]))
+        for c, n, nm in rows:
+            ce = e16.get(n, 1.0)
+            if not (1 - c) <= 3 * (1 - ce) + 0.02:
+                bad.append('%s grad %s cos %.4f vs torch-bf16 %.4f (|ref| %.3g)' % (
+                    tag, n, c, ce, nm))
+    assert not bad, '; '.join(bad[:20])
 
 
 def test_spade_iteration_hip_bf16_matches_eager_fp32(tmp_path):
@@ -173,6 +241,7 @@ def test_fs_vid2vid_iteration_hip_bf16_matches_eager_fp32(tmp_path, k):
     # softmax + bmm under autocast) exactly as much as on the fused path
     # (scripts/probe/fs_attn_probe.py, profiles/fs_attention_bf16_probe_mi355x.txt). The losses
     # and the rest of the generator are still compared; K = 1 covers the weight generator.
+    # (round 5: the per-tensor direction check below covers the weight generator too)
     _compare(tmp_path, 'fs_vid2vid_face.yaml', seq_len=2,
              overrides=[('data.initial_few_shot_K', k)],
              grad_exclude=('weight_generator.',) if k > 1 else ())
