@@ -237,32 +237,35 @@ __device__ __forceinline__ int pad_list(int i, int p0, int p1, int n, int mode,
   return cnt;
 }
 
-// grid (ceil(Wo*C/8 / kT), B*Ho): one block row per output image row, 32-bit in-row indices
+// grid (ceil(Wo*C/V / kT), B*Ho): one block row per output image row, 32-bit in-row indices
 // (the flat int64 index with three 64-bit div/mods per 16-byte copy made these kernels
-// ALU-bound at ~1/10 of HBM bandwidth)
-template <typename T>
+// ALU-bound at ~1/10 of HBM bandwidth). V channels per thread: 8 (16-byte copies) when
+// C % 8 == 0, else the widest of 4 / 2 / 1 dividing C (RGB inputs, 1-channel masks).
+template <typename T, int V>
 __global__ void __launch_bounds__(kT)
 pad_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int B, int C, int H, int W, int Ho,
                int Wo, int pt, int pl, int mode) {
-  const int cv = C / 8;
+  const int cv = C / V;
   const int e = blockIdx.x * kT + threadIdx.x;
   if (e >= Wo * cv) return;
   const int ox = e / cv, c8 = e - ox * cv;
   const int sx = pad_src(ox, pl, W, mode);
   for (int row = blockIdx.y; row < B * Ho; row += gridDim.y) {  // row = b * Ho + oy
     const int b = row / Ho, oy = row - b * Ho;
-    const int64_t src = (((int64_t)b * H + pad_src(oy, pt, H, mode)) * W + sx) * C + c8 * 8;
-    *reinterpret_cast<Pack<T, 8>*>(y + ((int64_t)row * Wo + ox) * C + c8 * 8) =
-        *reinterpret_cast<const Pack<T, 8>*>(x + src);
+    const int64_t src = (((int64_t)b * H + pad_src(oy, pt, H, mode)) * W + sx) * C + c8 * V;
+    *reinterpret_cast<Pack<T, V>*>(y + ((int64_t)row * Wo + ox) * C + c8 * V) =
+        *reinterpret_cast<const Pack<T, V>*>(x + src);
   }
 }
 
-template <typename T>
+template <typename T, int V>
 __global__ void __launch_bounds__(kT)
 pad_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int B, int C, int H, int W, int Ho,
                int Wo, int pt, int pb, int pl, int pr, int mode) {
-  // grid (ceil(W*C/8 / kT), B*H): one block row per input image row (see pad_fwd_kernel)
-  const int cv = C / 8;
+  // grid (ceil(W*C/V / kT), B*H): one block row per input image row (see pad_fwd_kernel); a
+  // gather over the (at most kPadMax^2) padded positions that copy this input pixel — no
+  // atomics (PyTorch's reflection_pad2d backward scatters with atomics)
+  const int cv = C / V;
   const int e = blockIdx.x * kT + threadIdx.x;
   if (e >= W * cv) return;
   const int ix = e / cv, c8 = e - ix * cv;
@@ -273,18 +276,18 @@ pad_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int B, int C, int H
     const int64_t t = (int64_t)row * W * cv + e;
     int ys[kPadMax];
     const int ny = pad_list(iy, pt, pb, H, mode, ys);
-    float acc[8];
+    float acc[V];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-    const T* base = dy + (int64_t)b * Ho * Wo * C + c8 * 8;
+    for (int k = 0; k < V; ++k) acc[k] = 0.f;
+    const T* base = dy + (int64_t)b * Ho * Wo * C + c8 * V;
     for (int u = 0; u < ny; ++u)
       for (int v = 0; v < nx; ++v) {
-        float g[8];
-        load_vec<T, 8>(base + ((int64_t)ys[u] * Wo + xs[v]) * C, g);
+        float g[V];
+        load_vec<T, V>(base + ((int64_t)ys[u] * Wo + xs[v]) * C, g);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] += g[k];
+        for (int k = 0; k < V; ++k) acc[k] += g[k];
       }
-    store_vec<T, 8>(dx + t * 8, acc);
+    store_vec<T, V>(dx + t * V, acc);
   }
 }
 
@@ -407,28 +410,45 @@ void nhwc_concat_into(at::Tensor& out, const at::Tensor& a, const at::Tensor& b)
   IAMD_LAUNCH_CHECK();
 }
 
+namespace {
+int pad_vec(int C) { return C % 8 == 0 ? 8 : C % 4 == 0 ? 4 : C % 2 == 0 ? 2 : 1; }
+
+template <typename F>
+void by_pad_vec(at::ScalarType st, int V, F&& f) {
+  auto by_v = [&](auto tv) {
+    switch (V) {
+      case 8: f(tv, std::integral_constant<int, 8>()); break;
+      case 4: f(tv, std::integral_constant<int, 4>()); break;
+      case 2: f(tv, std::integral_constant<int, 2>()); break;
+      default: f(tv, std::integral_constant<int, 1>()); break;
+    }
+  };
+  if (st == at::kBFloat16) by_v(__hip_bfloat16());
+  else by_v(float());
+}
+}  // namespace
+
 at::Tensor pad_nhwc_fwd(const at::Tensor& x, int64_t pl, int64_t pr, int64_t pt, int64_t pb,
                         int64_t mode) {
   IAMD_CHECK(x.is_cuda() && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
-                 x.size(1) % 8 == 0 &&
                  (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat),
-             "pad_nhwc_fwd: packed channels-last bf16/fp32 tensor with C % 8 == 0 expected");
+             "pad_nhwc_fwd: packed channels-last bf16/fp32 tensor expected");
   const int B = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
   IAMD_CHECK(pl >= 0 && pr >= 0 && pt >= 0 && pb >= 0 && (mode == 1 ||
              (pl < W && pr < W && pt < H && pb < H)), "pad_nhwc_fwd: bad padding");
   const int Ho = (int)(H + pt + pb), Wo = (int)(W + pl + pr);
   auto y = at::empty({B, C, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  const int64_t n = (int64_t)B * Ho * Wo * (C / 8);
-  if (n == 0) return y;
-  if (x.scalar_type() == at::kBFloat16)
-    hipLaunchKernelGGL(pad_fwd_kernel<__hip_bfloat16>, pad_rows_grid(Wo * (C / 8), B * Ho), dim3(kT), 0, stream(),
-                       reinterpret_cast<const __hip_bfloat16*>(x.data_ptr()),
-                       reinterpret_cast<__hip_bfloat16*>(y.data_ptr()), B, C, H, W, Ho, Wo,
-                       (int)pt, (int)pl, (int)mode);
-  else
-    hipLaunchKernelGGL(pad_fwd_kernel<float>, pad_rows_grid(Wo * (C / 8), B * Ho), dim3(kT), 0, stream(),
-                       x.data_ptr<float>(), y.data_ptr<float>(), B, C, H, W, Ho, Wo, (int)pt,
-                       (int)pl, (int)mode);
+  if ((int64_t)B * Ho * Wo * C == 0) return y;
+  const int V = pad_vec(C);
+  auto launch = [&](auto tv, auto vv) {
+    using T = decltype(tv);
+    constexpr int VV = decltype(vv)::value;
+    hipLaunchKernelGGL((pad_fwd_kernel<T, VV>), pad_rows_grid(Wo * (C / VV), B * Ho), dim3(kT), 0,
+                       stream(), reinterpret_cast<const T*>(x.data_ptr()),
+                       reinterpret_cast<T*>(y.data_ptr()), B, C, H, W, Ho, Wo, (int)pt, (int)pl,
+                       (int)mode);
+  };
+  by_pad_vec(x.scalar_type(), V, launch);
   IAMD_LAUNCH_CHECK();
   return y;
 }
@@ -436,25 +456,25 @@ at::Tensor pad_nhwc_fwd(const at::Tensor& x, int64_t pl, int64_t pr, int64_t pt,
 at::Tensor pad_nhwc_bwd(const at::Tensor& dy, int64_t H, int64_t W, int64_t pl, int64_t pr,
                         int64_t pt, int64_t pb, int64_t mode) {
   IAMD_CHECK(dy.is_cuda() && dy.dim() == 4 && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
-                 dy.size(1) % 8 == 0 && dy.size(2) == H + pt + pb && dy.size(3) == W + pl + pr,
+                 (dy.scalar_type() == at::kBFloat16 || dy.scalar_type() == at::kFloat) &&
+                 dy.size(2) == H + pt + pb && dy.size(3) == W + pl + pr,
              "pad_nhwc_bwd: gradient shape / layout");
   IAMD_CHECK(mode == 0 || (pt + 1 <= kPadMax && pb + 1 <= kPadMax && pl + 1 <= kPadMax &&
                            pr + 1 <= kPadMax), "pad_nhwc_bwd: replicate padding above 15");
   const int B = (int)dy.size(0), C = (int)dy.size(1);
   auto dx = at::empty({B, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
-  const int64_t n = (int64_t)B * H * W * (C / 8);
-  if (n == 0) return dx;
-  if (dy.scalar_type() == at::kBFloat16)
-    hipLaunchKernelGGL(pad_bwd_kernel<__hip_bfloat16>, pad_rows_grid(W * (C / 8), B * H), dim3(kT), 0, stream(),
-                       reinterpret_cast<const __hip_bfloat16*>(dy.data_ptr()),
-                       reinterpret_cast<__hip_bfloat16*>(dx.data_ptr()), B, C, (int)H, (int)W,
+  if ((int64_t)B * H * W * C == 0) return dx;
+  const int V = pad_vec(C);
+  auto launch = [&](auto tv, auto vv) {
+    using T = decltype(tv);
+    constexpr int VV = decltype(vv)::value;
+    hipLaunchKernelGGL((pad_bwd_kernel<T, VV>), pad_rows_grid((int)W * (C / VV), B * (int)H),
+                       dim3(kT), 0, stream(), reinterpret_cast<const T*>(dy.data_ptr()),
+                       reinterpret_cast<T*>(dx.data_ptr()), B, C, (int)H, (int)W,
                        (int)dy.size(2), (int)dy.size(3), (int)pt, (int)pb, (int)pl, (int)pr,
                        (int)mode);
-  else
-    hipLaunchKernelGGL(pad_bwd_kernel<float>, pad_rows_grid(W * (C / 8), B * H), dim3(kT), 0, stream(),
-                       dy.data_ptr<float>(), dx.data_ptr<float>(), B, C, (int)H, (int)W,
-                       (int)dy.size(2), (int)dy.size(3), (int)pt, (int)pb, (int)pl, (int)pr,
-                       (int)mode);
+  };
+  by_pad_vec(dy.scalar_type(), V, launch);
   IAMD_LAUNCH_CHECK();
   return dx;
 }

@@ -5,7 +5,7 @@ import torch
 from torch import nn
 
 from imaginaire_amd.layers import Conv2dBlock, Res2dBlock
-from imaginaire_amd.ops.pool import AvgPool2d
+from imaginaire_amd.ops.pool import AvgPool2d, ReflectionPad2d
 from imaginaire_amd.discriminators.munit import _kw
 
 
@@ -49,7 +49,7 @@ class ResDiscriminator(nn.Module):
             model += [Res2dBlock(num_filters_prev, num_filters_prev, **conv_params),
                       Res2dBlock(num_filters_prev, num_filters, **conv_params)]
             if i != num_layers - 1:
-                model += [nn.ReflectionPad2d(1), AvgPool2d(3, stride=2)]
+                model += [ReflectionPad2d(1), AvgPool2d(3, stride=2)]
         self.model = nn.Sequential(*model)
         self.classifier = Conv2dBlock(num_filters, 1, 1, 1, 0, nonlinearity='leakyrelu',
                                       weight_norm_type=weight_norm_type, order='NACNAC')

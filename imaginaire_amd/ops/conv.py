@@ -1087,9 +1087,10 @@ _PAD_MODES = {'reflect': 0, 'replicate': 1}
 
 def pad(x, pad_lrtb, mode):
     """``F.pad(x, pad_lrtb, mode)`` for 4-D inputs; reflect / replicate padding of packed NHWC
-    activations (channels % 8 == 0) runs the HIP gather kernels (forward and backward)."""
+    activations (any channel count: 16-byte copies when it is a multiple of 8) runs the HIP
+    gather kernels (forward and backward)."""
     m = _PAD_MODES.get(mode)
-    if m is not None and x.dim() == 4 and x.shape[1] % 8 == 0 and \
+    if m is not None and x.dim() == 4 and \
             x.dtype in (torch.bfloat16, torch.float32) and _ext.use_native(x) and \
             x.is_contiguous(memory_format=_CL) and len(pad_lrtb) == 4 and min(pad_lrtb) >= 0 and \
             (m == 1 or (max(pad_lrtb[0], pad_lrtb[1]) < x.shape[3] and

@@ -72,3 +72,23 @@ class AvgPool2d(nn.Module):
     def extra_repr(self):
         return 'kernel_size={}, stride={}, padding={}'.format(self.kernel_size, self.stride,
                                                               self.padding)
+
+
+class ReflectionPad2d(nn.Module):
+    """Drop-in for ``nn.ReflectionPad2d`` running the NHWC gather kernels forward and backward
+    (ops/conv.py ``pad``; PyTorch's reflection-pad backward scatters with atomics, and its
+    output drops the channels-last layout the following pooling kernel needs)."""
+
+    def __init__(self, padding):
+        super().__init__()
+        self.padding = (padding,) * 4 if isinstance(padding, int) else tuple(padding)
+
+    def forward(self, x):
+        from imaginaire_amd.ops.conv import nhwc, pad
+        if x.is_cuda and x.dim() == 4:
+            x = nhwc(x)
+        return pad(x, self.padding, 'reflect')
+
+    def extra_repr(self):
+        return str(self.padding)
+

@@ -851,13 +851,16 @@ def test_cat0_view_of_adjacent_weights():
 @pytest.mark.parametrize('mode', ['reflect', 'replicate'])
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('pad', [(3, 3, 3, 3), (1, 2, 0, 3), (1, 1, 1, 1)])
-def test_pad_nhwc(mode, dtype, pad):
-    """NHWC reflect / replicate padding (gather forward and backward) vs F.pad in fp32."""
+@pytest.mark.parametrize('channels', [16, 3, 1, 6, 12])
+def test_pad_nhwc(mode, dtype, pad, channels):
+    """NHWC reflect / replicate padding (gather forward and backward) vs F.pad in fp32, for
+    16-byte (C % 8 == 0) and narrower (RGB, masks) channel vectors."""
     from imaginaire_amd.ops.conv import pad as pad_nhwc
     torch.manual_seed(15)
-    x = torch.randn(2, 16, 9, 11, device='cuda').to(dtype).contiguous(
+    x = torch.randn(2, channels, 9, 11, device='cuda').to(dtype).contiguous(
         memory_format=torch.channels_last).requires_grad_(True)
     y = pad_nhwc(x, pad, mode)
+    assert y.grad_fn is not None and 'PadNHWC' in type(y.grad_fn).__name__
     xr = x.detach().float().requires_grad_(True)
     yr = F.pad(xr, pad, mode=mode)
     assert y.shape == yr.shape and torch.equal(y.float(), yr)
@@ -1946,12 +1949,19 @@ def test_non_local_block_k16_matches_fp32(c, h, w):
     ref = run(False, True)
     assert len(calls) == n_calls  # (fp32: SDPA)
 
+    floor = [1e-30]
+
     def rel(a, b):
-        return float((a.float() - b).norm() / b.norm().clamp_min(1e-30))
-    # (y = gamma * attn + x: the attention branch is compared, not the identity)
-    for name, a, t, r in (('out', k16[0], tbf[0], ref[0]), ('dx', k16[1], tbf[1], ref[1])) + \
-            tuple(('param%d' % i, a, t, r) for i, (a, t, r) in enumerate(zip(k16[2], tbf[2],
-                                                                          ref[2]))):
-        if float(r.norm()) == 0:
-            continue
+        return float((a.float() - b).norm() / b.norm().clamp_min(floor[0]))
+    # (y = gamma * attn + x: the attention branch is compared, not the identity). The output
+    # and input gradient within 1.5x PyTorch's bf16 error; the weight / bias gradients within 3x
+    # + 3e-2: k16's dQ / dK are ~2x noisier than SDPA's (its dS operand of the dQ / dK GEMMs is
+    # bf16; scripts/probe/attn_dq_bias_probe.py: dq rel 4.8e-3 vs 2.3e-3), and the theta bias
+    # gradient sums dq over every query, where most of it cancels. (The phi (key) bias gradient
+    # is zero analytically — softmax ignores a shift shared by all keys — so every gradient is
+    # measured against at least 1% of the largest parameter gradient.)
+    for name, a, t, r in (('out', k16[0], tbf[0], ref[0]), ('dx', k16[1], tbf[1], ref[1])):
         assert rel(a, r) <= 1.5 * rel(t, r) + 1e-2, (name, rel(a, r), rel(t, r))
+    floor[0] = 1e-2 * max(float(r.norm()) for r in ref[2])
+    for i, (a, t, r) in enumerate(zip(k16[2], tbf[2], ref[2])):
+        assert rel(a, r) <= 3.0 * rel(t, r) + 3e-2, ('param%d' % i, rel(a, r), rel(t, r))
