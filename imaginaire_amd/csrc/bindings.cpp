@@ -145,6 +145,7 @@ at::Tensor pad_nhwc_fwd(const at::Tensor& x, int64_t pl, int64_t pr, int64_t pt,
                         int64_t mode);
 at::Tensor pad_nhwc_bwd(const at::Tensor& dy, int64_t H, int64_t W, int64_t pl, int64_t pr,
                         int64_t pt, int64_t pb, int64_t mode);
+at::Tensor sn_dot_partials(const at::Tensor& dx, const at::Tensor& x, const at::Tensor& sigma);
 at::Tensor wgrad_finalize(const at::Tensor& part, int64_t S, int64_t Cop, int64_t Cip,
                           int64_t Cout, int64_t Cin, int64_t KH, int64_t KW,
                           at::ScalarType dtype);
@@ -196,6 +197,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "stride-1 conv data gradient from the forward weight (k10 v4 transposed-weight path)",
         py::arg("dy"), py::arg("w"), py::arg("ph"), py::arg("pw"), py::arg("ncv") = -1,
         py::arg("ascale") = py::none());
+  m.def("sn_dot_partials", &iamd::sn_dot_partials,
+        "sigma * <dx, x> as partial sums: <G, W> of a spectrally normalised conv (k11 SN)",
+        py::arg("dx"), py::arg("x"), py::arg("sigma"));
   m.def("conv2d_wgrad_mfma", &iamd::conv2d_wgrad_mfma, "MFMA conv weight gradient (k11)",
         py::arg("dy"), py::arg("x"), py::arg("KH"), py::arg("KW"), py::arg("sh"), py::arg("sw"),
         py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("out_cout") = -1,

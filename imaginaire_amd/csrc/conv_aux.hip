@@ -813,6 +813,66 @@ at::Tensor wgrad_finalize_sn(const at::Tensor& part, int64_t S, int64_t Cop, int
   return out;
 }
 
+namespace {
+// scale * sum over pixels p and channels c < C of a[p * Ca + c] * b[p * Cb + c] (bf16, packed
+// channels-last, C % 8 == 0): one fp32 partial per block, fixed grid and order (deterministic)
+constexpr int kDotBlocks = 512;
+__global__ void __launch_bounds__(kT)
+sn_dot_kernel(const __hip_bfloat16* __restrict__ a, const __hip_bfloat16* __restrict__ b,
+              int64_t P, int Ca, int Cb, int C, const float* __restrict__ scale,
+              float* __restrict__ part) {
+  const int cv = C / 8;
+  const int64_t n = P * cv;
+  float acc = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
+    const int64_t p = i / cv;
+    const int c = (int)(i - p * cv) * 8;
+    float x[8], y[8];
+    load_vec<__hip_bfloat16, 8>(a + p * Ca + c, x);
+    load_vec<__hip_bfloat16, 8>(b + p * Cb + c, y);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc = fmaf(x[k], y[k], acc);
+  }
+  __shared__ float red[kT / 64];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < kT / 64; ++k) t += red[k];
+    part[blockIdx.x] = t * (scale ? scale[0] : 1.f);
+  }
+}
+}  // namespace
+
+// <G, W> of a spectrally normalised conv from its data gradient: for y = conv(x, W) / sigma,
+// <G, W> = sum_m dy_m . conv(x, W)_m = <conv^T(dy, W), x> = sigma * <dx, x> (the adjoint
+// identity; any stride / padding / dilation). dx [B, Ca, H, W] is the k10 data gradient
+// (1 / sigma applied), x [B, Cb, H, W] the conv's bf16 input; channels >= min(Ca, Cb) are zero
+// in whichever operand has them. Returns kDotBlocks partials whose sum is <G, W> — the dotp of
+// wgrad_finalize_sn, replacing the k11 epilogue's per-block W reads where the activation is
+// smaller than the weight (deep, low-resolution layers).
+at::Tensor sn_dot_partials(const at::Tensor& dx, const at::Tensor& x, const at::Tensor& sigma) {
+  IAMD_CHECK(dx.is_cuda() && x.is_cuda() && dx.scalar_type() == at::kBFloat16 &&
+                 x.scalar_type() == at::kBFloat16 && dx.dim() == 4 && x.dim() == 4 &&
+                 dx.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                 x.is_contiguous(at::MemoryFormat::ChannelsLast) && dx.size(0) == x.size(0) &&
+                 dx.size(2) == x.size(2) && dx.size(3) == x.size(3),
+             "sn_dot_partials: packed channels-last bf16 [B, C, H, W] operands of one shape");
+  IAMD_CHECK(sigma.scalar_type() == at::kFloat && sigma.numel() == 1, "sn_dot_partials: sigma");
+  const int Ca = (int)dx.size(1), Cb = (int)x.size(1), C = std::min(Ca, Cb);
+  IAMD_CHECK(C % 8 == 0 && Ca % 8 == 0 && Cb % 8 == 0, "sn_dot_partials: channels % 8");
+  auto part = at::empty({kDotBlocks}, x.options().dtype(at::kFloat));
+  const int64_t P = x.size(0) * x.size(2) * x.size(3);
+  hipLaunchKernelGGL(sn_dot_kernel, dim3(kDotBlocks), dim3(kT), 0, stream(),
+                     reinterpret_cast<const __hip_bfloat16*>(dx.data_ptr()),
+                     reinterpret_cast<const __hip_bfloat16*>(x.data_ptr()), P, Ca, Cb, C,
+                     sigma.data_ptr<float>(), part.data_ptr<float>());
+  IAMD_LAUNCH_CHECK();
+  return part;
+}
+
 // src [B, C, Hs, Ws] -> the (ry, rx) parity sub-grid of dst [B, C, H, W] (both channels-last bf16)
 void conv_phase_scatter(const at::Tensor& src, at::Tensor& dst, int64_t s, int64_t ry, int64_t rx,
                         int64_t i0, int64_t j0, int64_t Qy, int64_t Qx) {

@@ -1041,10 +1041,13 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
   // with <G, W> summed in the k11 epilogue (one partial per block) and the rest applied by
   // wgrad_finalize_sn in the pass that sums the split-K slabs: no bf16 G round trip and no
   // separate <G, W> / apply passes (layers/spectral_norm.py _SNScale.backward)
+  // a fifth element: <G, W> already known as partial sums (sn_dot_partials, from the data
+  // gradient) — the epilogue then reads no W
   const bool use_sn = sn.has_value() && !sn->empty();
   at::Tensor dotp;
   if (use_sn) {
-    IAMD_CHECK(nb == 1 && sn->size() == 4, "conv2d_wgrad_mfma: sn = [shadow, u, v, sigma]");
+    IAMD_CHECK(nb == 1 && (sn->size() == 4 || sn->size() == 5),
+               "conv2d_wgrad_mfma: sn = [shadow, u, v, sigma(, <G, W> partials)]");
     const at::Tensor& shw = (*sn)[0];
     IAMD_CHECK(shw.is_cuda() && shw.scalar_type() == at::kBFloat16 && shw.dim() == 4 &&
                    shw.size(0) == oc && shw.size(1) == oi && shw.size(2) == KH &&
@@ -1055,11 +1058,17 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
                    (*sn)[3].numel() == 1 && (*sn)[1].scalar_type() == at::kFloat &&
                    (*sn)[2].scalar_type() == at::kFloat && (*sn)[3].scalar_type() == at::kFloat,
                "conv2d_wgrad_mfma: SN u / v / sigma sizes");
-    a.wsn = reinterpret_cast<const __hip_bfloat16*>(shw.data_ptr());
-    a.wsn_cout = (int)oc;
-    a.wsn_cin = (int)oi;
-    dotp = at::empty({(int64_t)tiles * S}, x.options().dtype(at::kFloat));
-    a.dotp = dotp.data_ptr<float>();
+    if (sn->size() == 5) {
+      dotp = (*sn)[4];
+      IAMD_CHECK(dotp.is_cuda() && dotp.scalar_type() == at::kFloat && dotp.is_contiguous(),
+                 "conv2d_wgrad_mfma: <G, W> partials must be a contiguous fp32 tensor");
+    } else {
+      a.wsn = reinterpret_cast<const __hip_bfloat16*>(shw.data_ptr());
+      a.wsn_cout = (int)oc;
+      a.wsn_cin = (int)oi;
+      dotp = at::empty({(int64_t)tiles * S}, x.options().dtype(at::kFloat));
+      a.dotp = dotp.data_ptr<float>();
+    }
   }
   const bool direct = !use_sn && S == 1 && !out_bf16 && oc == Cout && oi == Cin;
   at::Tensor dW, part;

@@ -398,6 +398,10 @@ def _strided_dgrad(dy, wb, H, W, s, padding, wts=None, ncv=-1, ascale=None):
 # stream (51.1-51.2 vs 52.2 images/s back to back, gpurun_out r4t) — the large dgrad and wgrad
 # grids each fill the chip, and sharing it costs both more than the launch gaps it hides.
 _OVERLAP_BWD = os.environ.get('IMAGINAIRE_AMD_CONV_BWD_OVERLAP', '0')  # '1' | 'bias' | '0'
+# spectral-norm weight gradient: <G, W> from the data gradient (sigma <dx, x>, one bandwidth
+# pass over dx and x) when the input has at most this many times the weight's elements, else in
+# the k11 epilogue (which re-reads W once per split-K slab). 0: always the epilogue.
+_SN_DOT_RATIO = float(os.environ.get('IMAGINAIRE_AMD_SN_DOT_RATIO', '8'))
 _BWD_SIDE = {}
 
 
@@ -540,6 +544,12 @@ class _MfmaConv2d(torch.autograd.Function):
                         [True, False, False])[0]
                     if sig is not None:
                         dx = dx * (1.0 / sig).to(dx.dtype)
+            if sn is not None and need_w and dw is None and _SN_DOT_RATIO > 0 and \
+                    xb.numel() <= _SN_DOT_RATIO * wb.numel() and dx.dtype == torch.bfloat16 and \
+                    dx.shape[1] % 8 == 0 and dx.is_contiguous(memory_format=_CL):
+                # <G, W> = sigma <dx, x> (the adjoint identity): for a low-resolution layer the
+                # activation is smaller than the weight the k11 epilogue would re-read per split
+                sn = tuple(sn) + (_ext.ext().sn_dot_partials(dx, xb, sig),)
             if dx.shape[1] != xc:
                 dx = dx[:, :xc]
             dx = dx.to(xdt)
@@ -920,7 +930,8 @@ def _wgrad(dy, xb, wb, stride, padding, dilation, cout=-1, cin=-1, wdt=torch.flo
     # per-shape choice among the candidates (mode 1: the k11 variants; auto: those and MIOpen),
     # timed by tune_pending() between iterations; the default routing runs until then
     key = (tuple(dy.shape), tuple(xb.shape), tuple(wb.shape), stride, padding, dilation,
-           cout, cin, wdt) + (() if sn is None else ('sn',))  # (tuned with the SN epilogue)
+           cout, cin, wdt) + (() if sn is None else ('sn',) if len(sn) == 4 else ('sndx',))
+    # ('sn': tuned with the k11 <G, W> epilogue; 'sndx': <G, W> came from the data gradient)
     choice = _WGRAD_CHOICE.get(key)
     if choice is None:
         _WGRAD_PENDING.setdefault(key, (dy.dtype, xb.dtype, wb.dtype))
@@ -1006,7 +1017,7 @@ def tune_pending():
             xb = torch.randn(xs, device=dev).to(xt).contiguous(memory_format=cl)
             wb = torch.randn(ws, device=dev).to(wt).contiguous(memory_format=cl)
             sn = None
-            if len(key) > 9:  # spectral norm: the k11 variants with their <G, W> epilogue
+            if len(key) > 9 and key[9] == 'sn':  # the k11 variants with their <G, W> epilogue
                 kk = ws[2] * ws[3]
                 sn = (torch.randn((cout, cin) + tuple(ws[2:]), device=dev).to(
                     torch.bfloat16).contiguous(memory_format=cl),
@@ -1200,32 +1211,41 @@ def deconv_eligible(x, weight, stride, padding, output_padding, groups, dilation
     return ho > 0 and wo > 0 and (cap or x.shape[0] * ho * wo >= _DECONV_MIN_PIX)
 
 
-def _deconv_phase_weights(weight, s, padding, cp, op):
-    """The s*s flipped phase sub-kernels of a transposed-conv weight. For a Parameter (FlowNet2's
-    frozen decoders) they are cached on the Parameter itself, keyed on its storage and version
-    counter, so the cache dies with the weight and an in-place update invalidates it."""
-    key = (weight.data_ptr(), weight._version, s, tuple(padding), cp, op)
+def _deconv_phase_weights(weight, s, padding, cp, op, phases=True):
+    """The padded bf16 weight of a transposed conv and (``phases``) its s*s flipped phase
+    sub-kernels. For a Parameter (FlowNet2's frozen decoders) they are cached on the Parameter
+    itself, keyed on its storage and version counter, so the cache dies with the weight and an
+    in-place update invalidates it."""
+    key = (weight.data_ptr(), weight._version, s, tuple(padding), cp, op, phases)
     cached = getattr(weight, '_iamd_deconv', None)
     if cached is not None and cached[0] == key:
         return cached[1]
     wb = _pad_rows(_pad_channels(weight.detach(), op, torch.bfloat16), cp)
-    wts = {}
-    for ry in range(s):
-        for rx in range(s):
-            wts[(ry, rx)] = _ext.ext().conv_weight_flip_t(
-                wb, s, (ry + padding[0]) % s, (rx + padding[1]) % s, 1)
-    if isinstance(weight, torch.nn.Parameter):
-        weight._iamd_deconv = (key, (wb, wts))
+    wts = None
+    if phases:
+        wts = {}
+        for ry in range(s):
+            for rx in range(s):
+                wts[(ry, rx)] = _ext.ext().conv_weight_flip_t(
+                    wb, s, (ry + padding[0]) % s, (rx + padding[1]) % s, 1)
+    if isinstance(weight, torch.nn.Parameter) or not weight.requires_grad:
+        weight._iamd_deconv = (key, (wb, wts))  # (dies with the weight tensor)
     return wb, wts
 
 
 def _deconv_phase(x, weight, bias, st, pd, ho, wo):
-    """Transposed conv as the s*s k10 phase convolutions of :func:`_strided_dgrad`."""
-    cin, cout = weight.shape[0], weight.shape[1]
+    """Transposed conv as the strided data gradient of :func:`_strided_dgrad`: the one-launch
+    kernel (every phase stored straight into its parity sub-grid, no scatter pass) when
+    ``IMAGINAIRE_AMD_STRIDED_ONE_LAUNCH`` is on, else the s*s k10 phase convolutions + scatter."""
+    cin, cout, kh, kw = weight.shape
     cp, op = _round_up(cin, 64), _out_pad(cout)
-    wb, wts = _deconv_phase_weights(weight, st[0], pd, cp, op)
-    y = _strided_dgrad(_pad_channels(x, cp, torch.bfloat16), wb, ho, wo, st[0], pd, wts)
-    y = y[:, :cout] if op != cout else y
+    one = _STRIDED_ONE_LAUNCH and 0 <= pd[0] < kh and 0 <= pd[1] < kw
+    wb, wts = _deconv_phase_weights(weight, st[0], pd, cp, op, phases=not one)
+    # (one launch: Cout % 8 == 0 stores only the real output channels, no crop copy)
+    ncv = cout if (one and op != cout and cout % 8 == 0) else -1
+    y = _strided_dgrad(_pad_channels(x, cp, torch.bfloat16), wb, ho, wo, st[0], pd, wts,
+                       ncv=ncv)
+    y = y[:, :cout] if y.shape[1] != cout else y
     return y if bias is None else y + bias.to(y.dtype).view(1, -1, 1, 1)
 
 

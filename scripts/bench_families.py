@@ -37,6 +37,10 @@ def main():
     p.add_argument('--op-sites', action='store_true',
                    help='after the timed steps, attribute the aten glue of one more iteration '
                         'to Python call sites (scripts/probe/op_sites.py) on stderr')
+    p.add_argument('--ext-sites', default='',
+                   help='after the timed steps, count the calls of these extension functions '
+                        '(comma-separated, e.g. pad_channels_cast,conv_phase_scatter) of one more '
+                        'eager iteration by Python call site, on stderr')
     p.add_argument('--graph', action='store_true',
                    help='replay the steady-state iteration from a captured hipGraph (any family)')
     p.add_argument('--conv-log', action='store_true',
@@ -266,6 +270,14 @@ def main():
         record_sites(lambda: step(args.warmup + args.steps + 1), out=sys.stderr,
                      **({'ops': os.environ['OP_SITES_OPS']} if 'OP_SITES_OPS' in os.environ
                         else {}))
+    if args.ext_sites and device.type == 'cuda':
+        # one more eager iteration with the captured step's routing: extension calls by site
+        sys.path.insert(0, os.path.join(HERE, 'probe'))
+        from pad_sites_probe import record_ext_sites
+        from imaginaire_amd.utils.cuda_graph import graph_routing
+        with graph_routing():
+            record_ext_sites(lambda: step(args.warmup + args.steps + 1),
+                             tuple(args.ext_sites.split(',')), out=sys.stderr)
     if args.conv_log and device.type == 'cuda':
         from imaginaire_amd.ops import conv as conv_ops
         conv_ops.enable_conv_log(True)

@@ -24,8 +24,6 @@ def main():
     from imaginaire_amd.config import Config
     from imaginaire_amd.utils.trainer import get_model_optimizer_and_scheduler, get_trainer
     from imaginaire_amd.datasets.synthetic import DeviceBatchSource
-    from imaginaire_amd.ops import conv as C
-    from imaginaire_amd.ops import _ext
     torch.cuda.set_device(0)
     cfg = Config(args.config)
     cfg.logdir = '/tmp/iamd_padsites'
@@ -41,31 +39,41 @@ def main():
     for i in range(2):
         step(i)
     torch.cuda.synchronize()
+    record_ext_sites(lambda: step(2), ('pad_channels_cast',))
+
+
+def record_ext_sites(step_fn, names, out=sys.stdout, depth=3):
+    """Run ``step_fn`` once with the listed extension functions wrapped: count their calls by
+    (function, Python call site, first operand's shape) and print the table to ``out``."""
+    from imaginaire_amd.ops import _ext
     stats = collections.Counter()
     ext = _ext.ext()
-    orig = ext.pad_channels_cast
 
     class Shim(object):
         def __getattr__(self, name):
-            return getattr(ext, name)
+            fn = getattr(ext, name)
+            if name not in names:
+                return fn
 
-        def pad_channels_cast(self, t, c, dtype):
-            fr = [f for f in traceback.extract_stack()[:-1] if HERE in f.filename]
-            site = ' <- '.join('%s:%d' % (os.path.relpath(f.filename, HERE), f.lineno)
-                               for f in fr[-3:][::-1])
-            stats[(site, tuple(t.shape), c)] += 1
-            return orig(t, c, dtype)
+            def wrapped(*a, **k):
+                fr = [f for f in traceback.extract_stack()[:-1] if HERE in f.filename]
+                site = ' <- '.join('%s:%d' % (os.path.relpath(f.filename, HERE), f.lineno)
+                                   for f in fr[-depth:][::-1])
+                shape = tuple(a[0].shape) if a and torch.is_tensor(a[0]) else ()
+                stats[(name, site, shape)] += 1
+                return fn(*a, **k)
+            return wrapped
     shim = Shim()
     old = _ext.ext
     _ext.ext = lambda: shim
     try:
-        step(2)
+        step_fn()
         torch.cuda.synchronize()
     finally:
         _ext.ext = old
-    print('pad_channels_cast launches: %d' % sum(stats.values()))
-    for (site, shape, c), n in stats.most_common():
-        print('%4d  %-24s -> %4d  %s' % (n, shape, c, site))
+    print('extension calls (%s): %d' % (','.join(names), sum(stats.values())), file=out)
+    for (name, site, shape), n in stats.most_common():
+        print('%5d  %-18s %-26s %s' % (n, name, shape, site), file=out)
 
 
 if __name__ == '__main__':

@@ -1112,8 +1112,9 @@ def test_avg_pool_nhwc(dtype, cfg, channels):
 @pytest.mark.parametrize('shape', [(2, 194, 32, 128, 256), (1, 162, 16, 256, 512),
                                    (1, 130, 64, 64, 128)])
 def test_conv_transpose_phase_path(shape):
-    """Inference transposed conv (4x4 / s2 / p1) as k10 phase convolutions (ops.conv) vs
-    the fp32 PyTorch transposed conv; the FlowNet2 decoder shapes."""
+    """Inference transposed conv (4x4 / s2 / p1) as the strided data gradient (ops.conv: the
+    one-launch kernel, and the k10 phase convolutions + scatter) vs the fp32 PyTorch transposed
+    conv; the FlowNet2 decoder shapes."""
     from imaginaire_amd.ops import conv as C
     b, cin, cout, h, w = shape
     torch.manual_seed(0)
@@ -1122,20 +1123,22 @@ def test_conv_transpose_phase_path(shape):
     wt = (torch.randn(cin, cout, 4, 4, device='cuda') / (cin * 4) ** 0.5).to(torch.bfloat16)
     bias = torch.randn(cout, device='cuda').to(torch.bfloat16)
     ref = F.conv_transpose2d(x.float(), wt.float(), bias.float(), 2, 1)
-    saved = C._DECONV_MIN_PIX, C._DECONV_FORCE
+    saved = C._DECONV_MIN_PIX, C._DECONV_FORCE, C._STRIDED_ONE_LAUNCH
     C._DECONV_MIN_PIX = 0
     try:
         assert C.deconv_eligible(x, wt, (2, 2), (1, 1), (0, 0), 1, (1, 1))
-        for force in ('k10s', None):  # the phase path, then the tuned choice
-            C._DECONV_FORCE = force
-            for wgt in (wt, torch.nn.Parameter(wt, requires_grad=False)):  # uncached, cached
-                with torch.no_grad():
-                    y = C.conv_transpose2d(x, wgt, bias, 2, 1)
-                assert y.shape == ref.shape
-                err = (y.float() - ref).abs().max() / ref.abs().max()
-                assert err < 2e-2, (force, float(err))
+        for one in (True, False):
+            C._STRIDED_ONE_LAUNCH = one
+            for force in ('k10s', None):  # the HIP path, then the tuned choice
+                C._DECONV_FORCE = force
+                for wgt in (wt, torch.nn.Parameter(wt, requires_grad=False)):  # uncached, cached
+                    with torch.no_grad():
+                        y = C.conv_transpose2d(x, wgt, bias, 2, 1)
+                    assert y.shape == ref.shape
+                    err = (y.float() - ref).abs().max() / ref.abs().max()
+                    assert err < 2e-2, (one, force, float(err))
     finally:
-        C._DECONV_MIN_PIX, C._DECONV_FORCE = saved
+        C._DECONV_MIN_PIX, C._DECONV_FORCE, C._STRIDED_ONE_LAUNCH = saved
 
 
 @pytest.mark.gpu

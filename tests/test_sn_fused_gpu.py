@@ -35,7 +35,10 @@ def _cos(a, b):
     return float(torch.dot(a, b) / (a.norm() * b.norm()).clamp_min(1e-30))
 
 
-def test_sn_fused_conv_matches_materialised_and_fp32(monkeypatch):
+@pytest.mark.parametrize('dot_ratio', [8.0, 0.0, 1e9])
+def test_sn_fused_conv_matches_materialised_and_fp32(monkeypatch, dot_ratio):
+    """(``dot_ratio``: where <G, W> comes from — the default mix of the k11 epilogue and the
+    data-gradient identity sigma <dx, x>, the epilogue everywhere, the identity everywhere)"""
     from imaginaire_amd.layers import spectral_norm as snm
     from imaginaire_amd.ops import conv as C
     from imaginaire_amd.optimizers import fused_adam as FA
@@ -60,6 +63,7 @@ def test_sn_fused_conv_matches_materialised_and_fp32(monkeypatch):
                 calls.append(tuple(a[1].shape))
             return orig.forward(ctx, *a)
     monkeypatch.setattr(C, '_MfmaConv2d', Counting)
+    monkeypatch.setattr(C, '_SN_DOT_RATIO', dot_ratio)
 
     old_fused, old_shadow = snm._SN_FUSED, snm._SN_SHADOW
     snm._SN_SHADOW = True
