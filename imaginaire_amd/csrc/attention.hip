@@ -65,6 +65,39 @@ __device__ __forceinline__ bf16x8 read_a_split(const __bf16* row, int g) {
                *reinterpret_cast<const bf16x4*>(row + 16 + g * 4));
 }
 
+// Register-staged tile copy global -> LDS in two halves: load() issues the 16-byte global loads
+// of the NEXT block into registers before the current block's MFMAs, store() writes them to
+// LDS after the barrier — the global latency of block k + 1 overlaps the compute of block k
+// (the synchronous load -> LDS -> barrier -> compute loop waited a full L2 / HBM round trip per
+// block: ~0.2 us of MFMAs per step against ~1-2 us of latency). ROWS x COLS bf16 tile, source
+// row stride ``stride`` elements, LDS row pitch LDP elements, NT threads.
+template <int ROWS, int COLS, int LDP, int NT>
+struct TileStage {
+  static constexpr int T = ROWS * COLS / 8;    // 16-byte chunks
+  static constexpr int I = (T + NT - 1) / NT;  // chunks per thread
+  bf16x8 r[I];
+  __device__ __forceinline__ void load(const __bf16* base, int64_t stride, int tid) {
+#pragma unroll
+    for (int i = 0; i < I; ++i) {
+      const int e = tid + i * NT;
+      if (T % NT == 0 || e < T) {
+        const int rr = e / (COLS / 8), cc = (e - rr * (COLS / 8)) * 8;
+        r[i] = *reinterpret_cast<const bf16x8*>(base + (int64_t)rr * stride + cc);
+      }
+    }
+  }
+  __device__ __forceinline__ void store(__bf16* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < I; ++i) {
+      const int e = tid + i * NT;
+      if (T % NT == 0 || e < T) {
+        const int rr = e / (COLS / 8), cc = (e - rr * (COLS / 8)) * 8;
+        *reinterpret_cast<bf16x8*>(lds + rr * LDP + cc) = r[i];
+      }
+    }
+  }
+};
+
 // ---- forward -----------------------------------------------------------------------------
 // workgroup: 64 queries (wave w: queries 16w..16w+15) x all keys in blocks of 64 staged in LDS
 // (K row-major, V^T from a host-transposed copy: 16-byte copies, no LDS transposition). Per block and wave: S^T (4 key tiles x D/32 MFMAs), the online
@@ -95,19 +128,21 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(
   for (int i = 0; i < DV / 16; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = kNegBig, lsum = 0.f;
   const int kbeg = sp * klen, kend = min(Lk, kbeg + klen);
+  TileStage<KB, D, KP, NW * 64> sK;
+  TileStage<DV, KB, VP, NW * 64> sV;  // 16-byte rows of V^T
+  if (kbeg < kend) {
+    sK.load(kb + (int64_t)kbeg * D, D, tid);
+    sV.load(vtb + kbeg, Lk, tid);
+  }
   for (int k0 = kbeg; k0 < kend; k0 += KB) {
     __syncthreads();
-    for (int e = tid; e < KB * D / 8; e += NW * 64) {
-      const int r = e / (D / 8), c = (e - r * (D / 8)) * 8;
-      *reinterpret_cast<bf16x8*>(&Ks[r * KP + c]) =
-          *reinterpret_cast<const bf16x8*>(kb + (int64_t)(k0 + r) * D + c);
-    }
-    for (int e = tid; e < DV * KB / 8; e += NW * 64) {  // 16-byte rows of V^T
-      const int r = e / (KB / 8), c = (e - r * (KB / 8)) * 8;
-      *reinterpret_cast<bf16x8*>(&Vt[r * VP + c]) =
-          *reinterpret_cast<const bf16x8*>(vtb + (int64_t)r * Lk + k0 + c);
-    }
+    sK.store(Ks, tid);
+    sV.store(Vt, tid);
     __syncthreads();
+    if (k0 + KB < kend) {  // the next block's loads fly during this block's MFMAs
+      sK.load(kb + (int64_t)(k0 + KB) * D, D, tid);
+      sV.load(vtb + k0 + KB, Lk, tid);
+    }
     f32x4 s[4];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
@@ -212,7 +247,9 @@ __global__ __launch_bounds__(256) void attn_sum_splits(const float* __restrict__
 // in blocks of 32 staged in LDS both row-major (A operands of S, dP) and transposed (A operands
 // of dV^T, dK^T). S = Q K^T and dP = dO V^T put the key in the lane's column, so P and dS feed
 // dV^T += dO^T P and dK^T += Q^T dS as B operands.
-template <int D, int DV, int NW>
+// PFO: the dO / dO^T tiles are prefetched too (else loaded after the barrier, as the Q tiles
+// used to be): at D = 128, DV = 288 with 8 waves the full prefetch exceeds 256 VGPRs
+template <int D, int DV, int NW, bool PFO>
 __global__ __launch_bounds__(NW * 64) void attn_bwd_dkv_kernel(
     const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v,
     const __bf16* __restrict__ dout, const __bf16* __restrict__ qt,
@@ -247,34 +284,41 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkv_kernel(
   for (int i = 0; i < D / 16; ++i) dkt[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < DV / 16; ++i) dvt[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int qend = min(Lq, (sp + 1) * qlen);
-  for (int q0 = sp * qlen; q0 < qend; q0 += QB) {
-    __syncthreads();
-    for (int e = tid; e < QB * D / 8; e += NW * 64) {
-      const int r = e / (D / 8), c = (e - r * (D / 8)) * 8;
-      *reinterpret_cast<bf16x8*>(&Qs[r * QP + c]) =
-          *reinterpret_cast<const bf16x8*>(qb + (int64_t)(q0 + r) * D + c);
-    }
-    for (int e = tid; e < D * QB / 8; e += NW * 64) {  // Q^T rows (host-transposed copy)
-      const int r = e / (QB / 8), c = (e - r * (QB / 8)) * 8;
-      *reinterpret_cast<bf16x8*>(&Qt[r * TP + c]) =
-          *reinterpret_cast<const bf16x8*>(qtb + (int64_t)r * Lq + q0 + c);
-    }
-    for (int e = tid; e < QB * DV / 8; e += NW * 64) {
-      const int r = e / (DV / 8), c = (e - r * (DV / 8)) * 8;
-      *reinterpret_cast<bf16x8*>(&Os[r * OP + c]) =
-          *reinterpret_cast<const bf16x8*>(ob + (int64_t)(q0 + r) * DV + c);
-    }
-    for (int e = tid; e < DV * QB / 8; e += NW * 64) {  // dO^T rows
-      const int r = e / (QB / 8), c = (e - r * (QB / 8)) * 8;
-      *reinterpret_cast<bf16x8*>(&Ot[r * TP + c]) =
-          *reinterpret_cast<const bf16x8*>(otb + (int64_t)r * Lq + q0 + c);
+  const int qbeg = sp * qlen, qend = min(Lq, (sp + 1) * qlen);
+  TileStage<QB, D, QP, NW * 64> sQ;
+  TileStage<D, QB, TP, NW * 64> sQt;   // Q^T rows (host-transposed copy)
+  TileStage<QB, DV, OP, NW * 64> sO;
+  TileStage<DV, QB, TP, NW * 64> sOt;  // dO^T rows
+  float lsv = 0.f, dsv = 0.f;
+  auto prefetch = [&](int q0) {
+    sQ.load(qb + (int64_t)q0 * D, D, tid);
+    sQt.load(qtb + q0, Lq, tid);
+    if constexpr (PFO) {
+      sO.load(ob + (int64_t)q0 * DV, DV, tid);
+      sOt.load(otb + q0, Lq, tid);
     }
     if (tid < QB) {
-      Ls[tid] = lse2[(int64_t)b * Lq + q0 + tid];
-      Ds[tid] = dsum[(int64_t)b * Lq + q0 + tid];
+      lsv = lse2[(int64_t)b * Lq + q0 + tid];
+      dsv = dsum[(int64_t)b * Lq + q0 + tid];
+    }
+  };
+  if (qbeg < qend) prefetch(qbeg);
+  for (int q0 = qbeg; q0 < qend; q0 += QB) {
+    __syncthreads();
+    sQ.store(Qs, tid);
+    sQt.store(Qt, tid);
+    if constexpr (!PFO) {
+      sO.load(ob + (int64_t)q0 * DV, DV, tid);
+      sOt.load(otb + q0, Lq, tid);
+    }
+    sO.store(Os, tid);
+    sOt.store(Ot, tid);
+    if (tid < QB) {
+      Ls[tid] = lsv;
+      Ds[tid] = dsv;
     }
     __syncthreads();
+    if (q0 + QB < qend) prefetch(q0 + QB);  // in flight during this block's MFMAs
     float p[2][4], ds[2][4];
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
@@ -365,25 +409,23 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(
   f32x4 acc[D / 16];
 #pragma unroll
   for (int i = 0; i < D / 16; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int kend = min(Lk, (sp + 1) * klen);
-  for (int k0 = sp * klen; k0 < kend; k0 += KB) {
+  const int kbeg = sp * klen, kend = min(Lk, (sp + 1) * klen);
+  TileStage<KB, D, KP, NW * 64> sK;
+  TileStage<D, KB, TP, NW * 64> sKt;  // K^T rows (host-transposed copy)
+  TileStage<KB, DV, VP, NW * 64> sV;
+  auto prefetch = [&](int k0) {
+    sK.load(kb + (int64_t)k0 * D, D, tid);
+    sKt.load(ktb + k0, Lk, tid);
+    sV.load(vb + (int64_t)k0 * DV, DV, tid);
+  };
+  if (kbeg < kend) prefetch(kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += KB) {
     __syncthreads();
-    for (int e = tid; e < KB * D / 8; e += NW * 64) {
-      const int r = e / (D / 8), c = (e - r * (D / 8)) * 8;
-      *reinterpret_cast<bf16x8*>(&Ks[r * KP + c]) =
-          *reinterpret_cast<const bf16x8*>(kb + (int64_t)(k0 + r) * D + c);
-    }
-    for (int e = tid; e < D * KB / 8; e += NW * 64) {  // K^T rows (host-transposed copy)
-      const int r = e / (KB / 8), c = (e - r * (KB / 8)) * 8;
-      *reinterpret_cast<bf16x8*>(&Kt[r * TP + c]) =
-          *reinterpret_cast<const bf16x8*>(ktb + (int64_t)r * Lk + k0 + c);
-    }
-    for (int e = tid; e < KB * DV / 8; e += NW * 64) {
-      const int r = e / (DV / 8), c = (e - r * (DV / 8)) * 8;
-      *reinterpret_cast<bf16x8*>(&Vs[r * VP + c]) =
-          *reinterpret_cast<const bf16x8*>(vb + (int64_t)(k0 + r) * DV + c);
-    }
+    sK.store(Ks, tid);
+    sKt.store(Kt, tid);
+    sV.store(Vs, tid);
     __syncthreads();
+    if (k0 + KB < kend) prefetch(k0 + KB);  // in flight during this block's MFMAs
     float ds[2][4];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
@@ -547,13 +589,25 @@ void launch_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
     const dim3 grid((unsigned)(Lk / (nwk * 16)), (unsigned)nq, (unsigned)B);
     float* dkpp = nq > 1 ? dkp.data_ptr<float>() : nullptr;
     float* dvpp = nq > 1 ? dvp.data_ptr<float>() : nullptr;
-    if (nwk == 8)
-      hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, DV, 8>), grid, dim3(512), 0, stream(), bp(q),
-                         bp(k), bp(v), bp(dout), bp(qt), bp(dott), lse.data_ptr<float>(),
+    // IMAGINAIRE_AMD_ATTN_PF_O: prefetch the dO tiles of the 8-wave dK / dV kernel too
+    // (1) or not (0; default for the widest heads, where it would spill)
+    static const int pfo_env = [] {
+      const char* e = std::getenv("IMAGINAIRE_AMD_ATTN_PF_O");
+      return e == nullptr ? -1 : std::atoi(e);
+    }();
+    const bool pfo = pfo_env < 0 ? !(D == 128 && DV > 256) : pfo_env != 0;
+    if (nwk == 8 && pfo)
+      hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, DV, 8, true>), grid, dim3(512), 0, stream(),
+                         bp(q), bp(k), bp(v), bp(dout), bp(qt), bp(dott), lse.data_ptr<float>(),
+                         dsum.data_ptr<float>(), bpm(dk), bpm(dv), (int)Lq, (int)Lk, sl2, sc,
+                         qlen, dkpp, dvpp);
+    else if (nwk == 8)
+      hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, DV, 8, false>), grid, dim3(512), 0, stream(),
+                         bp(q), bp(k), bp(v), bp(dout), bp(qt), bp(dott), lse.data_ptr<float>(),
                          dsum.data_ptr<float>(), bpm(dk), bpm(dv), (int)Lq, (int)Lk, sl2, sc,
                          qlen, dkpp, dvpp);
     else
-      hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, DV, 4>), grid, dim3(256), 0, stream(), bp(q),
+      hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, DV, 4, true>), grid, dim3(256), 0, stream(), bp(q),
                          bp(k), bp(v), bp(dout), bp(qt), bp(dott), lse.data_ptr<float>(),
                          dsum.data_ptr<float>(), bpm(dk), bpm(dv), (int)Lq, (int)Lk, sl2, sc,
                          qlen, dkpp, dvpp);
