@@ -129,6 +129,8 @@ at::Tensor conv_tap_sum(const at::Tensor& z, const c10::optional<at::Tensor>& bi
 at::Tensor conv_tap_gather(const at::Tensor& dy, int64_t Cz, int64_t KH, int64_t KW, int64_t ph,
                            int64_t pw, int64_t dh, int64_t dw, int64_t H, int64_t W);
 // pool.hip
+at::Tensor max_pool_nhwc_fwd(const at::Tensor& x, int64_t kh, int64_t kw);
+at::Tensor max_pool_nhwc_bwd(const at::Tensor& x, const at::Tensor& dy, int64_t kh, int64_t kw);
 at::Tensor avg_pool_nhwc_fwd(const at::Tensor& x, int64_t kh, int64_t kw, int64_t sh, int64_t sw,
                              int64_t ph, int64_t pw, bool include_pad);
 at::Tensor avg_pool_nhwc_bwd(const at::Tensor& dy, int64_t H, int64_t W, int64_t kh, int64_t kw,
@@ -224,6 +226,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "strided-conv dgrad: one phase conv output into its parity sub-grid of dx");
   m.def("pad_channels_cast", &iamd::pad_channels_cast,
         "zero-padded channel copy + dtype cast into a channels-last tensor");
+  m.def("max_pool_nhwc_fwd", &iamd::max_pool_nhwc_fwd,
+        "k14 NHWC max pool, kernel == stride, no padding");
+  m.def("max_pool_nhwc_bwd", &iamd::max_pool_nhwc_bwd,
+        "k14 NHWC max pool backward (argmax recomputed from the input)");
   m.def("avg_pool_nhwc_fwd", &iamd::avg_pool_nhwc_fwd, "NHWC average pooling (k14)");
   m.def("avg_pool_nhwc_bwd", &iamd::avg_pool_nhwc_bwd, "k14 backward (gather)");
   m.def("pad_nhwc_fwd", &iamd::pad_nhwc_fwd, "NHWC reflect / replicate padding");

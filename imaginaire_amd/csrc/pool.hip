@@ -12,6 +12,8 @@
 //     output windows that cover it — no atomics, deterministic, one 16-byte store.
 #include "common.h"
 
+#include <cmath>
+
 namespace iamd {
 namespace {
 
@@ -108,6 +110,85 @@ avgpool_bwd(const T* __restrict__ dy, T* __restrict__ dx, PoolGeom g) {
   }
 }
 
+// NHWC max pooling, non-overlapping windows (kernel == stride, no padding: VGG-19's 2x2 pools in
+// the perceptual losses). Forward: one thread per (output pixel, V channels). Backward: one thread
+// per (output window, V channels) recomputes the window's argmax from the saved input — the first
+// maximum in scan order, the last NaN winning as in PyTorch's kernels — and writes the whole window of dx (dy at
+// the argmax, zeros elsewhere): no int64 index tensor, no atomics, every dx element written once.
+template <typename T, int V>
+__global__ void __launch_bounds__(kT)
+maxpool_fwd(const T* __restrict__ x, T* __restrict__ y, PoolGeom g) {
+  const int cv = g.C / V;
+  const int64_t total = (int64_t)g.B * g.Ho * g.Wo * cv;
+  for (int64_t t = (int64_t)blockIdx.x * kT + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * kT) {
+    const int c8 = (int)(t % cv);
+    int64_t p = t / cv;
+    const int ox = (int)(p % g.Wo);
+    p /= g.Wo;
+    const int oy = (int)(p % g.Ho);
+    const int b = (int)(p / g.Ho);
+    float m[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) m[k] = -INFINITY;
+    for (int dy = 0; dy < g.kh; ++dy)
+      for (int dx = 0; dx < g.kw; ++dx) {
+        float v[V];
+        load_vec<T, V>(x + (((int64_t)b * g.H + oy * g.sh + dy) * g.W + ox * g.sw + dx) * g.C +
+                           c8 * V, v);
+#pragma unroll
+        for (int k = 0; k < V; ++k)
+          if (v[k] > m[k] || isnan(v[k])) m[k] = v[k];
+      }
+    store_vec<T, V>(y + t * V, m);
+  }
+}
+
+template <typename T, int V>
+__global__ void __launch_bounds__(kT)
+maxpool_bwd(const T* __restrict__ x, const T* __restrict__ dy, T* __restrict__ dx, PoolGeom g) {
+  const int cv = g.C / V;
+  const int64_t total = (int64_t)g.B * g.Ho * g.Wo * cv;
+  for (int64_t t = (int64_t)blockIdx.x * kT + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * kT) {
+    const int c8 = (int)(t % cv);
+    int64_t p = t / cv;
+    const int ox = (int)(p % g.Wo);
+    p /= g.Wo;
+    const int oy = (int)(p % g.Ho);
+    const int b = (int)(p / g.Ho);
+    float m[V];
+    int arg[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      m[k] = -INFINITY;
+      arg[k] = 0;
+    }
+    for (int i = 0; i < g.kh * g.kw; ++i) {
+      const int ddy = i / g.kw, ddx = i - ddy * g.kw;
+      float v[V];
+      load_vec<T, V>(x + (((int64_t)b * g.H + oy * g.sh + ddy) * g.W + ox * g.sw + ddx) * g.C +
+                         c8 * V, v);
+#pragma unroll
+      for (int k = 0; k < V; ++k)
+        if (v[k] > m[k] || isnan(v[k])) {
+          m[k] = v[k];
+          arg[k] = i;
+        }
+    }
+    float gv[V];
+    load_vec<T, V>(dy + t * V, gv);
+    for (int i = 0; i < g.kh * g.kw; ++i) {
+      const int ddy = i / g.kw, ddx = i - ddy * g.kw;
+      float o[V];
+#pragma unroll
+      for (int k = 0; k < V; ++k) o[k] = arg[k] == i ? gv[k] : 0.f;
+      store_vec<T, V>(dx + (((int64_t)b * g.H + oy * g.sh + ddy) * g.W + ox * g.sw + ddx) * g.C +
+                          c8 * V, o);
+    }
+  }
+}
+
 int grid_for(int64_t n) {
   return (int)std::max<int64_t>(1, std::min<int64_t>((n + kT - 1) / kT, 65536));
 }
@@ -172,6 +253,62 @@ at::Tensor avg_pool_nhwc_bwd(const at::Tensor& dy, int64_t H, int64_t W, int64_t
                          reinterpret_cast<scalar_t*>(dx.data_ptr()), g);
     else
       hipLaunchKernelGGL((avgpool_bwd<scalar_t, 1>), dim3(grid_for(n)), dim3(kT), 0, stream(),
+                         reinterpret_cast<const scalar_t*>(dy.data_ptr()),
+                         reinterpret_cast<scalar_t*>(dx.data_ptr()), g);
+  });
+  IAMD_LAUNCH_CHECK();
+  return dx;
+}
+
+// (kernel == stride, no padding; rows / columns past the last whole window get no window)
+at::Tensor max_pool_nhwc_fwd(const at::Tensor& x, int64_t kh, int64_t kw) {
+  IAMD_CHECK(x.is_cuda() && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                 (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat) &&
+                 x.size(2) >= kh && x.size(3) >= kw && kh >= 1 && kw >= 1,
+             "max_pool_nhwc_fwd: packed channels-last bf16 / fp32 tensor, window within it");
+  const PoolGeom g = geom(x, x.size(2) / kh, x.size(3) / kw, kh, kw, kh, kw, 0, 0, true);
+  auto y = at::empty({g.B, g.C, g.Ho, g.Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const bool v8 = g.C % 8 == 0;
+  const int64_t n = (int64_t)g.B * g.Ho * g.Wo * (v8 ? g.C / 8 : g.C);
+  IAMD_DISPATCH_FLOAT_TYPES(x.scalar_type(), "max_pool_nhwc_fwd", [&] {
+    if (v8)
+      hipLaunchKernelGGL((maxpool_fwd<scalar_t, 8>), dim3(grid_for(n)), dim3(kT), 0, stream(),
+                         reinterpret_cast<const scalar_t*>(x.data_ptr()),
+                         reinterpret_cast<scalar_t*>(y.data_ptr()), g);
+    else
+      hipLaunchKernelGGL((maxpool_fwd<scalar_t, 1>), dim3(grid_for(n)), dim3(kT), 0, stream(),
+                         reinterpret_cast<const scalar_t*>(x.data_ptr()),
+                         reinterpret_cast<scalar_t*>(y.data_ptr()), g);
+  });
+  IAMD_LAUNCH_CHECK();
+  return y;
+}
+
+at::Tensor max_pool_nhwc_bwd(const at::Tensor& x, const at::Tensor& dy, int64_t kh, int64_t kw) {
+  IAMD_CHECK(x.is_cuda() && dy.is_cuda() && x.dim() == 4 && dy.dim() == 4 &&
+                 x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                 dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                 x.scalar_type() == dy.scalar_type() &&
+                 (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat) &&
+                 dy.size(0) == x.size(0) && dy.size(1) == x.size(1) &&
+                 dy.size(2) == x.size(2) / kh && dy.size(3) == x.size(3) / kw,
+             "max_pool_nhwc_bwd: input / gradient shapes");
+  const PoolGeom g = geom(x, dy.size(2), dy.size(3), kh, kw, kh, kw, 0, 0, true);
+  // pixels past the last whole window get no gradient: zero-fill only when there are any
+  const bool tail = x.size(2) % kh != 0 || x.size(3) % kw != 0;
+  auto dx = tail ? at::zeros_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast))
+                 : at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const bool v8 = g.C % 8 == 0;
+  const int64_t n = (int64_t)g.B * g.Ho * g.Wo * (v8 ? g.C / 8 : g.C);
+  IAMD_DISPATCH_FLOAT_TYPES(x.scalar_type(), "max_pool_nhwc_bwd", [&] {
+    if (v8)
+      hipLaunchKernelGGL((maxpool_bwd<scalar_t, 8>), dim3(grid_for(n)), dim3(kT), 0, stream(),
+                         reinterpret_cast<const scalar_t*>(x.data_ptr()),
+                         reinterpret_cast<const scalar_t*>(dy.data_ptr()),
+                         reinterpret_cast<scalar_t*>(dx.data_ptr()), g);
+    else
+      hipLaunchKernelGGL((maxpool_bwd<scalar_t, 1>), dim3(grid_for(n)), dim3(kT), 0, stream(),
+                         reinterpret_cast<const scalar_t*>(x.data_ptr()),
                          reinterpret_cast<const scalar_t*>(dy.data_ptr()),
                          reinterpret_cast<scalar_t*>(dx.data_ptr()), g);
   });

@@ -20,6 +20,7 @@ from imaginaire_amd.utils.distributed import master_only_print as print
 from imaginaire_amd.ops.loss import weighted_l1
 from imaginaire_amd.utils.misc import apply_imagenet_normalization
 from imaginaire_amd.ops.resize import interpolate
+from imaginaire_amd.ops.pool import max_pool2d
 
 
 class PerceptualLoss(nn.Module):
@@ -135,6 +136,9 @@ class _PerceptualNetwork(nn.Module):
             elif x.is_cuda and type(layer) is nn.Conv2d:
                 x = nhwc_conv.conv2d(x, layer.weight, layer.bias, layer.stride, layer.padding,
                                      layer.dilation, layer.groups, layer.padding_mode)
+            elif x.is_cuda and type(layer) is nn.MaxPool2d:
+                x = max_pool2d(x, layer.kernel_size, layer.stride, layer.padding, layer.dilation,
+                               layer.ceil_mode)
             else:
                 x = layer(x)
             layer_name = self.layer_name_mapping.get(i, None)

@@ -1,4 +1,5 @@
-"""NHWC average pooling (k14, ``csrc/pool.hip``) with a gather backward.
+"""NHWC average pooling (k14, ``csrc/pool.hip``) with a gather backward, and NHWC max pooling
+over non-overlapping windows (``max_pool2d``).
 
 ``avg_pool2d`` / ``AvgPool2d`` are drop-ins for ``F.avg_pool2d`` / ``nn.AvgPool2d`` (no
 parameters, identical state dicts). Packed channels-last bf16 / fp32 activations run the HIP
@@ -50,6 +51,39 @@ def avg_pool2d(x, kernel_size, stride=None, padding=0, ceil_mode=False, count_in
     if valid is not None:  # pooling acts per channel: a zero channel tail stays zero
         y._iamd_valid_channels = valid
     return y
+
+
+class _MaxPoolNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k):
+        ctx.k = k
+        ctx.save_for_backward(x)
+        return _ext.ext().max_pool_nhwc_fwd(x, k[0], k[1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        if dy.dtype != x.dtype:
+            dy = dy.to(x.dtype)
+        return _ext.ext().max_pool_nhwc_bwd(x, dy, ctx.k[0], ctx.k[1]), None
+
+
+def max_pool2d(x, kernel_size, stride=None, padding=0, dilation=1, ceil_mode=False,
+               return_indices=False):
+    """``F.max_pool2d``. Non-overlapping windows (kernel == stride, no padding / dilation — VGG's
+    2x2 pools) on packed NHWC bf16 / fp32 activations run the k14 max-pool kernels (the backward
+    recomputes each window's argmax from the input: no int64 index tensor); anything else runs
+    PyTorch."""
+    k = _pair(kernel_size)
+    s = _pair(stride if stride is not None else kernel_size)
+    if x.is_cuda and x.dim() == 4 and k == s and _pair(padding) == (0, 0) and \
+            _pair(dilation) == (1, 1) and not ceil_mode and not return_indices and \
+            x.dtype in (torch.bfloat16, torch.float32) and \
+            x.is_contiguous(memory_format=torch.channels_last) and _ext.use_native(x) and \
+            x.shape[2] >= k[0] and x.shape[3] >= k[1]:
+        return _MaxPoolNHWC.apply(x, k)
+    return F.max_pool2d(x, kernel_size, stride, padding, dilation, ceil_mode, return_indices)
 
 
 class AvgPool2d(nn.Module):

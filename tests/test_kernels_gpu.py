@@ -1968,3 +1968,27 @@ def test_non_local_block_k16_matches_fp32(c, h, w):
     floor[0] = 1e-2 * max(float(r.norm()) for r in ref[2])
     for i, (a, t, r) in enumerate(zip(k16[2], tbf[2], ref[2])):
         assert rel(a, r) <= 3.0 * rel(t, r) + 3e-2, ('param%d' % i, rel(a, r), rel(t, r))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize('shape,k', [((2, 64, 32, 48), 2), ((2, 24, 17, 19), 2), ((1, 5, 9, 9), 3)])
+def test_max_pool_nhwc_matches_torch(dtype, shape, k):
+    """k14 NHWC max pool (non-overlapping windows, VGG's 2x2 pools) and its argmax-recomputing
+    backward against PyTorch's max_pool2d (fp32): values, gradients (incl. ties: the first
+    maximum in scan order gets the gradient, as in PyTorch), odd sizes and narrow channels."""
+    from imaginaire_amd.ops import pool as P
+    torch.manual_seed(51)
+    x = torch.randn(shape, device='cuda')
+    x[:, :, :4, :4] = torch.round(x[:, :, :4, :4])  # ties inside some windows
+    x = x.to(dtype).contiguous(memory_format=torch.channels_last)
+    xa = x.clone().requires_grad_(True)
+    y = P.max_pool2d(xa, k)
+    assert y.grad_fn is not None and 'MaxPoolNHWC' in type(y.grad_fn).__name__
+    xr = x.detach().float().requires_grad_(True)
+    yr = F.max_pool2d(xr, k)
+    assert y.shape == yr.shape and torch.equal(y.float(), yr)
+    g = torch.randn_like(yr).to(dtype).float()
+    y.backward(g.to(dtype).contiguous(memory_format=torch.channels_last))
+    yr.backward(g)
+    assert torch.equal(xa.grad.float(), xr.grad)
