@@ -300,8 +300,16 @@ class SPADEGenerator(nn.Module):
         x = self.up_2a(x, seg)
         x = self.cbn_up_2a(x, z) if self.use_style_encoder else self.conv_up_2a(x)
         x = self.up_2b(x, seg)
-        x = self.nearest_upsample2x(x)
-        if self.out_image_small_side_size == 256:
+        if self.out_image_small_side_size == 256 and x.is_cuda and \
+                list(self.conv_img256.layers.keys())[:1] == ['nonlinearity']:
+            # the head's leading activation commutes with the nearest upsampling: applied before
+            # it, on a quarter of the pixels (the 2 x F-channel full-resolution map is the
+            # largest activation of the generator)
+            act = self.conv_img256.layers['nonlinearity']
+            x = self.nearest_upsample2x(act(x))
+            x = torch.tanh(self.conv_img256(x, skip_first_act=True))
+        elif self.out_image_small_side_size == 256:
+            x = self.nearest_upsample2x(x)
             x = torch.tanh(self.conv_img256(x))
         elif self.out_image_small_side_size == 512:
             x256 = self.nearest_upsample2x(self.conv_img256(x))

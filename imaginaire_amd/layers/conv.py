@@ -98,11 +98,14 @@ class _BaseConvBlock(nn.Module):
         self.conditional = getattr(conv_layer, 'conditional', False) or \
             getattr(activation_norm_layer, 'conditional', False)
 
-    def forward(self, x, *cond_inputs, residual=None, **kw_cond_inputs):
+    def forward(self, x, *cond_inputs, residual=None, skip_first_act=False, **kw_cond_inputs):
         """``residual``: added to the block's output (a residual block's shortcut). When the
-        block ends in a plain 2-D conv it lands in the k10 epilogue (ops/conv.py ``conv2d``)."""
+        block ends in a plain 2-D conv it lands in the k10 epilogue (ops/conv.py ``conv2d``).
+        ``skip_first_act``: the caller already applied the block's leading nonlinearity (an
+        'A..' order block; e.g. before a nearest upsampling it commutes with, on 4x fewer
+        pixels)."""
         keys = list(self.layers.keys())
-        i = 0
+        i = 1 if (skip_first_act and keys and keys[0] == 'nonlinearity') else 0
         n = len(keys)
         while i < n:
             name = keys[i]
