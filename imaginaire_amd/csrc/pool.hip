@@ -74,34 +74,6 @@ avgpool_fwd(const T* __restrict__ x, T* __restrict__ y, PoolGeom g) {
   }
 }
 
-// V = 1 (odd channel counts: the 185-channel COCO label map FPSE pools) as a row kernel: grid
-// (ceil(Wo * C / kT), B * Ho), one block row per output image row and 32-bit in-row indices —
-// the flat kernel's three 64-bit div / mod per 2-byte element left it ALU-bound at ~1.6 TB/s
-template <typename T>
-__global__ void __launch_bounds__(kT)
-avgpool_fwd_rows(const T* __restrict__ x, T* __restrict__ y, PoolGeom g) {
-  const int e = blockIdx.x * kT + threadIdx.x;
-  if (e >= g.Wo * g.C) return;
-  const int ox = e / g.C, c = e - ox * g.C;
-  const int x0 = ox * g.sw - g.pw;
-  for (int row = blockIdx.y; row < g.B * g.Ho; row += gridDim.y) {  // row = b * Ho + oy
-    const int b = row / g.Ho, oy = row - b * g.Ho;
-    const int y0 = oy * g.sh - g.ph;
-    float acc = 0.f;
-    for (int dy = 0; dy < g.kh; ++dy) {
-      const int iy = y0 + dy;
-      if (iy < 0 || iy >= g.H) continue;
-      const T* src = x + ((int64_t)b * g.H + iy) * g.W * g.C + c;
-      for (int dx = 0; dx < g.kw; ++dx) {
-        const int ix = x0 + dx;
-        if (ix < 0 || ix >= g.W) continue;
-        acc += to_f<T>(src[(int64_t)ix * g.C]);
-      }
-    }
-    y[((int64_t)row * g.Wo) * g.C + e] = from_f<T>(acc / window_count(g, oy, ox));
-  }
-}
-
 template <typename T, int V>
 __global__ void __launch_bounds__(kT)
 avgpool_bwd(const T* __restrict__ dy, T* __restrict__ dx, PoolGeom g) {
@@ -254,10 +226,8 @@ at::Tensor avg_pool_nhwc_fwd(const at::Tensor& x, int64_t kh, int64_t kw, int64_
                          reinterpret_cast<const scalar_t*>(x.data_ptr()),
                          reinterpret_cast<scalar_t*>(y.data_ptr()), g);
     else
-      hipLaunchKernelGGL((avgpool_fwd_rows<scalar_t>),
-                         dim3((unsigned)((g.Wo * g.C + kT - 1) / kT),
-                              (unsigned)std::min<int64_t>((int64_t)g.B * g.Ho, 65535)),
-                         dim3(kT), 0, stream(), reinterpret_cast<const scalar_t*>(x.data_ptr()),
+      hipLaunchKernelGGL((avgpool_fwd<scalar_t, 1>), dim3(grid_for(n)), dim3(kT), 0, stream(),
+                         reinterpret_cast<const scalar_t*>(x.data_ptr()),
                          reinterpret_cast<scalar_t*>(y.data_ptr()), g);
   });
   IAMD_LAUNCH_CHECK();
