@@ -132,12 +132,17 @@ def _pad_channels(t, c, dtype=None):
     ``pad_channels_cast`` kernel (16-byte stores of whole padded pixels, any input layout);
     differentiable inputs keep the autograd-visible slice copy."""
     dtype = dtype or t.dtype
+    one_pass = t.is_cuda and t.dim() == 4 and c % 8 == 0 and _ext.use_native(t) and \
+        t.dtype in (torch.bfloat16, torch.float32) and \
+        dtype in (torch.bfloat16, torch.float32) and \
+        not (t.requires_grad and torch.is_grad_enabled())
     if t.shape[1] == c:
+        # a cast of a non-channels-last tensor (an fp32 OIHW weight) is a cast pass plus a
+        # layout pass through PyTorch: one pad_channels_cast pass instead
+        if one_pass and t.dtype != dtype and not t.is_contiguous(memory_format=_CL):
+            return _ext.ext().pad_channels_cast(t, c, dtype)
         return nhwc(t.to(dtype))
-    if t.is_cuda and t.dim() == 4 and c % 8 == 0 and _ext.use_native(t) and \
-            t.dtype in (torch.bfloat16, torch.float32) and \
-            dtype in (torch.bfloat16, torch.float32) and \
-            not (t.requires_grad and torch.is_grad_enabled()):
+    if one_pass:
         return _ext.ext().pad_channels_cast(t, c, dtype)
     out = torch.empty((t.shape[0], c, t.shape[2], t.shape[3]), dtype=dtype, device=t.device,
                       memory_format=_CL)
