@@ -12,6 +12,7 @@ iterations run back to back first (``extra_sn_power_iteration``), so u / v advan
 in the reference and only the σ that each set is normalised by shifts by one iteration (as in
 discriminators/spade.py). ``dis.batch_real_fake: False`` restores the reference passes.
 """
+import os
 import warnings
 
 import torch
@@ -27,7 +28,9 @@ class Discriminator(nn.Module):
     def __init__(self, dis_cfg, data_cfg):
         super().__init__()
         kw = _kw(dis_cfg)
-        self.batched = bool(kw.pop('batch_real_fake', True))
+        # (IMAGINAIRE_AMD_DIS_BATCH=0: A/B switch to the reference passes)
+        self.batched = bool(kw.pop('batch_real_fake', True)) and \
+            os.environ.get('IMAGINAIRE_AMD_DIS_BATCH', '1') != '0'
         self.model = ResDiscriminator(**kw)
 
     def _passes(self, sets):
