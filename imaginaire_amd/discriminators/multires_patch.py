@@ -4,6 +4,7 @@ The strided 4×4 convolutions run bias-free on MIOpen (NHWC bf16) with the
 bias + leaky-ReLU applied by the fused HIP epilogue (k2) through Conv2dBlock.
 """
 import functools
+import os
 import warnings
 
 import numpy as np
@@ -12,6 +13,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from imaginaire_amd.layers import Conv2dBlock
+from imaginaire_amd.layers.spectral_norm import extra_sn_power_iteration
 from imaginaire_amd.utils.data import (get_paired_input_image_channel_number,
                                        get_paired_input_label_channel_number)
 from imaginaire_amd.utils.distributed import master_only_print as print
@@ -35,6 +37,11 @@ class Discriminator(nn.Module):
         activation_norm_type = getattr(dis_cfg, 'activation_norm_type', 'none')
         weight_norm_type = getattr(dis_cfg, 'weight_norm_type', 'spectral')
         num_input_channels = image_channels + num_labels
+        # D update: fake and real as ONE batch-concatenated pass (per-sample layers only; SN
+        # iterations kept: see ``forward``). IMAGINAIRE_AMD_DIS_BATCH=0: A/B switch.
+        self.batched = getattr(dis_cfg, 'batch_real_fake', True) and \
+            activation_norm_type in ('none', '', 'instance') and \
+            os.environ.get('IMAGINAIRE_AMD_DIS_BATCH', '1') != '0'
         self.model = MultiResPatchDiscriminator(num_discriminators, kernel_size,
                                                 num_input_channels, num_filters, num_layers,
                                                 max_num_filters, activation_norm_type,
@@ -52,6 +59,32 @@ class Discriminator(nn.Module):
 
     def forward(self, data, net_G_output, real=True):
         output_x = dict()
+        fake = net_G_output['fake_images']
+        if real and self.batched and fake.shape == data['images'].shape and \
+                not (torch.is_grad_enabled() and fake.requires_grad):
+            # D update (fake detached): the reference's fake and real passes as one pass over
+            # the concatenated batch; the real pass's spectral-norm power iteration runs first
+            # (u / v advance as in the reference, both halves see the second σ — see
+            # discriminators/spade.py). The G update keeps two passes: its real pass needs no
+            # backward.
+            extra_sn_power_iteration(self)
+            real_img = data['images']
+            if 'label' in data:
+                label = data['label']
+                if label.is_cuda and _ext.use_native(label):
+                    x = stack_nhwc([[label, fake], [label, real_img]])
+                else:
+                    x = torch.cat((torch.cat((label, fake.to(real_img.dtype)), 1),
+                                   torch.cat((label, real_img), 1)), 0)
+            else:
+                x = torch.cat((fake.to(real_img.dtype), real_img), 0)
+            outs, feats, _ = self.model(x)
+            n = fake.shape[0]
+            output_x['fake_outputs'] = [o[:n] for o in outs]
+            output_x['real_outputs'] = [o[n:] for o in outs]
+            output_x['fake_features'] = [[f[:n] for f in fl] for fl in feats]
+            output_x['real_features'] = [[f[n:] for f in fl] for fl in feats]
+            return output_x
         if 'label' in data:
             fake_input_x = self._input(data['label'], net_G_output['fake_images'])
         else:
