@@ -118,6 +118,7 @@ class _PerceptualNetwork(nn.Module):
         self.last_index = max(idx) if idx else len(network) - 1
         for param in self.parameters():
             param.requires_grad = False
+            param._iamd_frozen = True  # never trained: ops/conv.py caches its k10 operand
 
     def forward(self, x):
         output = {}

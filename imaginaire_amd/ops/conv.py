@@ -304,6 +304,7 @@ def _flip_t(w):
 # reused by another tensor while the entry lives.
 _WFLIP = {}
 _WFLIP_FROZEN = {}
+_FROZEN_PREP = {}  # padded k10 operands of frozen weights / biases, see _frozen_prep
 _GRAPH_KEEP = {}  # cached tensors a captured graph uses (kept for the process lifetime)
 
 
@@ -339,6 +340,26 @@ def _dgrad_weight(wb):
             _GRAPH_KEEP[id(ent[1])] = ent
         return ent[1]
     return None
+
+
+def _frozen_prep(t, tag, fn):
+    """``fn()`` — the padded / cast k10 operand made from ``t`` — cached when ``t`` is marked
+    ``_iamd_frozen`` (never trained: the VGG-19 of the perceptual loss, FlowNet2's parameters
+    and their bf16 casts), keyed on its storage and version counter, so the per-call pad / cast
+    launches of those convs happen once. Not for parameters that are merely not requiring grad
+    at the moment (a discriminator frozen for the G update): native optimizer steps change them
+    without moving the version counter. Other tensors: ``fn()`` every call."""
+    if t is None or t.requires_grad or not t.is_cuda or not getattr(t, '_iamd_frozen', False):
+        return fn()
+    key = (tag, t.data_ptr(), t._version, tuple(t.shape), t.dtype)
+    ent = _FROZEN_PREP.get(key)
+    if ent is None:
+        if len(_FROZEN_PREP) > 1024:
+            _FROZEN_PREP.clear()
+        ent = _FROZEN_PREP[key] = (t, fn())
+    if torch.cuda.is_current_stream_capturing():
+        _GRAPH_KEEP[id(ent[1])] = ent  # a captured graph reads it on every replay
+    return ent[1]
 
 
 def _pad_rows(t, n):
@@ -444,14 +465,20 @@ class _MfmaConv2d(torch.autograd.Function):
         cp, op = _round_up(cin, 64), _out_pad(cout)
         xb = _pad_channels(x, cp, torch.bfloat16)
         sig = None if sw is None else sw.sigma.reshape(1)
-        wb = _pad_rows(_pad_channels(w if sw is None else sw.shadow, cp, torch.bfloat16), op)
+        if sw is None:
+            wb = _frozen_prep(w, ('w', cp, op), lambda: _pad_rows(
+                _pad_channels(w, cp, torch.bfloat16), op))
+        else:
+            wb = _pad_rows(_pad_channels(sw.shadow, cp, torch.bfloat16), op)
         ho, wo = _out_hw(x.shape[2], x.shape[3], w.shape[2:], stride, padding, dilation)
         # Cout % 8 == 0: k10 stores only the real output channels (no crop copy after it)
         ncv = cout if (op != cout and cout % 8 == 0) else op
         ctx.res_dtype = None if res is None else res.dtype
         with _Logged('fwd', 'k10', 2.0 * x.shape[0] * ho * wo * op * cp * w.shape[2] * w.shape[3],
                      _gemm_desc(xb, wb, stride, padding) + ('' if sw is None else ' sn')):
-            y = _ext.ext().conv2d_mfma(xb, wb, _pad_rows(bias, op), stride[0], stride[1],
+            bp = None if bias is None else _frozen_prep(bias, ('b', op),
+                                                        lambda: _pad_rows(bias, op).float())
+            y = _ext.ext().conv2d_mfma(xb, wb, bp, stride[0], stride[1],
                                        padding[0], padding[1], dilation[0], dilation[1],
                                        float(slope), 1, ncv, res, sig)
         ctx.conf = (stride, padding, dilation, float(slope), cin, cout, x.dtype, w.dtype,
