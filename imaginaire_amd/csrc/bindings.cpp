@@ -143,6 +143,7 @@ at::Tensor conv_weight_flip_t(const at::Tensor& w, int64_t s, int64_t qy, int64_
                               int64_t nb);
 std::vector<at::Tensor> conv_weight_phase_flip(const at::Tensor& w, int64_t s);
 void lds_poison(int64_t blocks);
+int64_t conv_last_variant();
 at::Tensor pad_nhwc_fwd(const at::Tensor& x, int64_t pl, int64_t pr, int64_t pt, int64_t pb,
                         int64_t mode);
 at::Tensor pad_nhwc_bwd(const at::Tensor& dy, int64_t H, int64_t W, int64_t pl, int64_t pr,
@@ -238,6 +239,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "flipped, in/out-transposed channels-last conv weight (dgrad-as-conv); s/qy/qx select "
         "the taps of one stride-s phase; nb per-sample weights", py::arg("w"), py::arg("s") = 1,
         py::arg("qy") = 0, py::arg("qx") = 0, py::arg("nb") = 1);
+  m.def("conv_last_variant", &iamd::conv_last_variant,
+        "k10 tile of the last conv2d_mfma launch on this thread (1-5, 6 = row-window)");
   m.def("lds_poison", &iamd::lds_poison,
         "test support: fill every CU's LDS with NaN bits (finds reads of never-written LDS)",
         py::arg("blocks") = 2048);

@@ -24,99 +24,12 @@
 // reads bank-conflict free. Epilogue: + bias, leaky/relu slope, bf16, staged through LDS so
 // every global store is a 16-byte row segment. Block ids are XCD-remapped so the BN-tiles
 // that share one pixel tile run on the same XCD (shared L2 for the activation halo).
-#include "common.h"
+#include "conv_common.h"
 
 #include <cstdlib>
 
 namespace iamd {
 namespace {
-
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
-typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-typedef __attribute__((ext_vector_type(4))) float f32x4;
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-typedef __attribute__((address_space(3))) bf16x4* lds_bf16x4_t;
-
-constexpr int kBK = 64;
-constexpr int kRowBytes = kBK * 2;  // 128 B per staged row
-constexpr int kEpiStride = 272;     // epilogue LDS row stride in bytes (BN<=128 bf16 + 16 pad)
-
-// buffer-resource word 3 for raw (unformatted, stride-0) buffers on gfx9-family parts
-constexpr int kBufCfg = 0x00020000;
-// a byte offset past every tensor this kernel accepts (< 2^31 bytes): the buffer unit
-// returns zeros for it
-constexpr int kOobOffset = 0x7ffffff0;
-
-struct ConvArgs {
-  const __hip_bfloat16* x;
-  const __hip_bfloat16* w;
-  const float* bias;
-  __hip_bfloat16* y;
-  int xbytes, wbytes;
-  int H, W, Cin, Ho, Wo, Cout;
-  int KH, KW, sh, sw, ph, pw, dh, dw;
-  int M, nk, cpt, nNt;
-  int kps;          // k-steps per split (split-K: blockIdx.y = split)
-  float* part;      // split-K fp32 partial slabs [S][M][Cout] (nullptr: direct epilogue)
-  float slope;
-  // output-pixel mapping (phase-decomposed stride-2 data gradient): GEMM row m = (b, oh, ow)
-  // is stored at pixel (b, oh * osy + ory, ow * osx + orx) of a [B, oH, oW, Cout] tensor.
-  // omode 0: identity (row m is pixel m)
-  int omode, oH, oW, osy, osx, ory, orx;
-  // batch of independent convs (per-sample weights: the fs-vid2vid hyper convolutions), one per
-  // blockIdx.z: operand / output / bias strides in elements between samples (v1 kernel only)
-  int64_t xbs, wbs, ybs;
-  int bbs, nz;
-  // channels stored per output pixel = row stride of y (<= Cout, a multiple of 8): the padded
-  // output channels of a Cout % 64 != 0 conv are never written, so no crop copy follows
-  int ldy;
-  // residual added after the activation, same layout as y (nullptr: none): the shortcut of a
-  // residual block whose branch ends in this conv (reference layers/residual.py:150
-  // ``x_shortcut + dx``) lands in the epilogue instead of a separate full-tensor add
-  const __hip_bfloat16* res;
-  // spectrally normalised weight (layers/spectral_norm.py): the operand w is bf16(W) and the
-  // epilogue scales the accumulator by 1 / *ascale (sigma, a device scalar written by the power
-  // iteration in the same graph) before the bias: conv(x, W / sigma) without a W / sigma copy.
-  // nullptr: no scale.
-  const float* ascale = nullptr;
-};
-
-__device__ __forceinline__ float ascale_of(const ConvArgs& a) {
-  return a.ascale ? 1.f / a.ascale[0] : 1.f;
-}
-
-// y[off .. off + 8) = v (+ res[off .. off + 8) when the conv carries a residual), one 16-byte
-// store. The residual is added to the bf16-rounded conv output and rounded again: the same
-// two roundings as the unfused bf16 conv followed by a bf16 add.
-__device__ __forceinline__ void store_chunk(const ConvArgs& a, __hip_bfloat16* y, size_t off,
-                                            uint4 v) {
-  if (a.res) {
-    const uint4 r = *reinterpret_cast<const uint4*>(a.res + off);
-    const uint32_t* pv = reinterpret_cast<const uint32_t*>(&v);
-    const uint32_t* pr = reinterpret_cast<const uint32_t*>(&r);
-    uint4 o;
-    uint32_t* po = reinterpret_cast<uint32_t*>(&o);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float lo = __uint_as_float(pv[k] << 16) + __uint_as_float(pr[k] << 16);
-      const float hi = __uint_as_float(pv[k] & 0xffff0000u) + __uint_as_float(pr[k] & 0xffff0000u);
-      const __hip_bfloat16 blo = __float2bfloat16(lo), bhi = __float2bfloat16(hi);
-      po[k] = (uint32_t)(*reinterpret_cast<const uint16_t*>(&blo)) |
-              ((uint32_t)(*reinterpret_cast<const uint16_t*>(&bhi)) << 16);
-    }
-    v = o;
-  }
-  *reinterpret_cast<uint4*>(y + off) = v;
-}
-
-// destination pixel (row of the NHWC output) of GEMM row m
-__device__ __forceinline__ size_t out_row(const ConvArgs& a, int m) {
-  if (!a.omode) return (size_t)m;
-  const int HoWo = a.Ho * a.Wo;
-  const int b = m / HoWo, r = m - b * HoWo;
-  const int oh = r / a.Wo, ow = r - oh * a.Wo;
-  return ((size_t)b * a.oH + oh * a.osy + a.ory) * a.oW + ow * a.osx + a.orx;
-}
 
 // BM = 128 (4 waves, 2 blocks/CU) or 256 (8 waves, 1 block/CU: the B tile is shared by twice
 // the pixels, 25% fewer L2->LDS bytes per MFMA); waves form a (BM/64) x 2 grid.
@@ -1384,46 +1297,6 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_mfma_v5(ConvArgs a) {
 #endif  // __HIP_DEVICE_COMPILE__
 }
 
-// y = act(sum_s part[s] + bias) in bf16, 8 channels per thread.
-__global__ void __launch_bounds__(256)
-conv_splitk_reduce(const float* __restrict__ part, const float* __restrict__ bias,
-                   __hip_bfloat16* __restrict__ y, int S, int64_t MC, int C, float slope,
-                   ConvArgs map) {
-  const float asc = ascale_of(map);
-  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < MC / 8;
-       v += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t e = v * 8;
-    float acc[8];
-    const float4* p = reinterpret_cast<const float4*>(part + e);
-    float4 lo = p[0], hi = p[1];
-    acc[0] = lo.x; acc[1] = lo.y; acc[2] = lo.z; acc[3] = lo.w;
-    acc[4] = hi.x; acc[5] = hi.y; acc[6] = hi.z; acc[7] = hi.w;
-    for (int s = 1; s < S; ++s) {
-      const float4* q = reinterpret_cast<const float4*>(part + (int64_t)s * MC + e);
-      lo = q[0]; hi = q[1];
-      acc[0] += lo.x; acc[1] += lo.y; acc[2] += lo.z; acc[3] += lo.w;
-      acc[4] += hi.x; acc[5] += hi.y; acc[6] += hi.z; acc[7] += hi.w;
-    }
-    const int c = (int)(e % C);
-    if (c >= map.ldy) continue;  // padded output channels are not stored
-    const int zb = (int)(e / ((int64_t)map.M * C));  // sample of a batched launch
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float t = fmaf(acc[k], asc, bias ? bias[zb * map.bbs + c + k] : 0.f);
-      acc[k] = t > 0.f ? t : t * slope;
-    }
-    const int64_t m = e / C - (int64_t)zb * map.M;
-    const size_t off = (size_t)zb * map.ybs + out_row(map, (int)m) * map.ldy + c;
-    if (map.res) {  // (bf16 conv output + residual, as store_chunk)
-      float r[8];
-      load_vec<__hip_bfloat16, 8>(map.res + off, r);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] = __bfloat162float(__float2bfloat16(acc[k])) + r[k];
-    }
-    store_vec<__hip_bfloat16, 8>(y + off, acc);
-  }
-}
-
 }  // namespace
 
 namespace {
@@ -1555,6 +1428,15 @@ void run_v5(ConvArgs& a, const at::Tensor& x) {
   IAMD_LAUNCH_CHECK();
 }
 
+}  // namespace
+
+// The k10 tile of the most recent conv2d_mfma launch on this host thread (1 = v1, 2, 3, 4, 5,
+// 6 = row-window): read by the per-call conv log (ops/conv.py) and the tests.
+thread_local int g_last_conv_variant = 0;
+int64_t conv_last_variant() { return g_last_conv_variant; }
+
+namespace {
+
 // Kernel choice, split-K and launch for a filled-in ConvArgs (x supplies the tensor options of
 // the split-K slabs).
 void run_conv(ConvArgs& a, const at::Tensor& x) {
@@ -1582,15 +1464,25 @@ void run_conv(ConvArgs& a, const at::Tensor& x) {
     return ceil_div(a.nk, ceil_div(a.nk, S));
   };
   if ((ver == 0 && v5_eligible(a)) || (ver == 5 && v5_shape_ok(a))) {
+    g_last_conv_variant = 5;
     run_v5(a, x);
     return;
   }
   if ((ver == 4 || ver == 0) && v4_eligible(a)) {
     // default: every eligible conv (1.02-1.52x v1 and 1.0-1.08x v3 on the SPADE-step shapes,
     // the N = 128 data gradients 1.36-1.52x: profiles/conv_v4_probe_mi355x.txt)
+    g_last_conv_variant = 4;
     run_v4(a, x, false);
     return;
   }
+  // the generalised row-window tile (conv_rw.hip): stride 2, 1x1 / 4x4 / 7x7, Cout = 64,
+  // Cin = 32, any output width
+  if ((ver == 0 || ver == 6) && run_rw(a, x)) {
+    g_last_conv_variant = 6;
+    return;
+  }
+  IAMD_CHECK(a.Cin % kBK == 0, "conv2d_mfma: Cin = ", a.Cin, " runs on the row-window tile "
+             "only, which does not take this shape");
   bool v3 = false, v2 = false;
   if (ver == 3) {
     v3 = v3_ok;
@@ -1605,6 +1497,7 @@ void run_conv(ConvArgs& a, const at::Tensor& x) {
     const int64_t t3 = (int64_t)ceil_div(a.M, v3_bm) * (Cout / v3_bn);
     v3 = split_for(t3, 256) == 1 && a.nk >= 40;
   }
+  g_last_conv_variant = v3 ? 3 : v2 ? 2 : 1;
   int bm = 128;
   if (v3) {
     bm = v3_bm;
@@ -1718,7 +1611,8 @@ at::Tensor conv2d_mfma(const at::Tensor& x, const at::Tensor& w, const c10::opti
              "conv2d_mfma: per-sample weights need x batch == nb and w rows % nb == 0");
   const int Cout = (int)(w.size(0) / nb), KH = (int)w.size(2), KW = (int)w.size(3);
   IAMD_CHECK(w.size(1) == Cin, "conv2d_mfma: channel mismatch ", w.size(1), " vs ", Cin);
-  IAMD_CHECK(Cin % kBK == 0, "conv2d_mfma: Cin must be a multiple of 64, got ", Cin);
+  IAMD_CHECK(Cin % kBK == 0 || Cin == 32,
+             "conv2d_mfma: Cin must be a multiple of 64 (or 32: row-window tile), got ", Cin);
   IAMD_CHECK(Cout % 64 == 0, "conv2d_mfma: Cout must be a multiple of 64, got ", Cout);
   IAMD_CHECK(sh >= 1 && sw >= 1 && dh >= 1 && dw >= 1 && ph >= 0 && pw >= 0, "conv2d_mfma: bad geometry");
   const int Ho = (int)((H + 2 * ph - dh * (KH - 1) - 1) / sh + 1);
@@ -1923,6 +1817,7 @@ at::Tensor conv2d_dgrad_strided(const at::Tensor& dy, const at::Tensor& w, int64
     }
   }
   if (zero_fill) dx.zero_();
+  g_last_conv_variant = 7;  // (v1 phase tiles)
   // up to four phases per launch (the ConvPhases kernel argument; s = 3, 4 take several)
   for (size_t p0 = 0; p0 < phases.size(); p0 += 4) {
     ConvPhases P;

@@ -67,6 +67,8 @@ class _Logged(object):
     def __exit__(self, *exc):
         if self.rec is not None:
             self.rec[5].record()
+            if self.rec[1].startswith('k10'):  # which k10 tile ran (csrc conv_last_variant)
+                self.rec[1] += '/v%d' % _ext.ext().conv_last_variant()
             _CONV_LOG.append(self.rec)
         return False
 
@@ -596,6 +598,8 @@ class _MfmaConv2d(torch.autograd.Function):
             if dw.shape[0] != cout or dw.shape[1] != cin:
                 dw = dw[:cout, :cin]
             dw = dw.to(wdt)
+            if _TEST_FLIP_WGRAD[0]:
+                dw = _test_flip_wgrad(dw)
         if slope == 1.0 and need_b and not side_bias:
             # identity activation: bias gradient only (the k2 kernel reads dy, writes no dx),
             # after the data and weight gradients
@@ -610,6 +614,17 @@ class _MfmaConv2d(torch.autograd.Function):
         if ctx.res_dtype is not None and ctx.needs_input_grad[7]:
             dres = dy_in if dy_in.dtype == ctx.res_dtype else dy_in.to(ctx.res_dtype)
         return dx, dw, db, None, None, None, None, dres, None
+
+
+# Negative control of the model-parity gate (tests/test_model_parity_gpu.py): with
+# ``_TEST_FLIP_WGRAD = [k, 0]`` (or IMAGINAIRE_AMD_TEST_FLIP_WGRAD=k at import) the k-th k10/k11
+# conv weight gradient computed from then on is returned negated. Test use only.
+_TEST_FLIP_WGRAD = [int(os.environ.get('IMAGINAIRE_AMD_TEST_FLIP_WGRAD', '0')), 0]
+
+
+def _test_flip_wgrad(dw):
+    _TEST_FLIP_WGRAD[1] += 1
+    return -dw if _TEST_FLIP_WGRAD[1] == _TEST_FLIP_WGRAD[0] else dw
 
 
 class SNWeight(object):

@@ -18,9 +18,11 @@ iteration is captured ONCE into a hipGraph (``torch.cuda.graph``) and replayed:
 Multi-rank steps are captured too (the default since round 4), with their collectives: the
 DDP bucket all-reduces and sync-BN exchanges run on the native RCCL communicator
 (parallel/rccl.py: no torch Work objects for the watchdog to poll) and DDP uses its rank-local
-unused-parameter mask (no host sync in ``finish()``), which holds for the trainers that declare
-``rank_uniform_control_flow``. The others (the vid2vid family: data-dependent hand
-discriminator) keep the eager step at world > 1. Capture is rank-local (nothing executes while
+unused-parameter mask (no host sync in ``finish()``), which holds for the trainers whose
+``rank_uniform(cfg)`` is true: SPADE, pix2pixHD, MUNIT / UNIT, FUNIT, and the vid2vid family
+unless its config adds the data-dependent hand / face discriminators
+(trainers/vid2vid.py ``rank_uniform``); those keep the eager step at world > 1. Capture is
+rank-local (nothing executes while
 recording), so the ranks agree on its outcome afterwards: one all-reduce of a success flag and a
 batch-signature hash; if any rank failed, every rank runs eagerly. Both paths run the same
 kernels: the eager step also runs under :class:`graph_routing`. Batch structures must be
@@ -187,6 +189,26 @@ class graph_routing(object):
 _WARNED = [False]
 
 
+def packet_capture_refusal():
+    """None when graphs may be captured, else the reason they may not: the HIP runtime's graph
+    packet-capture mode is (or may be) on in this process (imaginaire_amd/__init__.py
+    ``PACKET_CAPTURE_STATE``). ``IMAGINAIRE_AMD_GRAPH_ALLOW_PACKET_CAPTURE=1`` captures anyway
+    (probes that compare the two modes)."""
+    import imaginaire_amd
+    state = getattr(imaginaire_amd, 'PACKET_CAPTURE_STATE', 'off')
+    if state == 'off' or os.environ.get('IMAGINAIRE_AMD_GRAPH_ALLOW_PACKET_CAPTURE') == '1':
+        return None
+    if state == 'unknown':
+        return ('HIP was initialised before imaginaire_amd was imported, with '
+                'DEBUG_CLR_GRAPH_PACKET_CAPTURE unset, so the runtime\'s packet-capture mode is '
+                'on (replays of long graphs have read stale operands in that mode); import '
+                'imaginaire_amd before using torch.cuda, or export '
+                'DEBUG_CLR_GRAPH_PACKET_CAPTURE=0')
+    return ('DEBUG_CLR_GRAPH_PACKET_CAPTURE=%s: packet-capture mode is on (replays of long '
+            'graphs have read stale operands in that mode)' %
+            os.environ.get('DEBUG_CLR_GRAPH_PACKET_CAPTURE'))
+
+
 class GraphedStep(object):
     """Runs ``step_fn(data)`` eagerly for ``warmup`` iterations (on a side stream, as
     stream capture requires), then captures it and replays the graph from then on.
@@ -276,17 +298,23 @@ class GraphedStep(object):
 
     def _capture_and_run(self, ent, data):
         from imaginaire_amd.ops import _ext
-        if os.environ.get('DEBUG_CLR_GRAPH_PACKET_CAPTURE', '0') != '0' and not _WARNED[0]:
-            _WARNED[0] = True
-            print('[graph] warning: DEBUG_CLR_GRAPH_PACKET_CAPTURE=%s — long captured steps have '
-                  'replayed with stale operands in this mode (imaginaire_amd/__init__.py)' %
-                  os.environ['DEBUG_CLR_GRAPH_PACKET_CAPTURE'])
+        refuse = packet_capture_refusal()
+        if refuse is not None:
+            if not _WARNED[0]:
+                _WARNED[0] = True
+                print('[graph] not capturing {}: {}; running eagerly'.format(self.name, refuse))
+            self.failed = True
+            ent['static'] = None
+            return self.step_fn(data)
         torch.cuda.synchronize()
         t0 = time.time()
         # private copies: the batch source may hand out views of its own pool
         ent['static'] = _clone(data)
         saved = self.save_host() if self.save_host else None
-        g = torch.cuda.CUDAGraph()
+        dot = os.environ.get('IMAGINAIRE_AMD_GRAPH_DOT')
+        # (the DOT dump needs the captured hipGraph_t, which is freed at instantiation unless
+        # the graph is kept)
+        g = torch.cuda.CUDAGraph(keep_graph=True) if dot else torch.cuda.CUDAGraph()
         err = None
         try:
             st = self._side_stream()
@@ -295,9 +323,13 @@ class GraphedStep(object):
             # thread-local capture mode: the RCCL process group's watchdog thread keeps polling
             # its work events while a (seconds-long) step is being captured; under the default
             # global mode those calls from another thread are refused and abort the process
+            if dot:  # hipGraphDebugDotPrint of the captured graph (scripts/probe/graph_dot.py)
+                g.enable_debug_mode()
             with torch.cuda.graph(g, pool=ent['pool'], stream=st,
                                   capture_error_mode='thread_local'), graph_routing():
                 self.step_fn(ent['static'])
+            if dot:
+                g.debug_dump(dot)
         except Exception as e:  # noqa: BLE001 - any capture failure: stay eager
             if os.environ.get('IMAGINAIRE_AMD_GRAPH_DEBUG'):
                 raise

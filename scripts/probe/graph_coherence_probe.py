@@ -24,9 +24,17 @@ reps = int(sys.argv[3]) if len(sys.argv) > 3 else 5
 hop = 16
 # MODE=kernel: the hop is two multiply kernels; MODE=copy: two device-to-device copies
 # (copy_ of same-dtype contiguous tensors: memcpy nodes in the graph, not kernels)
+# MODE=hip: the hop is one of the framework's HIP kernels (pad_channels_cast: a fp32 NCHW ->
+# NHWC pass, every element equal so the layout change is value-preserving) and a copy back
 mode = os.environ.get('MODE', 'kernel')
 a = torch.zeros(size, device='cuda')
 b = torch.zeros(size, device='cuda')
+if mode == 'hip':
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+    os.environ.setdefault('IMAGINAIRE_AMD_GRAPH_ALLOW_PACKET_CAPTURE', '1')
+    from imaginaire_amd.ops import _ext  # noqa: E402
+    X = _ext.ext()
+    a4 = a.view(1, size // 64, 8, 8)
 
 
 def body():
@@ -35,6 +43,9 @@ def body():
             if mode == 'copy':
                 b.copy_(a)
                 a.copy_(b)
+            elif mode == 'hip':
+                t = X.pad_channels_cast(a4, size // 64, torch.float32)
+                a4.copy_(t)
             else:
                 torch.mul(a, 2.0, out=b)
                 torch.mul(b, 0.5, out=a)

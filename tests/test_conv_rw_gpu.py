@@ -1,0 +1,139 @@
+"""The row-window k10 tile (csrc/conv_rw.hip) against fp32 PyTorch convolutions.
+
+Shapes cover every mode of the tile: stride 1 / 2 (the de-interleaved stride-2 window), filter
+widths 1 / 3 / 4 / 5 / 7, BN = 64 / 128, Cin = 32 (two filter taps per 64-deep k-chunk, odd KW
+with a zero half tap) and Cin multiples of 64, output widths that do not tile the 256 / 128
+pixel block (masked virtual pixels: 5, 47, 100, 260), split-K, the residual / 1 / sigma
+epilogue and the LDS-poison determinism check. Reference: the convolutions of
+/root/reference/imaginaire/layers/conv.py:59-91 (cuDNN there)."""
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+CL = torch.channels_last
+
+# B, Cin, Cout, H, W, KH, KW, stride, pad
+RW_CASES = [
+    (2, 64, 64, 32, 64, 3, 3, 1, 1),       # BN 64, stride 1
+    (2, 64, 128, 33, 47, 4, 4, 2, 1),      # 4x4 s2 (PatchGAN), odd sizes: Wo 24
+    (2, 64, 128, 31, 33, 3, 3, 2, 1),      # 3x3 s2
+    (1, 128, 128, 16, 100, 7, 7, 1, 3),    # 7x7, Wo 100 of a 128-pixel segment
+    (2, 64, 64, 20, 30, 1, 1, 1, 0),       # 1x1
+    (2, 128, 64, 17, 9, 1, 1, 2, 0),       # 1x1 s2
+    (1, 64, 128, 13, 260, 3, 3, 1, 1),     # Wo 260: two 256-pixel segments per row
+    (2, 192, 128, 16, 32, 4, 4, 2, 1),     # three channel blocks per filter row
+    (1, 64, 64, 9, 9, 3, 3, 2, 1),         # Wo 5: 16-pixel segments
+    (2, 256, 256, 8, 8, 3, 3, 1, 1),       # 8x8 map (split-K)
+    (1, 64, 128, 12, 40, 5, 3, 1, 2),      # KH != KW
+    (1, 64, 64, 20, 40, 7, 7, 2, 3),       # 7x7 s2
+    (1, 64, 64, 19, 37, 5, 5, 2, 2),       # 5x5 s2
+    (1, 32, 64, 24, 40, 3, 3, 1, 1),       # Cin 32: virtual taps (0, 1), (2, zero)
+    (1, 32, 128, 20, 36, 4, 4, 2, 1),      # Cin 32, 4x4 s2
+    (1, 32, 64, 16, 30, 7, 7, 1, 3),       # Cin 32, 7x7
+    (1, 32, 64, 16, 16, 1, 1, 1, 0),       # Cin 32, 1x1 (one half-zero tap)
+    (1, 32, 64, 15, 21, 5, 5, 2, 2),       # Cin 32, 5x5 s2
+    (2, 32, 64, 64, 128, 3, 3, 1, 1),      # Cin 32 at a 128-wide row
+]
+
+
+def _inputs(case, seed=5):
+    B, cin, cout, H, W, kh, kw, s, p = case
+    torch.manual_seed(seed)
+    x = torch.randn(B, cin, H, W, device='cuda').to(torch.bfloat16).contiguous(memory_format=CL)
+    # asymmetric weights: catches row / column swaps in the fragment maps
+    w = (torch.randn(cout, cin, kh, kw, device='cuda') / (cin * kh * kw) ** 0.5 +
+         torch.arange(cout, device='cuda').view(-1, 1, 1, 1) * 1e-3)
+    w = w.to(torch.bfloat16).contiguous(memory_format=CL)
+    b = torch.randn(cout, device='cuda') * 0.1
+    return x, w, b
+
+
+def _run(X, x, w, b, s, p, slope=0.2, res=None, asc=None, ver='6', splitk=None):
+    os.environ['IMAGINAIRE_AMD_CONV_V'] = ver
+    if splitk:
+        os.environ['IMAGINAIRE_AMD_CONV_SPLITK'] = splitk
+    try:
+        y = X.conv2d_mfma(x, w, b, s, s, p, p, 1, 1, slope, 1, -1, res, asc)
+        var = X.conv_last_variant()
+    finally:
+        os.environ.pop('IMAGINAIRE_AMD_CONV_V')
+        os.environ.pop('IMAGINAIRE_AMD_CONV_SPLITK', None)
+    return y, var
+
+
+@pytest.mark.parametrize('case', RW_CASES)
+def test_rw_forward_matches_fp32(case):
+    from imaginaire_amd.ops import _ext
+    X = _ext.ext()
+    B, cin, cout, H, W, kh, kw, s, p = case
+    x, w, b = _inputs(case)
+    y, var = _run(X, x, w, b, s, p)
+    assert var == 6, 'the row-window tile did not take %s (variant %d)' % (case, var)
+    ref = F.leaky_relu(F.conv2d(x.float(), w.float(), b, s, p), 0.2)
+    assert y.shape == ref.shape
+    err = (y.float() - ref).abs().max().item()
+    assert err <= 1e-2 * max(1.0, ref.abs().max().item()), err
+
+
+@pytest.mark.parametrize('case', [RW_CASES[1], RW_CASES[3], RW_CASES[13], RW_CASES[14]])
+@pytest.mark.parametrize('splitk', ['2', '3'])
+def test_rw_splitk_matches(case, splitk):
+    from imaginaire_amd.ops import _ext
+    X = _ext.ext()
+    x, w, b = _inputs(case, seed=6)
+    s, p = case[7], case[8]
+    y1, _ = _run(X, x, w, b, s, p)
+    y2, var = _run(X, x, w, b, s, p, splitk=splitk)
+    assert var == 6
+    ref = F.leaky_relu(F.conv2d(x.float(), w.float(), b, s, p), 0.2)
+    for y in (y1, y2):
+        err = (y.float() - ref).abs().max().item()
+        assert err <= 1e-2 * max(1.0, ref.abs().max().item()), err
+
+
+@pytest.mark.parametrize('case', [RW_CASES[0], RW_CASES[1], RW_CASES[14]])
+def test_rw_residual_and_sigma_epilogue(case):
+    """y = act(conv(x, W) / sigma + b) + res, the residual added after the activation."""
+    from imaginaire_amd.ops import _ext
+    X = _ext.ext()
+    x, w, b = _inputs(case, seed=7)
+    s, p = case[7], case[8]
+    ref = F.conv2d(x.float(), w.float(), None, s, p)
+    res = torch.randn(ref.shape, device='cuda').to(torch.bfloat16).contiguous(memory_format=CL)
+    sig = torch.tensor([1.7], device='cuda')
+    y, var = _run(X, x, w, b, s, p, res=res, asc=sig)
+    assert var == 6
+    ref = F.leaky_relu(ref / 1.7 + b.view(1, -1, 1, 1), 0.2) + res.float()
+    err = (y.float() - ref).abs().max().item()
+    assert err <= 1.5e-2 * max(1.0, ref.abs().max().item()), err
+
+
+@pytest.mark.parametrize('case', [RW_CASES[0], RW_CASES[1], RW_CASES[3], RW_CASES[14],
+                                  RW_CASES[9]])
+def test_rw_never_reads_unwritten_lds(case):
+    """Bitwise the same output after the LDS of every CU was filled with NaN bits."""
+    from imaginaire_amd.ops import _ext
+    X = _ext.ext()
+    x, w, b = _inputs(case, seed=8)
+    s, p = case[7], case[8]
+    y0, _ = _run(X, x, w, b, s, p)
+    X.lds_poison()
+    y1, var = _run(X, x, w, b, s, p)
+    torch.cuda.synchronize()
+    assert var == 6
+    assert torch.isfinite(y1.float()).all()
+    assert torch.equal(y0, y1)
+
+
+def test_rw_taken_by_default_for_v1_shapes():
+    """Without a forced variant, the shapes v4 / v5 do not take run on the row-window tile."""
+    from imaginaire_amd.ops import _ext
+    X = _ext.ext()
+    for case in (RW_CASES[1], RW_CASES[4], RW_CASES[13]):
+        x, w, b = _inputs(case)
+        _, var = _run(X, x, w, b, case[7], case[8], ver='0')
+        assert var == 6, (case, var)
