@@ -143,6 +143,9 @@ at::Tensor conv_weight_flip_t(const at::Tensor& w, int64_t s, int64_t qy, int64_
                               int64_t nb);
 std::vector<at::Tensor> conv_weight_phase_flip(const at::Tensor& w, int64_t s);
 void lds_poison(int64_t blocks);
+at::Tensor im2col_pack(const at::Tensor& x, int64_t KH, int64_t KW, int64_t sh, int64_t sw,
+                       int64_t ph, int64_t pw, int64_t dh, int64_t dw, int64_t Kp);
+
 int64_t conv_last_variant();
 at::Tensor pad_nhwc_fwd(const at::Tensor& x, int64_t pl, int64_t pr, int64_t pt, int64_t pb,
                         int64_t mode);
@@ -241,6 +244,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("qy") = 0, py::arg("qx") = 0, py::arg("nb") = 1);
   m.def("conv_last_variant", &iamd::conv_last_variant,
         "k10 tile of the last conv2d_mfma launch on this thread (1-5, 6 = row-window)");
+  m.def("im2col_pack", &iamd::im2col_pack,
+        "tap-packed [M][Kp] operand of a thin-input (Cin <= 16) conv (bf16, channels-last)");
   m.def("lds_poison", &iamd::lds_poison,
         "test support: fill every CU's LDS with NaN bits (finds reads of never-written LDS)",
         py::arg("blocks") = 2048);

@@ -147,6 +147,6 @@ conv_splitk_reduce(const float* __restrict__ part, const float* __restrict__ bia
 // Row-window k10 for the shapes the v4 / v5 tiles do not take (stride 2, 1x1 / 4x4 / 7x7
 // filters, Cout = 64, Cin = 32, output rows of any width): conv_rw.hip. Launches and returns
 // true when the shape is eligible (IMAGINAIRE_AMD_CONV_RW != 0), else launches nothing.
-bool run_rw(ConvArgs& a, const at::Tensor& x);
+bool run_rw(ConvArgs& a, const at::Tensor& x, bool forced);
 bool rw_eligible(const ConvArgs& a);
 }  // namespace iamd

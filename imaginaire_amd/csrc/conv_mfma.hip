@@ -1477,7 +1477,16 @@ void run_conv(ConvArgs& a, const at::Tensor& x) {
   }
   // the generalised row-window tile (conv_rw.hip): stride 2, 1x1 / 4x4 / 7x7, Cout = 64,
   // Cin = 32, any output width
-  if ((ver == 0 || ver == 6) && run_rw(a, x)) {
+  // Default routing (ver 0): the row-window tile where it measured faster than v1 — long
+  // filter rows (K = KH*KW*Cin >= 2048 at stride 1: 1.09-1.20x on the 7x7 / 5x5 64-128-channel
+  // stems and decoders; >= 6144 at stride 2: 1.18x on the 512-channel PatchGAN layers) — and
+  // Cin = 32, which v1 cannot take. Short filters stay on v1: its two co-resident 128-pixel
+  // blocks overlap one tile's loads with the other's epilogue, and those convs are latency /
+  // bandwidth bound (0.55-0.86x, profiles/conv_rw_probe_mi355x.txt).
+  const int64_t kfull = (int64_t)KH * KW * a.Cin;
+  const bool rw_pref = a.Cin == 32 ||
+                       (a.KW >= 3 && ((a.sh == 1 && kfull >= 2048) || (a.sh == 2 && kfull >= 6144)));
+  if ((ver == 6 || (ver == 0 && rw_pref)) && run_rw(a, x, ver == 6 || a.Cin == 32)) {
     g_last_conv_variant = 6;
     return;
   }

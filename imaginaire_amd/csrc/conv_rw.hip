@@ -343,8 +343,12 @@ int pow2ceil(int v) {
   return p;
 }
 
-// Fill in the row-window geometry; false if the shape does not fit the tile.
-bool rw_plan(ConvArgs& a) {
+// Fill in the row-window geometry; false if the shape does not fit the tile. The segment width
+// SW is the largest power of two whose masked tail wastes at most 10% of the virtual pixels
+// (else the least wasteful one); with min_eff > 0 a shape wasting more than 1 - min_eff of its
+// pixels is refused (default routing: a 66- or 262-wide output on 128 / 256-pixel segments ran
+// at half the useful rate of the v1 tile).
+bool rw_plan(ConvArgs& a, double min_eff = 0.0) {
   if (a.nz != 1 || a.dh != 1 || a.dw != 1 || a.sh != a.sw || (a.sh != 1 && a.sh != 2))
     return false;
   if (a.Cout % 64 != 0 || a.KH > 31 || a.KH < 1 || a.KW < 1) return false;
@@ -355,7 +359,21 @@ bool rw_plan(ConvArgs& a) {
   if (pair ? (kwv > 4) : (a.KW != 1 && a.KW != 3 && a.KW != 4 && a.KW != 5 && a.KW != 7))
     return false;
   const int BM = S == 1 ? 256 : 128;
-  int SW = std::min(BM, std::max(S == 1 ? 32 : 16, pow2ceil(a.Wo)));
+  int SW = 0;
+  double best = -1.0;
+  for (int sw = BM; sw >= (S == 1 ? 32 : 16); sw >>= 1) {
+    const double eff = (double)a.Wo / ((double)ceil_div(a.Wo, sw) * sw);
+    if (eff >= 0.9 - 1e-9) {
+      SW = sw;
+      best = eff;
+      break;
+    }
+    if (eff > best + 1e-9) {
+      best = eff;
+      SW = sw;
+    }
+  }
+  if (best < min_eff) return false;
   int P, Ph = 0;
   if (S == 2 && !pair) {
     Ph = SW + 4;  // >= SW + (KW - 1) / 2 even columns
@@ -425,8 +443,8 @@ bool rw_eligible(const ConvArgs& a) {
   return rw_plan(t);
 }
 
-bool run_rw(ConvArgs& a, const at::Tensor& x) {
-  if (rw_disabled() || !rw_plan(a)) return false;
+bool run_rw(ConvArgs& a, const at::Tensor& x, bool forced) {
+  if (rw_disabled() || !rw_plan(a, forced ? 0.0 : 0.85)) return false;
   const int BM = a.sh == 1 ? 256 : 128;
   const int R = BM / a.SW;
   const int BN = a.Cout % 128 == 0 ? 128 : 64;

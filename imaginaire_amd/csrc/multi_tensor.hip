@@ -562,14 +562,14 @@ at::Tensor mt_sn_sigma(const std::vector<at::Tensor>& weights, const std::vector
   std::vector<at::Tensor> vms;
   {
     std::lock_guard<std::mutex> lk(ws_mu);
-    at::Tensor& ws = ws_map[weights[0].get_device()];
+    const int dev = weights[0].get_device();
+    at::Tensor& ws = ws_map[dev];
     if (!ws.defined() || ws.numel() < total) {
-      // the old workspace may be named by a captured graph: never free it
-      static std::vector<at::Tensor> retired;
-      if (ws.defined()) retired.push_back(ws);
+      // an old workspace that a captured graph names is never freed (kept by keep_for_graph);
+      // one only ever used eagerly is released with its last reference
       ws = at::empty({total}, weights[0].options());
     }
-    keep_for_graph(ws);
+    keep_for_graph(ws);  // (no-op outside a capture)
     int64_t off = 0;
     for (auto& w : weights) {
       const int64_t cols = w.numel() / std::max<int64_t>(1, w.size(0));

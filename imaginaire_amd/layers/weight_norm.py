@@ -49,6 +49,10 @@ def get_weight(module, ref=False):
         if ref and hasattr(hook, 'weight_ref'):
             r = hook.weight_ref(module)
             if r is not None:
+                # module.weight must not keep a stale tensor (torch's spectral_norm leaves the
+                # forward's W / sigma there): it holds the unmaterialised reference, whose
+                # .materialize() gives bf16(W / sigma)
+                setattr(module, hook.name, r)
                 return r
         w = hook.compute_weight(module, do_power_iteration=module.training)
         setattr(module, hook.name, w)

@@ -525,16 +525,28 @@ class _MfmaConv2d(torch.autograd.Function):
         dy = _pad_channels(dy, wb.shape[0], torch.bfloat16)
         dx = dw = None
         cap = _capturing()
+        kh, kw = wb.shape[2], wb.shape[3]
+        if cout <= 16 and stride == (1, 1) and dilation == (1, 1) and sn is None and \
+                _TAPPACK and kh * kw > 1 and kh * kw * cout <= 512 and \
+                0 <= padding[0] < kh and 0 <= padding[1] < kw and (need_x or need_w):
+            # thin OUTPUT (the RGB heads): both gradients from ONE tap-packed operand of dy,
+            # dycol[q][(t', co)] = dy[q + t' - (K - 1 - pad)] (t' = flipped tap): dx is the 1x1
+            # GEMM of dycol with the flipped weight, dW the 1x1 k11 GEMM of (dycol, x) — no
+            # 64-channel padding of dy, no KH*KW x 64 implicit-GEMM k loop over zero channels
+            dx, dw = _thin_output_grads(dy[:, :cout], xb, wb, padding, cout, cin, xc, need_x,
+                                        need_w, wdt)
+            need_x_left, need_w_left = False, False
+        else:
+            need_x_left, need_w_left = need_x, need_w
         if side is not None:
             main = torch.cuda.current_stream()
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 if side_bias:  # bias gradient only: the k2 kernel reads dy, writes no dx
                     db = _ext.ext().bias_act_bwd(dy, dy, 1.0)[1]
-                if need_w and _OVERLAP_BWD == '1':
+                if need_w_left and _OVERLAP_BWD == '1':
                     dw = _wgrad(dy, xb, wb, stride, padding, dilation, cout, cin, wdt, sn)
-        if need_x:
-            kh, kw = wb.shape[2], wb.shape[3]
+        if need_x_left:
             pt = (dilation[0] * (kh - 1) - padding[0], dilation[1] * (kw - 1) - padding[1])
             cp = wb.shape[1]
             dblocks = -(-dy.shape[0] * xb.shape[2] * xb.shape[3] // 128) * \
@@ -587,6 +599,10 @@ class _MfmaConv2d(torch.autograd.Function):
             if dx.shape[1] != xc:
                 dx = dx[:, :xc]
             dx = dx.to(xdt)
+        elif dx is not None:  # (thin-output path)
+            if dx.shape[1] != xc:
+                dx = dx[:, :xc]
+            dx = dx.to(xdt)
         if side is not None:
             main.wait_stream(side)
             for t in (dw, db):  # (allocated on the side stream, consumed on this one)
@@ -595,6 +611,8 @@ class _MfmaConv2d(torch.autograd.Function):
         if need_w:
             if dw is None:
                 dw = _wgrad(dy, xb, wb, stride, padding, dilation, cout, cin, wdt, sn)
+            elif not need_w_left:  # (thin-output path: already cropped, in fp32)
+                pass
             if dw.shape[0] != cout or dw.shape[1] != cin:
                 dw = dw[:cout, :cin]
             dw = dw.to(wdt)
@@ -627,6 +645,37 @@ def _test_flip_wgrad(dw):
     return -dw if _TEST_FLIP_WGRAD[1] == _TEST_FLIP_WGRAD[0] else dw
 
 
+def _thin_output_grads(dy, xb, wb, padding, cout, cin, xc, need_x, need_w, wdt):
+    """Data and weight gradients of a stride-1 conv with a thin output (Cout <= 16) from the
+    tap-packed operand of its output gradient (see :class:`_MfmaConv2d` backward).
+    dy [B, cout, Ho, Wo] (a view is fine), xb [B, cp, H, W] bf16, wb [op, cp, KH, KW] bf16.
+    Returns (dx [B, xc or cp, H, W] bf16 or None, dW [cout, cin, KH, KW] fp32 or None)."""
+    X = _ext.ext()
+    kh, kw = wb.shape[2], wb.shape[3]
+    cp = wb.shape[1]
+    K = kh * kw * cout
+    kp = _round_up(K, 64)
+    dyc = X.im2col_pack(dy, kh, kw, 1, 1, kh - 1 - padding[0], kw - 1 - padding[1], 1, 1, kp)
+    fl = 2.0 * dyc.shape[0] * dyc.shape[2] * dyc.shape[3] * kp * cp
+    dx = dw = None
+    if need_x:
+        # Wd[ci][(t', co)] = w[co, ci, flip(t')]
+        wd = torch.zeros((cp, kp), dtype=torch.bfloat16, device=wb.device)
+        wd[:, :K] = wb[:cout].flip(2, 3).permute(1, 2, 3, 0).reshape(cp, K)
+        ncv = xc if (cp != xc and xc % 8 == 0) else cp
+        with _Logged('dgrad', 'k10p', fl, '%s thin-out' % list(dyc.shape)):
+            dx = X.conv2d_mfma(dyc, wd.view(cp, kp, 1, 1), None, 1, 1, 0, 0, 1, 1, 1.0, 1, ncv,
+                               None, None)
+    if need_w:
+        with _Logged('wgrad', 'k11', fl, '%s thin-out' % list(dyc.shape)):
+            g = X.conv2d_wgrad_mfma(dyc, xb, 1, 1, 1, 1, 0, 0, 1, 1, K, cin, False, 1)
+        # g[(t', co)][ci] -> dW[co, ci, t] with t = flip(t')
+        dw = g.reshape(kh, kw, cout, cin).flip(0, 1).permute(2, 3, 0, 1)
+        if _TEST_FLIP_WGRAD[0]:
+            dw = _test_flip_wgrad(dw)
+    return dx, dw
+
+
 class SNWeight(object):
     """A spectrally normalised conv weight handed to :func:`conv2d` / :func:`conv2d_act`
     unmaterialised (layers/spectral_norm.py ``weight_ref``): the fp32 parameter ``W``, its bf16
@@ -634,7 +683,9 @@ class SNWeight(object):
     and sigma (a device scalar). On the k10 / k11 path the conv runs on the shadow with
     1 / sigma in its epilogues and the SN backward in its weight gradient
     (:class:`_MfmaConv2d`); any other consumer calls :meth:`materialize` for the usual
-    bf16(W / sigma) tensor (reference: torch.nn.utils.spectral_norm, W / (u^T W v))."""
+    bf16(W / sigma) tensor (reference: torch.nn.utils.spectral_norm, W / (u^T W v)). After such
+    a fused forward the module's ``weight`` attribute holds this object (not a stale tensor):
+    ``module.weight.materialize()`` is the normalised weight that forward used."""
 
     __slots__ = ('W', 'shadow', 'u', 'v', 'sigma', 'hook', 'module')
 
@@ -664,7 +715,8 @@ def _sn_fused_ok(x, sw, stride, padding, dilation, residual=None):
         return False
     wm = torch.empty((sw.shadow.shape[0], cx) + tuple(sw.shadow.shape[2:]), dtype=torch.bfloat16,
                      device='meta')
-    if tapsplit_eligible(x, wm, stride, padding, dilation, 1) or \
+    if tappack_eligible(_thin_view(x, cw), sw.shadow, stride, padding, dilation, 1) or \
+            tapsplit_eligible(x, wm, stride, padding, dilation, 1) or \
             not mfma_eligible(x, wm, stride, padding, dilation, 1):
         return False
     return residual is None or _residual_fusible(residual, x, wm, stride, padding, dilation)
@@ -860,6 +912,146 @@ class _TapSplitConv2d(torch.autograd.Function):
             dyb = nhwc(dy if dy.dtype in (torch.bfloat16, torch.float32) else dy.float())
             db = _ext.ext().bias_act_bwd(dyb, dyb, 1.0)[1].to(bdt)
         return dx, dw, db, None, None
+
+
+def _pack_taps(w, kp, op):
+    """[Cout, Cin, KH, KW] -> the 1x1 GEMM weight [op, kp, 1, 1] (bf16) of a tap-packed conv:
+    row n = w[n] in (ky, kx, ci) order, zero-padded to kp columns and op rows."""
+    cout, cin, kh, kw = w.shape
+    out = torch.zeros((op, kp), dtype=torch.bfloat16, device=w.device)
+    out[:cout, :kh * kw * cin] = w.detach().to(torch.bfloat16).permute(0, 2, 3, 1).reshape(cout, -1)
+    return out.view(op, kp, 1, 1)
+
+
+class _TapPackConv2d(torch.autograd.Function):
+    """Thin-input convolutions (Cin <= 16: RGB stems, image + mask inputs, flow inputs) with the
+    filter taps packed into the GEMM's K dimension (csrc/im2col.hip): im2col_pack writes
+    col[m][(ky, kx, ci)] once (K = KH*KW*Cin padded to 64, e.g. 147 -> 192 for a 7x7 RGB stem,
+    instead of 49 taps x 64 zero-padded channels), the conv is a 1x1 k10 GEMM with the fused
+    bias / activation epilogue, and the weight gradient a 1x1 k11 GEMM on the same operand; the
+    data gradient (a thin-output conv of dy) runs on the k10 dgrad."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias, stride, padding, dilation, slope):
+        cout, cin, kh, kw = w.shape
+        kp, op = _round_up(kh * kw * cin, 64), _out_pad(cout)
+        X = _ext.ext()
+        col = X.im2col_pack(x.detach(), kh, kw, stride[0], stride[1], padding[0], padding[1],
+                            dilation[0], dilation[1], kp)
+        wp = _frozen_prep(w, ('tp', kp, op), lambda: _pack_taps(w, kp, op))
+        ncv = cout if (op != cout and cout % 8 == 0) else op
+        with _Logged('fwd', 'k10p', 2.0 * col.shape[0] * col.shape[2] * col.shape[3] * op * kp,
+                     _gemm_desc(x, w, stride, padding) + ' tappack'):
+            bp = None if bias is None else _frozen_prep(bias, ('b', op),
+                                                        lambda: _pad_rows(bias, op).float())
+            y = X.conv2d_mfma(col, wp, bp, 1, 1, 0, 0, 1, 1, float(slope), 1, ncv, None, None)
+        ctx.conf = (stride, padding, dilation, float(slope), cin, cout, kh, kw, x.shape[2],
+                    x.shape[3], x.dtype, w.dtype, None if bias is None else bias.dtype)
+        ctx.save_for_backward(col, wp, y if slope != 1.0 else None)
+        if y.shape[1] == cout:
+            return y
+        return y[:, :cout].contiguous(memory_format=_CL)
+
+    @staticmethod
+    def backward(ctx, dy):
+        col, wp, y = ctx.saved_tensors
+        (stride, padding, dilation, slope, cin, cout, kh, kw, H, W, xdt, wdt, bdt) = ctx.conf
+        need_x, need_w, need_b = ctx.needs_input_grad[:3]
+        X = _ext.ext()
+        op, kp = wp.shape[0], wp.shape[1]
+        db = None
+        if slope != 1.0:
+            dy = _pad_channels(dy, y.shape[1], torch.bfloat16)
+            dy, db = X.bias_act_bwd(y, dy, slope)
+        elif need_b:
+            dy = _pad_channels(dy, dy.shape[1], torch.bfloat16)
+            db = X.bias_act_bwd(dy, dy, 1.0)[1]
+        dy = _pad_channels(dy, op, torch.bfloat16)
+        dx = dw = None
+        if need_x:
+            # the data gradient of a thin INPUT is a thin-output conv of dy: on the usual k10
+            # dgrad (flipped weight, output channels padded to 64). (The adjoint of the packing —
+            # a [M][Kp] dcol GEMM + col2im_pack gather — ran at ~12 TF/s: its 2-byte gathers
+            # from KH*KW rows per pixel are the bottleneck; gpurun_out r6b, MUNIT / pix2pixHD.)
+            K = kh * kw * cin
+            wb = torch.empty((op, 64, kh, kw), dtype=torch.bfloat16, device=wp.device,
+                             memory_format=_CL).zero_()
+            wb[:cout, :cin] = wp.view(op, kp)[:cout, :K].view(cout, kh, kw, cin).permute(
+                0, 3, 1, 2)
+            fl = 2.0 * dy.shape[0] * dy.shape[2] * dy.shape[3] * wb.numel()
+            ncv = cin if cin % 8 == 0 else 64
+            if stride == (1, 1) and dilation == (1, 1):
+                with _Logged('dgrad', 'k10', fl, _gemm_desc(dy, wb.transpose(0, 1), (1, 1),
+                                                           padding) + ' tappack-in'):
+                    dx = X.conv2d_dgrad_mfma(dy, wb, padding[0], padding[1], ncv, None)
+            elif stride[0] == stride[1] and 2 <= stride[0] <= 4 and dilation == (1, 1) and \
+                    0 <= padding[0] < kh and 0 <= padding[1] < kw:
+                with _Logged('dgrad', 'k10s', fl, _gemm_desc(dy, wb, stride, padding) +
+                             ' tappack-in'):
+                    dx = _strided_dgrad(dy, wb, H, W, stride[0], padding, ncv=ncv)
+            else:
+                dx = torch.ops.aten.convolution_backward(
+                    dy, torch.empty((dy.shape[0], 64, H, W), dtype=torch.bfloat16,
+                                    device=dy.device, memory_format=_CL),
+                    wb, None, stride, padding, dilation, False, [0, 0], 1,
+                    [True, False, False])[0]
+            dx = dx[:, :cin].to(xdt)
+        if need_w:
+            with _Logged('wgrad', 'k11', 2.0 * col.shape[0] * col.shape[2] * col.shape[3] * op *
+                         kp, '%s tappack' % list(col.shape)):
+                g = X.conv2d_wgrad_mfma(dy, col, 1, 1, 1, 1, 0, 0, 1, 1, cout, kh * kw * cin,
+                                        False, 1)
+            dw = g.reshape(cout, kh, kw, cin).permute(0, 3, 1, 2).to(wdt)
+            if _TEST_FLIP_WGRAD[0]:
+                dw = _test_flip_wgrad(dw)
+        if db is not None:
+            db = db[:cout].to(bdt) if need_b else None
+        return dx, dw, db, None, None, None, None
+
+
+_TAPPACK = os.environ.get('IMAGINAIRE_AMD_TAPPACK', '1') == '1'
+
+
+def _thin_view(x, cin):
+    """``x`` itself, or — for a channel-padded buffer whose zero tail starts at a thin weight's
+    ``cin`` (``mark_zero_tail``) — the strided view of its real channels, which im2col_pack reads
+    without a copy."""
+    if x.dim() == 4 and x.shape[1] != cin and cin <= 16 and \
+            getattr(x, '_iamd_valid_channels', None) == cin:
+        return x[:, :cin]
+    return x
+
+
+def tappack_eligible(x, w, stride, padding, dilation, groups):
+    """The tap-packed path (:class:`_TapPackConv2d`): bf16 compute, groups 1, a thin input
+    (Cin <= 16) whose packed K = KH*KW*Cin fits 512, a spatial filter, and enough output pixels
+    for the 1x1 GEMM (or inside a graph capture)."""
+    if not (_TAPPACK and x.is_cuda and x.dim() == 4 and w.dim() == 4 and groups == 1 and
+            _mfma_enabled() and x.dtype in (torch.float32, torch.bfloat16)):
+        return False
+    cout, cin, kh, kw = w.shape
+    if cin > 16 or x.shape[1] != cin or kh * kw * cin > 512 or kh * kw == 1:
+        return False
+    if _compute_dtype(x, w) != torch.bfloat16:
+        return False
+    ho, wo = _out_hw(x.shape[2], x.shape[3], (kh, kw), stride, padding, dilation)
+    if ho <= 0 or wo <= 0:
+        return False
+    m = x.shape[0] * ho * wo
+    kp, op = _round_up(kh * kw * cin, 64), _out_pad(cout)
+    # the packed operand is written once and read twice (forward, weight gradient): it pays
+    # where it removes >= 8x of the implicit GEMM's zero-padded k loop (RGB / 1-6 channel
+    # inputs). Cin 8 / 16 layers (pix2pixHD's instance encoder: 7x7x8 -> 448, 3x3x16 -> 192)
+    # moved ~0.6 ms of operand traffic per call for a 3-7x smaller GEMM: no net gain
+    # (gpurun_out r6ab)
+    if kh * kw * 64 < 8 * kp:
+        return False
+    if m * kp * 2 >= (1 << 30) or m * op * 2 >= (1 << 30):
+        return False
+    return m >= _TAPPACK_MIN_PIX or _capturing()
+
+
+_TAPPACK_MIN_PIX = int(os.environ.get('IMAGINAIRE_AMD_TAPPACK_MIN_PIX', 2048))
 
 
 _TAPSPLIT = os.environ.get('IMAGINAIRE_AMD_TAPSPLIT', '1') == '1'
@@ -1113,6 +1305,9 @@ def conv2d_act(x, weight, bias=None, stride=1, padding=0, dilation=1, slope=1.0)
             return _MfmaConv2d.apply(x, weight.W, bias, stride, padding, dilation, slope, None,
                                      weight)
         weight = weight.materialize()
+    xt = _thin_view(x, weight.shape[1])
+    if tappack_eligible(xt, weight, stride, padding, dilation, 1):
+        return _TapPackConv2d.apply(xt, weight, bias, stride, padding, dilation, slope)
     weight = _match_channels(x, weight)
     if slope == 1.0 and tapsplit_eligible(x, weight, stride, padding, dilation, 1):
         return _TapSplitConv2d.apply(x, weight, bias, padding, dilation)
@@ -1200,11 +1395,19 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1,
                     _residual_fusible(residual, x, w, st, pd, dl):
                 return _MfmaConv2d.apply(x, w, bias, st, pd, dl, 1.0, residual)
         return conv2d(x, weight, bias, stride, padding, dilation, groups, padding_mode) + residual
+    if padding_mode != 'zeros' and padding_mode is not None:
+        vc = getattr(x, '_iamd_valid_channels', None)
+        x = pad(nhwc(x), _pad_arg(padding), padding_mode)
+        if vc is not None:
+            x._iamd_valid_channels = vc
+        padding = 0
+    if x.is_cuda and x.dim() == 4 and weight.dim() == 4:
+        st, pd, dl = _pair(stride), _pair(padding), _pair(dilation)
+        xt = _thin_view(x, weight.shape[1])
+        if tappack_eligible(xt, weight, st, pd, dl, groups):
+            return _TapPackConv2d.apply(xt, weight, bias, st, pd, dl, 1.0)
     if groups == 1:
         weight = _match_channels(x, weight)
-    if padding_mode != 'zeros' and padding_mode is not None:
-        x = pad(nhwc(x), _pad_arg(padding), padding_mode)
-        padding = 0
     if x.is_cuda and x.dim() == 4:
         st, pd, dl = _pair(stride), _pair(padding), _pair(dilation)
         if tapsplit_eligible(x, weight, st, pd, dl, groups):

@@ -291,8 +291,8 @@ def main():
         fl = sum(r[5] * r[4] * 1e9 for r in rows)
         print('conv kernels in one iteration: %.2f ms of %.1f ms wall, %.2f TFLOP, %.0f TF/s' % (
             tot, wall, fl / 1e12, fl / max(tot, 1e-9) / 1e9))
-        for kind, path, desc, n, ms, tfs in rows[:40]:
-            print('%8.3f ms %3d  %-6s %-7s %5.0f TF/s  %s' % (ms, n, kind, path, tfs, desc))
+        for kind, path, desc, n, ms, tfs in rows[:60]:
+            print('%8.3f ms %3d  %-6s %-8s %5.0f TF/s  %s' % (ms, n, kind, path, tfs, desc))
     frames = 1
     if video:
         img = data.get('images') if isinstance(data, dict) else None

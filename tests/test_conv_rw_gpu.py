@@ -37,6 +37,8 @@ RW_CASES = [
     (1, 32, 64, 16, 16, 1, 1, 1, 0),       # Cin 32, 1x1 (one half-zero tap)
     (1, 32, 64, 15, 21, 5, 5, 2, 2),       # Cin 32, 5x5 s2
     (2, 32, 64, 64, 128, 3, 3, 1, 1),      # Cin 32 at a 128-wide row
+    (1, 512, 128, 12, 32, 4, 4, 2, 1),     # 4x4 s2 over eight channel blocks (K 8192)
+    (2, 64, 64, 16, 64, 7, 7, 1, 3),       # 7x7 stem-like, 64-pixel rows
 ]
 
 
@@ -129,11 +131,95 @@ def test_rw_never_reads_unwritten_lds(case):
     assert torch.equal(y0, y1)
 
 
-def test_rw_taken_by_default_for_v1_shapes():
-    """Without a forced variant, the shapes v4 / v5 do not take run on the row-window tile."""
+def test_rw_taken_by_default_for_long_filters():
+    """Without a forced variant, long-filter shapes v4 / v5 do not take (7x7, 4x4 over three
+    channel blocks) and Cin = 32 run on the row-window tile."""
     from imaginaire_amd.ops import _ext
     X = _ext.ext()
-    for case in (RW_CASES[1], RW_CASES[4], RW_CASES[13]):
+    for case in (RW_CASES[20], RW_CASES[19], RW_CASES[13]):
         x, w, b = _inputs(case)
         _, var = _run(X, x, w, b, case[7], case[8], ver='0')
         assert var == 6, (case, var)
+
+
+# ---- tap-packed thin-input convolutions (csrc/im2col.hip + 1x1 k10 / k11) -----------------
+# B, Cin, Cout, H, W, k, stride, pad, x layout
+PACK_CASES = [
+    (2, 3, 64, 38, 42, 7, 1, 3, 'nchw'),     # RGB stem (7x7, K 147 -> 192)
+    (2, 3, 32, 40, 48, 4, 2, 1, 'nchw'),     # PatchGAN first layer on an image
+    (1, 6, 64, 33, 35, 7, 2, 3, 'cl'),       # FlowNet-style two-image input, stride 2
+    (2, 1, 64, 20, 24, 3, 1, 1, 'cl'),       # one-channel mask
+    (1, 16, 128, 24, 24, 5, 1, 2, 'nchw'),   # K 400 -> 448
+]
+
+
+@pytest.mark.parametrize('case', PACK_CASES)
+@pytest.mark.parametrize('slope,bias', [(1.0, False), (0.2, True)])
+def test_tappack_conv_fwd_bwd(case, slope, bias):
+    from imaginaire_amd.ops import conv as C
+    C._TAPPACK_MIN_PIX = 0
+    B, cin, cout, H, W, k, s, p, layout = case
+    torch.manual_seed(9)
+    x = torch.randn(B, cin, H, W, device='cuda')
+    if layout == 'cl':
+        x = x.contiguous(memory_format=CL)
+    x.requires_grad_(True)
+    w = (torch.randn(cout, cin, k, k, device='cuda') / (cin * k * k) ** 0.5 +
+         torch.arange(cout, device='cuda').view(-1, 1, 1, 1) * 1e-3).requires_grad_(True)
+    b = (torch.randn(cout, device='cuda') * 0.1).requires_grad_(True) if bias else None
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        assert C.tappack_eligible(x, w, (s, s), (p, p), (1, 1), 1)
+        y = C.conv2d_act(x, w, b, s, p, 1, slope)
+    # reference on the bf16-rounded operands in fp32
+    xr = x.detach().to(torch.bfloat16).float().requires_grad_(True)
+    wr = w.detach().to(torch.bfloat16).float().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True) if bias else None
+    yr = F.conv2d(xr, wr, br, s, p)
+    if slope != 1.0:
+        yr = torch.where(y.detach().float() > 0, yr, yr * slope)
+    assert y.shape == yr.shape
+    err = (y.float() - yr).abs().max().item()
+    assert err <= 1e-2 * max(1.0, yr.abs().max().item()), err
+    go = torch.randn_like(yr)
+    y.backward(go.to(y.dtype))
+    yr.backward(go)
+    assert x.grad.dtype == x.dtype and x.grad.shape == x.shape
+    for got, ref, name in ((x.grad, xr.grad, 'dx'), (w.grad, wr.grad, 'dw')) + \
+            (((b.grad, br.grad, 'db'),) if bias else ()):
+        e = (got.float() - ref).abs().max().item()
+        assert e <= 2e-2 * max(1.0, ref.abs().max().item()), (name, e, ref.abs().max().item())
+
+
+@pytest.mark.parametrize('case', [
+    # B, Cin, Cout, H, W, k, pad
+    (2, 64, 3, 30, 34, 7, 3),    # MUNIT / pix2pixHD RGB head
+    (1, 128, 1, 20, 28, 3, 1),   # one-channel mask head
+    (2, 64, 8, 16, 40, 5, 2),
+    (1, 96, 3, 18, 22, 7, 0),    # unpadded head on a reflect-padded input
+])
+def test_thin_output_conv_grads(case):
+    """Heads with Cout <= 16: the data and weight gradients from one tap-packed dy operand."""
+    from imaginaire_amd.ops import conv as C
+    C._MFMA_MIN_BLOCKS = 0
+    C._MFMA_MIN_DGRAD_BLOCKS = 0
+    B, cin, cout, H, W, k, p = case
+    torch.manual_seed(11)
+    x = torch.randn(B, cin, H, W, device='cuda').to(torch.bfloat16).contiguous(
+        memory_format=CL).requires_grad_(True)
+    w = (torch.randn(cout, cin, k, k, device='cuda') / (cin * k * k) ** 0.5).to(
+        torch.bfloat16).contiguous(memory_format=CL).requires_grad_(True)
+    b = (torch.randn(cout, device='cuda') * 0.1).requires_grad_(True)
+    y = C.conv2d_act(x, w, b, 1, p, 1, 1.0)
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().float().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True)
+    yr = F.conv2d(xr, wr, br, 1, p)
+    assert y.shape == yr.shape
+    assert (y.float() - yr).abs().max().item() <= 1e-2 * max(1.0, yr.abs().max().item())
+    go = torch.randn_like(yr)
+    y.backward(go.to(y.dtype))
+    yr.backward(go)
+    for got, ref, name in ((x.grad, xr.grad, 'dx'), (w.grad, wr.grad, 'dw'),
+                           (b.grad, br.grad, 'db')):
+        e = (got.float() - ref).abs().max().item()
+        assert e <= 2e-2 * max(1.0, ref.abs().max().item()), (name, e, ref.abs().max().item())

@@ -88,6 +88,17 @@ def test_sn_fused_conv_matches_materialised_and_fp32(monkeypatch, dot_ratio):
             outs['fp32'] = (y32.detach(), xi.grad, [p.grad.clone() for p in f32.parameters()])
             if it == 0:
                 assert len(calls) == 5, calls        # every conv took the fused path
+                # after a fused forward, module.weight is the unmaterialised reference (not a
+                # stale tensor) and materialises to the W / sigma the materialised path used
+                from imaginaire_amd.layers.weight_norm import _sn_hook
+                fmods = [m for m in net.modules() if _sn_hook(m) is not None]
+                rmods = [m for m in ref.modules() if _sn_hook(m) is not None]
+                assert len(fmods) == len(rmods) == 5
+                for fm, rm in zip(fmods, rmods):
+                    assert isinstance(fm.weight, C.SNWeight), type(fm.weight)
+                    wm = fm.weight.materialize()
+                    assert wm.shape == rm.weight.shape
+                    assert _rel(wm, rm.weight) <= 1e-2, _rel(wm, rm.weight)
             yf, yr, y3 = outs['fused'][0], outs['mat'][0], outs['fp32'][0]
             assert _rel(yf, y3) <= max(2e-2, 1.5 * _rel(yr, y3)), (it, _rel(yf, y3), _rel(yr, y3))
             assert _rel(yf, yr) <= 2e-2, (it, _rel(yf, yr))
