@@ -29,6 +29,20 @@ hop = 16
 mode = os.environ.get('MODE', 'kernel')
 a = torch.zeros(size, device='cuda')
 b = torch.zeros(size, device='cuda')
+if mode in ('memset', 'memset4'):
+    # hipMemsetAsync on the capturing stream: MEMSET graph nodes, as the few-shot vid2vid
+    # graph holds (36 four-byte memsets, scripts/probe/graph_dot.py). The hop writes b, zeroes
+    # it (all of it / its first 4 bytes) and adds it back to a: a memset that runs out of order
+    # with its neighbours leaves a off by the b it should have cleared.
+    import ctypes
+    _hip = ctypes.CDLL('libamdhip64.so')
+    _hip.hipMemsetAsync.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t,
+                                    ctypes.c_void_p]
+
+    def _memset(t, nbytes):
+        err = _hip.hipMemsetAsync(ctypes.c_void_p(t.data_ptr()), 0, nbytes,
+                                  ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        assert err == 0, err
 if mode == 'hip':
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
     os.environ.setdefault('IMAGINAIRE_AMD_GRAPH_ALLOW_PACKET_CAPTURE', '1')
@@ -43,6 +57,13 @@ def body():
             if mode == 'copy':
                 b.copy_(a)
                 a.copy_(b)
+            elif mode in ('memset', 'memset4'):
+                torch.mul(a, 2.0, out=b)
+                _memset(b, b.numel() * 4 if mode == 'memset' else 4)
+                if mode == 'memset':
+                    a.add_(b)
+                else:
+                    a[:1].add_(b[:1])
             elif mode == 'hip':
                 t = X.pad_channels_cast(a4, size // 64, torch.float32)
                 a4.copy_(t)

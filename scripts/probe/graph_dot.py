@@ -75,10 +75,20 @@ def main():
     for a, b in edges:
         succ[a].append(b)
         pred[b].append(a)
+    def kname(n):
+        m = re.search(r'KERNEL \| \{ID \| \d+ \| ([^\\<]+)', nodes.get(n, ''))
+        return m.group(1)[:90] if m else kind(nodes.get(n, ''))
+
     odd = [n for n, l in nodes.items() if kind(l) not in ('KERNEL',)]
     print('non-kernel nodes: %d' % len(odd))
-    for n in odd[:10]:
-        print('  %s (%s): pred %s succ %s' % (n, kind(nodes[n]), pred[n][:3], succ[n][:3]))
+    pairs = collections.Counter()
+    for n in odd:
+        pairs[(kind(nodes[n]), tuple(kname(p) for p in pred[n]), tuple(kname(q) for q in succ[n]))] += 1
+    print('non-kernel node neighbourhoods (kind, predecessor kernel, successor kernel): count')
+    for (k, pr, sc), c in pairs.most_common(40):
+        print('  %4d  %-7s %s -> %s' % (c, k, pr, sc))
+    for n in [n for n in odd if kind(nodes[n]) == 'MEMSET'][:6]:
+        print('  memset %s: %s' % (n, re.sub(r'\s+', ' ', nodes[n])[:400]))
 
 
 if __name__ == '__main__':
