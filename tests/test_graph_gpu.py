@@ -455,3 +455,27 @@ def test_vid2vid_capture_with_rccl_collectives(tmp_path):
     for k in le:
         assert lg[k] == lg[k], k
         assert abs(lg[k] - le[k]) <= 1e-3 * max(1.0, abs(le[k])), (k, lg[k], le[k])
+
+
+@pytest.mark.gpu
+def test_package_default_orders_memset_nodes():
+    """Root cause of the round-4/5 few-shot vid2vid replay NaN: with the HIP runtime's graph
+    packet capture on, MEMSET nodes (PyTorch's reduction semaphores) run out of order with the
+    kernel packets around them (profiles/r6/README_graph_root_cause.txt). Under the package
+    default (DEBUG_CLR_GRAPH_PACKET_CAPTURE=0, set at import) a long chain with memset hops
+    replays exactly."""
+    import subprocess
+    import sys
+    import imaginaire_amd
+    assert imaginaire_amd.PACKET_CAPTURE_STATE == 'off'
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    assert env.get('DEBUG_CLR_GRAPH_PACKET_CAPTURE') == '0'
+    for mode in ('memset', 'memset4'):
+        env['MODE'] = mode
+        out = subprocess.run([sys.executable, os.path.join(root, 'scripts', 'probe',
+                                                           'graph_coherence_probe.py'),
+                              '4000', str(1 << 20), '2'], env=env, capture_output=True,
+                             text=True, timeout=240)
+        assert out.returncode == 0, out.stderr[-2000:]
+        assert 'COHERENCE OK 0' in out.stdout, out.stdout[-2000:]

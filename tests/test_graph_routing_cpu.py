@@ -1,6 +1,8 @@
 """Host-side logic of the graphed-step helpers (utils/cuda_graph.py), no GPU needed:
 graph_routing nests and restores, the static-batch copy ignores entries the captured step added
 to its static batch, and batch signatures separate structures."""
+import os
+
 import torch
 
 
@@ -39,3 +41,39 @@ def test_signature_separates_structures():
     c = {'x': torch.zeros(3, 3), 'key': 'file_a'}
     assert _signature(a) == _signature(b)
     assert _signature(a) != _signature(c)
+
+
+def test_packet_capture_guard_refuses_unless_off(monkeypatch):
+    """utils/cuda_graph.py refuses to capture when the runtime's packet-capture mode is (or may
+    be) on: HIP started before the package import with the variable unset, or an explicit
+    non-zero value (imaginaire_amd.PACKET_CAPTURE_STATE); the probe override captures anyway."""
+    import imaginaire_amd
+    from imaginaire_amd.utils import cuda_graph as G
+    monkeypatch.delenv('IMAGINAIRE_AMD_GRAPH_ALLOW_PACKET_CAPTURE', raising=False)
+    monkeypatch.setattr(imaginaire_amd, 'PACKET_CAPTURE_STATE', 'off')
+    assert G.packet_capture_refusal() is None
+    monkeypatch.setattr(imaginaire_amd, 'PACKET_CAPTURE_STATE', 'unknown')
+    r = G.packet_capture_refusal()
+    assert r is not None and 'before imaginaire_amd was imported' in r
+    monkeypatch.setattr(imaginaire_amd, 'PACKET_CAPTURE_STATE', 'on')
+    assert 'DEBUG_CLR_GRAPH_PACKET_CAPTURE' in G.packet_capture_refusal()
+    monkeypatch.setenv('IMAGINAIRE_AMD_GRAPH_ALLOW_PACKET_CAPTURE', '1')
+    assert G.packet_capture_refusal() is None
+
+
+def test_packet_capture_state_detects_late_import():
+    """A process that initialised HIP (torch.cuda) before importing the package is flagged
+    'unknown' (run in a fresh interpreter with a stub torch whose cuda reports initialised)."""
+    import subprocess
+    import sys
+    code = ('import sys, types, os\n'
+            'os.environ.pop("DEBUG_CLR_GRAPH_PACKET_CAPTURE", None)\n'
+            't = types.ModuleType("torch"); t.cuda = types.SimpleNamespace('
+            'is_initialized=lambda: True)\n'
+            'sys.modules["torch"] = t\n'
+            'import imaginaire_amd\n'
+            'print(imaginaire_amd.PACKET_CAPTURE_STATE)\n')
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, '-c', code], cwd=root, capture_output=True, text=True,
+                         timeout=60)
+    assert out.stdout.strip().endswith('unknown'), (out.stdout, out.stderr[-1000:])
