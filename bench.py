@@ -53,6 +53,10 @@ def parse():
                         'single-GPU multi-rank rehearsals with --share-gpu)')
     p.add_argument('--device', default='cuda', choices=('cuda', 'cpu'),
                    help='cpu: plumbing rehearsal of the launcher / DDP path (gloo), no GPU')
+    p.add_argument('--force-dist', action='store_true',
+                   help='measurement only: run the distributed wrappers (bucketed DDP over a '
+                        'native RCCL communicator, sync-BN exchanges) on a ONE-rank process '
+                        'group, to price their overhead against the plain world-1 step')
     p.add_argument('--share-gpu', action='store_true',
                    help='testing only: every rank uses cuda:0 (rehearse the DDP path on one GPU)')
     p.add_argument('--torch-profile', action='store_true',
@@ -145,7 +149,12 @@ def main():
     if on_gpu:
         # set the device before the process group so RCCL binds rank r to GPU r
         torch.cuda.set_device(local_rank)
-    if world > 1:
+    if args.force_dist and world == 1:
+        os.environ.setdefault('RANK', '0')
+        os.environ.setdefault('WORLD_SIZE', '1')
+        os.environ.setdefault('MASTER_PORT', str(29500 + os.getpid() % 1000))
+        os.environ['IMAGINAIRE_AMD_FORCE_DIST'] = '1'
+    if world > 1 or args.force_dist:
         init_dist(local_rank, backend=args.backend if on_gpu else 'gloo')
     from imaginaire_amd.utils.cudnn import init_cudnn
     init_cudnn(False, True)
@@ -320,7 +329,7 @@ def main():
                                 'sync-BN SPADE 5x5 separate-projection, 2xPatchGAN+FPSE D, '
                                 'VGG19 perceptual, EMA)',
                        'global_batch': bs * world, 'seq_len': None, 'resolution': '256x512',
-                       'parallelism': 'dp%d' % world,
+                       'parallelism': 'dp%d' % world + ('-forced-dist' if args.force_dist else ''),
                        'kernels': 'eager-reference' if args.eager else 'hip',
                        'hipgraph': bool(graphed is not None and graphed.graph is not None),
                        'backend': args.backend if (world > 1 and on_gpu) else

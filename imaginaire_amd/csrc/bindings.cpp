@@ -120,7 +120,8 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
                              int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh,
                              int64_t dw, int64_t out_cout, int64_t out_cin, bool out_bf16,
                              int64_t nb, int64_t variant,
-                             const c10::optional<std::vector<at::Tensor>>& sn);
+                             const c10::optional<std::vector<at::Tensor>>& sn,
+                             const c10::optional<at::Tensor>& dst);
 bool conv2d_wgrad_v2_eligible(const at::Tensor& dy, const at::Tensor& x, int64_t KH, int64_t KW,
                               int64_t sh, int64_t sw, int64_t dh, int64_t dw, int64_t nb);
 // conv_tapsplit.hip
@@ -154,7 +155,7 @@ at::Tensor pad_nhwc_bwd(const at::Tensor& dy, int64_t H, int64_t W, int64_t pl, 
 at::Tensor sn_dot_partials(const at::Tensor& dx, const at::Tensor& x, const at::Tensor& sigma);
 at::Tensor wgrad_finalize(const at::Tensor& part, int64_t S, int64_t Cop, int64_t Cip,
                           int64_t Cout, int64_t Cin, int64_t KH, int64_t KW,
-                          at::ScalarType dtype);
+                          at::ScalarType dtype, const c10::optional<at::Tensor>& dst);
 at::Tensor sn_scale_backward(const at::Tensor& grad_in, const at::Tensor& weight,
                              const at::Tensor& u, const at::Tensor& v, const at::Tensor& sigma,
                              const c10::optional<at::Tensor>& shadow);
@@ -210,7 +211,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dy"), py::arg("x"), py::arg("KH"), py::arg("KW"), py::arg("sh"), py::arg("sw"),
         py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("out_cout") = -1,
         py::arg("out_cin") = -1, py::arg("out_bf16") = false, py::arg("nb") = 1,
-        py::arg("variant") = 0, py::arg("sn") = py::none());
+        py::arg("variant") = 0, py::arg("sn") = py::none(), py::arg("dst") = py::none());
   m.def("conv2d_wgrad_v2_eligible", &iamd::conv2d_wgrad_v2_eligible,
         "whether the k11 v2 (one wave per SIMD) kernel can run this weight gradient",
         py::arg("dy"), py::arg("x"), py::arg("KH"), py::arg("KW"), py::arg("sh"), py::arg("sw"),

@@ -742,15 +742,32 @@ std::vector<at::Tensor> mt_conv_weight_flip_t(const std::vector<at::Tensor>& ws)
 }
 
 // part: fp32 [S * Cop * KK * Cip] -> [Cout, Cin, KH, KW] channels-last in `dtype`.
+// dst_opt: write into this tensor instead (the DDP bucket slice of the parameter's gradient:
+// [Cout, Cin, KH, KW] channels-last in `dtype`), so no copy into the bucket follows.
+static at::Tensor finalize_out(const at::Tensor& part, int64_t Cout, int64_t Cin, int64_t KH,
+                               int64_t KW, at::ScalarType dtype,
+                               const c10::optional<at::Tensor>& dst_opt) {
+  if (dst_opt.has_value() && dst_opt->defined()) {
+    const at::Tensor& d = *dst_opt;
+    IAMD_CHECK(d.is_cuda() && d.scalar_type() == dtype && d.dim() == 4 && d.size(0) == Cout &&
+                   d.size(1) == Cin && d.size(2) == KH && d.size(3) == KW &&
+                   d.is_contiguous(at::MemoryFormat::ChannelsLast),
+               "wgrad_finalize: the destination must be a channels-last [Cout, Cin, KH, KW] "
+               "tensor of the gradient dtype");
+    return d;
+  }
+  return at::empty({Cout, Cin, KH, KW},
+                   part.options().dtype(dtype).memory_format(at::MemoryFormat::ChannelsLast));
+}
+
 at::Tensor wgrad_finalize(const at::Tensor& part, int64_t S, int64_t Cop, int64_t Cip,
                           int64_t Cout, int64_t Cin, int64_t KH, int64_t KW,
-                          at::ScalarType dtype) {
+                          at::ScalarType dtype, const c10::optional<at::Tensor>& dst) {
   IAMD_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous(),
              "wgrad_finalize: contiguous fp32 slabs expected");
   IAMD_CHECK(part.numel() >= S * Cop * KH * KW * Cip && Cout <= Cop && Cin <= Cip,
              "wgrad_finalize: slab shape");
-  auto out = at::empty({Cout, Cin, KH, KW},
-                       part.options().dtype(dtype).memory_format(at::MemoryFormat::ChannelsLast));
+  auto out = finalize_out(part, Cout, Cin, KH, KW, dtype, dst);
   const int KK = (int)(KH * KW);
   const bool vec = Cin % 4 == 0 && Cip % 4 == 0;
   const int64_t n = Cout * KK * (vec ? Cin / 4 : Cin);
@@ -780,7 +797,7 @@ at::Tensor wgrad_finalize(const at::Tensor& part, int64_t S, int64_t Cop, int64_
 at::Tensor wgrad_finalize_sn(const at::Tensor& part, int64_t S, int64_t Cop, int64_t Cip,
                              int64_t Cout, int64_t Cin, int64_t KH, int64_t KW,
                              const at::Tensor& dotp, const at::Tensor& u, const at::Tensor& v,
-                             const at::Tensor& sigma) {
+                             const at::Tensor& sigma, const c10::optional<at::Tensor>& dst) {
   IAMD_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() &&
                  part.numel() >= S * Cop * KH * KW * Cip && Cout <= Cop && Cin <= Cip,
              "wgrad_finalize_sn: slab shape");
@@ -789,8 +806,7 @@ at::Tensor wgrad_finalize_sn(const at::Tensor& part, int64_t S, int64_t Cop, int
                  u.numel() == Cout && v.numel() == Cin * KH * KW && sigma.numel() == 1 &&
                  u.is_contiguous() && v.is_contiguous() && dotp.is_contiguous(),
              "wgrad_finalize_sn: u / v / sigma / partials");
-  auto out = at::empty({Cout, Cin, KH, KW},
-                       part.options().dtype(at::kFloat).memory_format(at::MemoryFormat::ChannelsLast));
+  auto out = finalize_out(part, Cout, Cin, KH, KW, at::kFloat, dst);
   const int KK = (int)(KH * KW);
   const bool vec = Cin % 4 == 0 && Cip % 4 == 0;
   const int64_t n = Cout * KK * (vec ? Cin / 4 : Cin);

@@ -897,12 +897,11 @@ __global__ __launch_bounds__(kThreads, 1) void conv_wgrad_mfma_w4(WgradArgs a) {
 // conv_aux.hip: split-K sum + channel crop + dtype cast of the slabs
 at::Tensor wgrad_finalize(const at::Tensor& part, int64_t S, int64_t Cop, int64_t Cip,
                           int64_t Cout, int64_t Cin, int64_t KH, int64_t KW,
-                          at::ScalarType dtype);
-// ... and the spectral-norm backward folded into the same pass (fp32 dW of W)
+                          at::ScalarType dtype, const c10::optional<at::Tensor>& dst);
 at::Tensor wgrad_finalize_sn(const at::Tensor& part, int64_t S, int64_t Cop, int64_t Cip,
                              int64_t Cout, int64_t Cin, int64_t KH, int64_t KW,
                              const at::Tensor& dotp, const at::Tensor& u, const at::Tensor& v,
-                             const at::Tensor& sigma);
+                             const at::Tensor& sigma, const c10::optional<at::Tensor>& dst);
 
 // dW [out_cout, out_cin, KH, KW] (channels-last memory = [Cout][KH][KW][Cin]) in fp32, or bf16
 // when out_bf16; out_cout / out_cin < 0 keep the (padded) channel counts of dy / x. Cropping
@@ -929,7 +928,8 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
                              int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh,
                              int64_t dw, int64_t out_cout, int64_t out_cin, bool out_bf16,
                              int64_t nb, int64_t variant,
-                             const c10::optional<std::vector<at::Tensor>>& sn) {
+                             const c10::optional<std::vector<at::Tensor>>& sn,
+                             const c10::optional<at::Tensor>& dst) {
   IAMD_CHECK(dy.is_cuda() && x.is_cuda(), "conv2d_wgrad_mfma: CUDA tensors expected");
   IAMD_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16,
              "conv2d_wgrad_mfma: bf16 operands expected");
@@ -1072,9 +1072,22 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
   }
   const bool direct = !use_sn && S == 1 && !out_bf16 && oc == Cout && oi == Cin;
   at::Tensor dW, part;
+  // dst: the caller's destination for dW (a DDP bucket slice, ops/conv.py): the split-K sum
+  // (or the single slab itself) lands there, no copy into the bucket follows
+  const bool has_dst = dst.has_value() && dst->defined();
+  IAMD_CHECK(!has_dst || nb == 1, "conv2d_wgrad_mfma: a destination needs nb == 1");
   if (direct) {
-    dW = at::empty({nb * Cout, Cin, KH, KW},
-                   x.options().dtype(at::kFloat).memory_format(at::MemoryFormat::ChannelsLast));
+    if (has_dst) {
+      IAMD_CHECK(dst->is_cuda() && dst->scalar_type() == at::kFloat && dst->dim() == 4 &&
+                     dst->size(0) == Cout && dst->size(1) == Cin && dst->size(2) == KH &&
+                     dst->size(3) == KW && dst->is_contiguous(at::MemoryFormat::ChannelsLast),
+                 "conv2d_wgrad_mfma: the destination must be a channels-last fp32 "
+                 "[Cout, Cin, KH, KW] tensor");
+      dW = *dst;
+    } else {
+      dW = at::empty({nb * Cout, Cin, KH, KW},
+                     x.options().dtype(at::kFloat).memory_format(at::MemoryFormat::ChannelsLast));
+    }
     a.out = dW.data_ptr<float>();
   } else {
     part = at::empty({(int64_t)S * nb * Cout * KK * Cin}, x.options().dtype(at::kFloat));
@@ -1169,11 +1182,12 @@ at::Tensor conv2d_wgrad_mfma(const at::Tensor& dy, const at::Tensor& x, int64_t 
   if (direct) return dW;
   if (use_sn)
     return wgrad_finalize_sn(part, S, Cout, Cin, oc, oi, KH, KW, dotp, (*sn)[1].contiguous(),
-                             (*sn)[2].contiguous(), (*sn)[3]);
+                             (*sn)[2].contiguous(), (*sn)[3], dst);
   if (nb > 1)  // slabs [S][nb][Cout][KK][Cin]: one [nb * Cout] output, no crop
     return wgrad_finalize(part, S, nb * Cout, Cin, nb * Cout, Cin, KH, KW,
-                          out_bf16 ? at::kBFloat16 : at::kFloat);
-  return wgrad_finalize(part, S, Cout, Cin, oc, oi, KH, KW, out_bf16 ? at::kBFloat16 : at::kFloat);
+                          out_bf16 ? at::kBFloat16 : at::kFloat, c10::nullopt);
+  return wgrad_finalize(part, S, Cout, Cin, oc, oi, KH, KW, out_bf16 ? at::kBFloat16 : at::kFloat,
+                        dst);
 }
 
 }  // namespace iamd

@@ -486,6 +486,8 @@ class _MfmaConv2d(torch.autograd.Function):
         ctx.conf = (stride, padding, dilation, float(slope), cin, cout, x.dtype, w.dtype,
                     None if bias is None else bias.dtype, x.shape[1])
         ctx.sn = None if sw is None else (sw.shadow, sw.u, sw.v, sig)
+        # the weight-gradient destination is looked up on the leaf parameter (DDP bucket slice)
+        ctx.wparam = w if (isinstance(w, torch.nn.Parameter) and w.dtype == torch.float32) else None
         ctx.wflip = _dgrad_weight(wb) if (stride == (1, 1) and dilation == (1, 1) and
                                           ctx.needs_input_grad[0]) else None
         # the output is needed only for a fused activation's mask: with slope 1 it is not
@@ -610,7 +612,8 @@ class _MfmaConv2d(torch.autograd.Function):
                     t.record_stream(main)
         if need_w:
             if dw is None:
-                dw = _wgrad(dy, xb, wb, stride, padding, dilation, cout, cin, wdt, sn)
+                dest = _take_grad_dest(ctx.wparam, (cout, cin, wb.shape[2], wb.shape[3]))
+                dw = _wgrad(dy, xb, wb, stride, padding, dilation, cout, cin, wdt, sn, dest)
             elif not need_w_left:  # (thin-output path: already cropped, in fp32)
                 pass
             if dw.shape[0] != cout or dw.shape[1] != cin:
@@ -1123,12 +1126,13 @@ def _agree(times):
     return out
 
 
-def _wgrad_fns(dy, xb, wb, stride, padding, dilation, cout, cin, wdt, variant=0, sn=None):
+def _wgrad_fns(dy, xb, wb, stride, padding, dilation, cout, cin, wdt, variant=0, sn=None,
+               dest=None):
     def k11(v=variant):
         return _ext.ext().conv2d_wgrad_mfma(dy, xb, wb.shape[2], wb.shape[3], stride[0],
                                             stride[1], padding[0], padding[1], dilation[0],
                                             dilation[1], cout, cin, wdt == torch.bfloat16, 1, v,
-                                            None if sn is None else list(sn))
+                                            None if sn is None else list(sn), dest)
 
     def miopen():
         return torch.ops.aten.convolution_backward(
@@ -1148,14 +1152,35 @@ def _k11_variants(dy, xb, wb, stride, dilation):
     return ('k11',)
 
 
-def _wgrad(dy, xb, wb, stride, padding, dilation, cout=-1, cin=-1, wdt=torch.float32, sn=None):
+def _take_grad_dest(p, shape):
+    """The DDP bucket slice armed for parameter ``p``'s gradient (``parallel/ddp.py``
+    ``begin()``: ``p._iamd_grad_dest = (flat, offset)``), handed out ONCE per backward and only
+    while ``p`` has no gradient yet: k11 then writes the weight gradient straight into the
+    bucket and autograd adopts that view as ``p.grad`` (no copy into the bucket). A second use
+    of the weight in the same backward gets fresh memory (autograd sums the two)."""
+    if p is None:
+        return None
+    d = getattr(p, '_iamd_grad_dest', None)
+    if d is None or p.grad is not None or getattr(p, '_iamd_grad_dest_used', True):
+        return None
+    if tuple(p.shape) != tuple(shape) or p.dtype != torch.float32 or \
+            not p.is_contiguous(memory_format=_CL):
+        return None
+    p._iamd_grad_dest_used = True
+    flat, off = d
+    return flat[off:off + p.numel()].as_strided(p.size(), p.stride())
+
+
+def _wgrad(dy, xb, wb, stride, padding, dilation, cout=-1, cin=-1, wdt=torch.float32, sn=None,
+           dest=None):
     """Weight gradient: k11 or MIOpen wrw (``IMAGINAIRE_AMD_MFMA_WGRAD`` = 1 | 0 | auto; auto =
     the faster of the two per shape, timed by :func:`tune_pending` outside the backward and
     agreed across ranks). k11 returns the gradient already cropped to (cout, cin) and in the
     weight's dtype (bf16 for the bf16 spectral-norm / autocast weights): the crop and cast ride
     in its split-K sum. ``sn`` = (bf16 shadow, u, v, sigma) of a spectrally normalised weight
     (:class:`_MfmaConv2d`): k11 only, returning the fp32 gradient w.r.t. W."""
-    k11, miopen = _wgrad_fns(dy, xb, wb, stride, padding, dilation, cout, cin, wdt, sn=sn)
+    k11, miopen = _wgrad_fns(dy, xb, wb, stride, padding, dilation, cout, cin, wdt, sn=sn,
+                             dest=dest)
     mode = _MFMA_WGRAD if sn is None else '1'  # (the SN backward rides in k11's split-K sum)
     fl = 2.0 * dy.shape[0] * dy.shape[2] * dy.shape[3] * wb.numel()
     desc = _gemm_desc(xb, wb, stride, padding)

@@ -5,8 +5,11 @@ Replaces the reference's torch-DDP(``find_unused_parameters=True``) / apex-DDP
 designed around how the GAN trainers actually use their networks:
 
 * **flat bucketed gradients** — each bucket owns one contiguous fp32 buffer
-  and every parameter's ``.grad`` is a view into it, so a bucket is reduced
-  with ONE collective and never copied (gradient-as-bucket-view);
+  and every parameter's ``.grad`` ends up a view into it, so a bucket is
+  reduced with ONE collective (gradient-as-bucket-view);
+* **one communicator per network** — G and D each get their own native RCCL communicator
+  and side stream (``comm_tag``), so the two networks' bucket all-reduces never queue
+  behind each other on one stream;
 * **overlap with backward** — a post-accumulate-grad hook counts arrivals and
   launches the bucket's async all-reduce as soon as its last gradient lands,
   so the reduction of late layers rides xGMI while earlier layers are still
@@ -19,10 +22,14 @@ designed around how the GAN trainers actually use their networks:
   are per-link bound, so buckets are large (default 256 MB; 288 GB HBM makes
   that free) with a small first bucket to start communication early;
 * optional **bf16 wire format** (``comm_dtype=torch.bfloat16``) halves bytes;
-* **no bucket zero-fill / accumulate pass** — ``begin()`` leaves ``.grad`` unset, autograd
-  hands each parameter its fresh gradient and the hook copies it into the bucket slice
-  (one read + one write, instead of a 1.7 GB memset plus a read-modify-write accumulate per
-  SPADE G backward); slices of parameters that got no gradient are zeroed at launch;
+* **zero-copy weight gradients** — ``begin()`` leaves ``.grad`` unset and arms every
+  channels-last conv weight with its bucket slice (``p._iamd_grad_dest``): the k11 weight
+  gradient (ops/conv.py ``_take_grad_dest``) writes its split-K sum straight into the bucket
+  and autograd adopts that view as ``.grad``, so the hook has nothing to copy. Other gradients
+  (norm affine parameters, linear layers, a weight's second use in one backward) arrive in
+  fresh memory and the hook copies them into their slice — one read + one write, instead of a
+  bucket memset plus a read-modify-write accumulate; slices of parameters that got no gradient
+  are zeroed at launch;
 * the 1/world scaling rides in the collective (``ReduceOp.AVG`` on RCCL, probed once at
   construction) instead of a separate pass over every bucket;
 * **buffers** (SN u/v, BN running stats) are broadcast once at construction
@@ -89,7 +96,7 @@ def _comm_device(group, tensors):
 class DistributedDataParallel(nn.Module):
     def __init__(self, module, process_group=None, bucket_cap_mb=256, first_bucket_mb=16,
                  broadcast_buffers=False, comm_dtype=None, overlap=True, find_unused='global',
-                 **unused):
+                 comm_tag=None, **unused):
         super().__init__()
         assert find_unused in ('local', 'global'), find_unused
         self.find_unused = find_unused
@@ -105,6 +112,7 @@ class DistributedDataParallel(nn.Module):
         self._active = False
         self._avg = False
         self._native = None
+        self.n_copies = 0  # gradients the hook copied into their bucket (diagnostics / tests)
         if self.world > 1 or unused.get('_force_distributed', False):
             self.world = max(self.world, 1)
             self._force = True
@@ -114,7 +122,7 @@ class DistributedDataParallel(nn.Module):
             # Work objects, so a step holding them can be captured into a hipGraph
             from imaginaire_amd.parallel.rccl import native_comm_for
             if self.buckets and self.buckets[0].flat.is_cuda:
-                self._native = native_comm_for(process_group)
+                self._native = native_comm_for(process_group, comm_tag)
             self._avg = True if self._native is not None else self._probe_avg()
         else:
             self._force = False
@@ -186,11 +194,16 @@ class DistributedDataParallel(nn.Module):
             self.buckets.append(b)
         self._param_bucket = {}
         self._param_list = [p for b in self.buckets for p in b.params]
+        # weights whose gradient k11 can write straight into the bucket (4-D fp32 channels-last)
+        self._dest_params = []
         for bi, b in enumerate(self.buckets):
             for p, off in zip(b.params, b.offsets):
                 self._param_bucket[p] = (bi, off)
                 p.grad = _grad_view(b.flat, off, p)
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+                if p.dim() == 4 and p.dtype == torch.float32 and \
+                        p.is_contiguous(memory_format=torch.channels_last):
+                    self._dest_params.append((p, b.flat, off))
 
     # -- per-phase protocol -----------------------------------------------
     def begin(self):
@@ -206,6 +219,13 @@ class DistributedDataParallel(nn.Module):
             b.work = None
             for p in b.params:
                 p.grad = None
+        for p, flat, off in self._dest_params:
+            p._iamd_grad_dest = (flat, off)
+            p._iamd_grad_dest_used = False
+
+    def _disarm(self):
+        for p, _, _ in self._dest_params:
+            p._iamd_grad_dest = None
 
     def _on_grad(self, p):
         if not self._active:
@@ -216,6 +236,7 @@ class DistributedDataParallel(nn.Module):
         if g is not None and g.data_ptr() != view.data_ptr():
             view.copy_(g)
             p.grad = view
+            self.n_copies += 1
         self._used.add(p)
         if not self.overlap:
             return
@@ -278,6 +299,7 @@ class DistributedDataParallel(nn.Module):
                 b.work = None
         # every used parameter's .grad is its bucket view again (the hook re-pointed it)
         self._active = False
+        self._disarm()
         self._drop_unused_grads()
 
     def _drop_unused_grads(self):

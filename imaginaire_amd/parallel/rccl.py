@@ -115,14 +115,15 @@ def _verified(group):
     return None
 
 
-def native_comm_for(group=None):
-    """The cached :class:`NativeComm` of ``group`` when native collectives are wanted and
+def native_comm_for(group=None, tag=None):
+    """The cached :class:`NativeComm` of ``group`` (one per ``tag``: the DDP wrappers of G and
+    D each get their own communicator and side stream) when native collectives are wanted and
     possible (RCCL backend, HIP extension loaded), else None."""
     if not (native_comm_wanted() and dist.is_available() and dist.is_initialized()):
         return None
     if dist.get_backend(group) != 'nccl' or not _ext.available():
         return None
-    key = id(group) if group is not None else None
+    key = (id(group) if group is not None else None, tag)
     if key not in _COMMS:
         _COMMS[key] = _verified(group)
     return _COMMS[key]

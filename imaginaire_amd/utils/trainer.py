@@ -102,8 +102,8 @@ def wrap_model_and_optimizer(cfg, net_G, net_D, opt_G, opt_D):
     net_G_module = net_G.module if cfg.trainer.model_average else net_G
     if hasattr(net_G_module, 'custom_init'):
         net_G_module.custom_init()
-    net_G = _wrap_model(cfg, net_G)
-    net_D = _wrap_model(cfg, net_D)
+    net_G = _wrap_model(cfg, net_G, 'G')
+    net_D = _wrap_model(cfg, net_D, 'D')
     return net_G, net_D, opt_G, opt_D
 
 
@@ -130,7 +130,7 @@ def _find_unused_mode(cfg):
     return 'local' if getattr(cls, 'rank_uniform_control_flow', False) else 'global'
 
 
-def _wrap_model(cfg, model):
+def _wrap_model(cfg, model, tag=None):
     # IMAGINAIRE_AMD_FORCE_DIST=1: the distributed wrappers (bucketed DDP, SyncBN exchanges)
     # also on a one-rank process group, e.g. to capture and test the collective path on one GPU
     force = os.environ.get('IMAGINAIRE_AMD_FORCE_DIST') == '1'
@@ -149,7 +149,7 @@ def _wrap_model(cfg, model):
                                        overlap=(ddp != 'apex'),
                                        broadcast_buffers=getattr(cfg.trainer,
                                                                  'ddp_broadcast_buffers', False),
-                                       find_unused=_find_unused_mode(cfg))
+                                       find_unused=_find_unused_mode(cfg), comm_tag=tag)
     return WrappedModel(model)
 
 

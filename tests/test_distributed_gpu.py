@@ -337,6 +337,75 @@ def _rccl_world1_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+def _zero_copy_worker(rank, world, port, q):
+    import sys
+    import faulthandler
+    import torch.distributed as dist
+    faulthandler.dump_traceback_later(150, exit=True, file=sys.__stderr__)
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK='0', WORLD_SIZE='1',
+                      LOCAL_RANK='0')
+    torch.cuda.set_device(0)
+    dist.init_process_group('nccl', rank=0, world_size=1, device_id=torch.device('cuda', 0))
+    from imaginaire_amd.parallel import DistributedDataParallel
+    from imaginaire_amd.ops import conv as C
+    C._MFMA_MIN_BLOCKS = 0
+    cl = torch.channels_last
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = torch.nn.Conv2d(64, 128, 3, padding=1)
+            self.b = torch.nn.Conv2d(128, 128, 3, padding=1)  # used twice per forward
+            self.g = torch.nn.Parameter(torch.ones(128))       # not a conv weight: copied
+
+        def forward(self, x):
+            h = C.conv2d_act(x, self.a.weight, self.a.bias, 1, 1, 1, 0.2)
+            h = C.conv2d(h, self.b.weight, self.b.bias, 1, 1) * self.g.view(1, -1, 1, 1)
+            return C.conv2d(h, self.b.weight, None, 1, 1)
+
+    torch.manual_seed(0)
+    net = Net().cuda().to(memory_format=cl)
+    ref = Net().cuda().to(memory_format=cl)
+    ref.load_state_dict(net.state_dict())
+    ddp = DistributedDataParallel(net, _force_distributed=True)
+    x = torch.randn(2, 64, 16, 64, device='cuda').contiguous(memory_format=cl)
+    out = {}
+    for it in range(2):
+        ddp.begin()
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            y = net(x * (it + 1))
+        y.float().pow(2).mean().backward()
+        ddp.finish()
+        ref.zero_grad(set_to_none=True)
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            yr = ref(x * (it + 1))
+        yr.float().pow(2).mean().backward()
+        ok = True
+        for (n, p), pr in zip(net.named_parameters(), ref.parameters()):
+            bi, off = ddp._param_bucket[p]
+            view_ptr = ddp.buckets[bi].flat[off:].data_ptr()
+            ok &= p.grad.data_ptr() == view_ptr
+            ok &= bool(torch.allclose(p.grad, pr.grad, atol=1e-4, rtol=1e-3))
+        out[it] = ok
+    # copied by the hook: a.bias, b.bias, g, and b.weight (its two uses are summed by autograd,
+    # the first into the bucket) at most; a.weight lands in the bucket directly
+    out['copies'] = ddp.n_copies
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+def test_ddp_zero_copy_weight_gradients_world1():
+    """k11 writes conv weight gradients straight into the DDP bucket (ops/conv.py
+    _take_grad_dest): the parameter's .grad IS its bucket slice, the hook copies only the other
+    gradients, and the values equal the plain (undistributed) backward, including a weight used
+    twice in one backward."""
+    (_, out), = _spawn(_zero_copy_worker, 1)
+    assert out[0] and out[1], out
+    # per backward at most: a.bias, b.bias, g, b.weight -> 4; a.weight never (all five were
+    # copied before round 6: 10 over the two backwards)
+    assert out['copies'] <= 2 * 4, out
+
+
 def test_ddp_rccl_world1_buckets_avg_and_unused():
     """The bucketed DDP on a real RCCL communicator (world size 1, forced through the
     distributed path): ReduceOp.AVG is detected, hook-filled buckets reproduce the plain
