@@ -12,6 +12,13 @@ std::vector<at::Tensor> norm_stats(const at::Tensor& x, bool per_instance, doubl
                                    const c10::optional<at::Tensor>& running_var,
                                    const c10::optional<at::Tensor>& num_batches,
                                    double momentum);
+std::vector<at::Tensor> sync_stats_merge(const at::Tensor& allst, double eps,
+                                         const c10::optional<at::Tensor>& weight,
+                                         const c10::optional<at::Tensor>& bias,
+                                         const c10::optional<at::Tensor>& running_mean,
+                                         const c10::optional<at::Tensor>& running_var,
+                                         const c10::optional<at::Tensor>& num_batches,
+                                         double momentum);
 std::vector<at::Tensor> norm_bwd_coeffs(const at::Tensor& S1, const at::Tensor& S2,
                                         const at::Tensor& rstd,
                                         const c10::optional<at::Tensor>& weight,
@@ -255,6 +262,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sn_scale_backward", &iamd::sn_scale_backward, "spectral-norm W/sigma backward (k5d)",
         py::arg("grad"), py::arg("weight"), py::arg("u"), py::arg("v"), py::arg("sigma"),
         py::arg("shadow") = c10::optional<at::Tensor>());
+  m.def("sync_stats_merge", &iamd::sync_stats_merge,
+        "sync-BN: merge gathered per-rank (count, mean, var) rows + finalize (k1)",
+        py::arg("allst"), py::arg("eps"), py::arg("weight") = py::none(),
+        py::arg("bias") = py::none(), py::arg("running_mean") = py::none(),
+        py::arg("running_var") = py::none(), py::arg("num_batches") = py::none(),
+        py::arg("momentum") = 0.0);
   m.def("norm_stats", &iamd::norm_stats, "per-(group,channel) statistics (k1)",
         py::arg("x"), py::arg("per_instance"), py::arg("eps"), py::arg("weight"),
         py::arg("bias"), py::arg("partial_only"), py::arg("running_mean") = py::none(),

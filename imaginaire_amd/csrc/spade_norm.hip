@@ -254,6 +254,44 @@ stats_finalize(const float* __restrict__ pcnt, const float* __restrict__ pmean,
   if (num_batches != nullptr && idx == 0) num_batches[0] += 1;
 }
 
+// Sync-BN: merge the all-gathered per-rank (count, mean, var) rows allst [W][3][C] (Chan) and
+// finish like stats_finalize — global (count, mean, var), rstd, the affine scale / shift, and the
+// running statistics + batch counter in place — in ONE launch (PyTorch: ~25 one-element-per-
+// channel launches per sync-BN layer: the merge, rsqrt, scale / shift and the running update).
+__global__ void __launch_bounds__(256)
+sync_stats_merge_kernel(const float* __restrict__ allst, int W, int C, float eps,
+                        const float* __restrict__ weight, const float* __restrict__ bias,
+                        float* __restrict__ out_cnt, float* __restrict__ out_mean,
+                        float* __restrict__ out_var, float* __restrict__ out_rstd,
+                        float* __restrict__ out_scale, float* __restrict__ out_shift,
+                        float* __restrict__ run_mean, float* __restrict__ run_var,
+                        int64_t* __restrict__ num_batches, float factor) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float n_a = 0.f, mean_a = 0.f, m2_a = 0.f;
+  for (int w = 0; w < W; ++w) {
+    const float* r = allst + (int64_t)w * 3 * C;
+    const float n = r[c];
+    chan_merge(n_a, mean_a, m2_a, n, r[C + c], r[2 * C + c] * n);
+  }
+  const float var = n_a > 0.f ? m2_a / n_a : 0.f;
+  const float rstd = rsqrtf(var + eps);
+  out_cnt[c] = n_a;
+  out_mean[c] = mean_a;
+  out_var[c] = var;
+  out_rstd[c] = rstd;
+  const float a = weight ? weight[c] : 1.f;
+  const float b = bias ? bias[c] : 0.f;
+  out_scale[c] = rstd * a;
+  out_shift[c] = b - mean_a * rstd * a;
+  if (run_mean != nullptr) {
+    const float unb = var * n_a / fmaxf(n_a - 1.f, 1.f);
+    run_mean[c] = (1.f - factor) * run_mean[c] + factor * mean_a;
+    run_var[c] = (1.f - factor) * run_var[c] + factor * unb;
+  }
+  if (num_batches != nullptr && c == 0) num_batches[0] += 1;
+}
+
 // Backward coefficients of the k1 data gradient from the per-sample sums S1 = Σ g', S2 =
 // Σ g'·x̂ ([N, C] each) in one launch (PyTorch: 2 column sums, a stack, a multiply and two
 // divides with their copies per norm layer). Batch norm (per_instance 0): k1 = rstd·w, k2 =
@@ -767,6 +805,55 @@ std::vector<at::Tensor> norm_stats(const at::Tensor& x, bool per_instance, doubl
                      rmp, rvp, nbp, (float)momentum);
   IAMD_LAUNCH_CHECK();
   return {cnt, mean, var, scale, shift, rstd};
+}
+
+// Sync-BN merge of the gathered [W, 3, C] (count, mean, var) rows: returns (count, mean, var,
+// rstd, scale, shift), each [1, C] fp32; running_mean / running_var (fp32 [C]) and num_batches
+// (int64 [1]) are updated in place when given.
+std::vector<at::Tensor> sync_stats_merge(const at::Tensor& allst, double eps,
+                                         const c10::optional<at::Tensor>& weight,
+                                         const c10::optional<at::Tensor>& bias,
+                                         const c10::optional<at::Tensor>& running_mean,
+                                         const c10::optional<at::Tensor>& running_var,
+                                         const c10::optional<at::Tensor>& num_batches,
+                                         double momentum) {
+  IAMD_CHECK(allst.is_cuda() && allst.scalar_type() == at::kFloat && allst.dim() == 3 &&
+                 allst.size(1) == 3 && allst.is_contiguous(),
+             "sync_stats_merge: contiguous fp32 [W, 3, C] rows expected");
+  const int W = (int)allst.size(0), C = (int)allst.size(2);
+  auto fopt = allst.options();
+  auto cnt = at::empty({1, C}, fopt), mean = at::empty({1, C}, fopt), var = at::empty({1, C}, fopt);
+  auto rstd = at::empty({1, C}, fopt), scale = at::empty({1, C}, fopt),
+       shift = at::empty({1, C}, fopt);
+  at::Tensor wf, bf;
+  if (weight.has_value() && weight->defined()) wf = weight->contiguous().to(at::kFloat);
+  if (bias.has_value() && bias->defined()) bf = bias->contiguous().to(at::kFloat);
+  float *rmp = nullptr, *rvp = nullptr;
+  int64_t* nbp = nullptr;
+  if (running_mean.has_value() && running_mean->defined()) {
+    IAMD_CHECK(running_var.has_value() && running_var->defined() &&
+                   running_mean->scalar_type() == at::kFloat &&
+                   running_var->scalar_type() == at::kFloat && running_mean->is_contiguous() &&
+                   running_var->is_contiguous() && running_mean->numel() == C &&
+                   running_var->numel() == C,
+               "sync_stats_merge: fp32 contiguous running statistics expected");
+    rmp = running_mean->data_ptr<float>();
+    rvp = running_var->data_ptr<float>();
+  }
+  if (num_batches.has_value() && num_batches->defined()) {
+    IAMD_CHECK(num_batches->scalar_type() == at::kLong && num_batches->numel() == 1,
+               "sync_stats_merge: int64 batch counter expected");
+    nbp = num_batches->data_ptr<int64_t>();
+  }
+  hipLaunchKernelGGL(sync_stats_merge_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, stream(),
+                     allst.data_ptr<float>(), W, C, (float)eps,
+                     wf.defined() ? wf.data_ptr<float>() : nullptr,
+                     bf.defined() ? bf.data_ptr<float>() : nullptr, cnt.data_ptr<float>(),
+                     mean.data_ptr<float>(), var.data_ptr<float>(), rstd.data_ptr<float>(),
+                     scale.data_ptr<float>(), shift.data_ptr<float>(), rmp, rvp, nbp,
+                     (float)momentum);
+  IAMD_LAUNCH_CHECK();
+  return {cnt, mean, var, rstd, scale, shift};
 }
 
 // (k1, k2, k3, dweight, dbias) of the k1 backward from the per-sample sums (see kernel)

@@ -71,6 +71,14 @@ def _gather_rows(allst, stacked, group, async_op=False):
     return dist.all_gather(bufs, stacked, group=group, async_op=async_op)
 
 
+def _gather_local(cnt, mean, var, group):
+    """This rank's (count, mean, var) [1, C] rows all-gathered into [W, 3, C] (one collective)."""
+    stacked = torch.stack([cnt.reshape(-1), mean.reshape(-1), var.reshape(-1)], 0).contiguous()
+    allst = stacked.new_empty((_world(group),) + tuple(stacked.shape))
+    _gather_rows(allst, stacked, group)
+    return allst
+
+
 def _merge_stats(cnt, mean, var, group):
     """All-gather per-rank (count, mean, var) [1, C] and merge (Chan)."""
     stacked = torch.stack([cnt.reshape(-1), mean.reshape(-1), var.reshape(-1)], 0).contiguous()
@@ -105,7 +113,11 @@ def _cached_stats(x, key):
     if c[1] == 'pending':
         work, allst, local = c[2], c[3], c[4]
         work.wait()
-        stats = _merge_gathered(allst, local)
+        if allst.is_cuda and _ext.available():
+            # (count, mean, var, rstd, scale, shift) of the param-free norm in one launch
+            stats = tuple(_ext.ext().sync_stats_merge(allst, key[1]))
+        else:
+            stats = _merge_gathered(allst, local)
         x._iamd_bn_stats = (key, 'done', stats)
         return stats
     return c[2]
@@ -221,9 +233,8 @@ class _SyncBwdJoin(torch.autograd.Function):
             return g, None
         h.work.wait()
         x, dout, scale, shift, mean, rstd, k1, M, gamma_v, beta_v, slope = h.args
-        s = h.sums
-        k2 = (s[0:1] / M).contiguous()
-        k3 = (s[1:2] / M).contiguous()
+        k = h.sums / M
+        k2, k3 = k[0:1], k[1:2]
         h.args = h.work = h.sums = None
         DeferredSyncBwd.completed += 1
         dx = _ext.ext().norm_bwd_apply(x, dout, scale, shift, mean, rstd, k1, k2, k3,
@@ -295,11 +306,19 @@ class _FusedNormActFn(torch.autograd.Function):
                     if fold:
                         updated = True
                     if sync:
-                        count, mean, var = _merge_stats(count, mean, var, cfg.group)
-                        rstd = None
+                        # one gather, then ONE kernel: merge + rsqrt + scale / shift + running
+                        # statistics and batch counter (ops that were ~25 PyTorch launches)
+                        fold_r = cfg.training and not per_instance and \
+                            _native_running(running_mean, running_var, cfg)
+                        allst = _gather_local(count, mean, var, cfg.group)
+                        count, mean, var, rstd, scale, shift = ext.sync_stats_merge(
+                            allst, cfg.eps, wf, bf, running_mean if fold_r else None,
+                            running_var if fold_r else None,
+                            cfg.num_batches if fold_r else None, float(cfg.momentum))
+                        updated = fold_r
                 if rstd is None:
                     rstd = torch.rsqrt(var + cfg.eps)
-                if sync or scale is None:
+                if scale is None:
                     a = wf.reshape(1, C) if wf is not None else 1.0
                     b = bf.reshape(1, C) if bf is not None else 0.0
                     scale = (rstd * a).contiguous()
@@ -381,8 +400,16 @@ class _FusedNormActFn(torch.autograd.Function):
             dx = ext.norm_bwd_apply(x, dout, scale, shift, mean, rstd, k1, k2, k3, gamma_v,
                                     beta_v, cfg.slope) if ctx.needs_input_grad[0] else None
             return dx, dweight, dbias, dgamma, dbeta, dgb, None, None, None
-        dweight = S2.sum(0).to(weight.dtype) if need_dw else None
-        dbias = S1.sum(0).to(weight.dtype if weight is not None else torch.float32) \
+        batch_sums = cfg.mode not in ('none', 'instance') and cfg.use_batch_stats
+        s_loc = None
+        if need_dw or need_db or batch_sums:
+            # [2, C] = (Σ_N S1, Σ_N S2): one reduction feeds dbias, dweight and k2 / k3
+            base = S1._base  # norm_bwd_reduce returns rows of one [Q, N, C] buffer
+            both = base[:2] if (base is not None and base.dim() == 3 and
+                                base[1].data_ptr() == S2.data_ptr()) else torch.stack([S1, S2], 0)
+            s_loc = both.sum(1)
+        dweight = s_loc[1].to(weight.dtype) if need_dw else None
+        dbias = s_loc[0].to(weight.dtype if weight is not None else torch.float32) \
             if need_db else None
         if cfg.mode == 'none' or not cfg.use_batch_stats:
             # no batch statistics in the graph: dx = g * scale
@@ -395,7 +422,8 @@ class _FusedNormActFn(torch.autograd.Function):
             k2 = (S1 / HW).contiguous()
             k3 = (S2 / HW).contiguous()
         else:
-            s = torch.stack([S1.sum(0), S2.sum(0)], 0)
+            # (the exchange is in place: keep the local sums dweight / dbias may alias)
+            s = s_loc.clone() if sync else s_loc
             M = ctx.count.reshape(1, C) if sync else float(N * HW)
             k1 = (rstd * (weight.float().reshape(1, C) if weight is not None else 1.0)).contiguous()
             h = cfg.deferred
@@ -408,8 +436,8 @@ class _FusedNormActFn(torch.autograd.Function):
                 return dx, dweight, dbias, dgamma, dbeta, dgb, None, None, None
             if sync:
                 _all_reduce_sums(s, cfg.group)
-            k2 = (s[0:1] / M).contiguous()
-            k3 = (s[1:2] / M).contiguous()
+            k = s / M
+            k2, k3 = k[0:1], k[1:2]
         mean_b, rstd_b = mean, rstd
         dx = ext.norm_bwd_apply(x, dout, scale, shift, mean_b, rstd_b, k1, k2, k3,
                                 gamma_v, beta_v, cfg.slope) if ctx.needs_input_grad[0] else None

@@ -113,6 +113,8 @@ class DistributedDataParallel(nn.Module):
         self._avg = False
         self._native = None
         self.n_copies = 0  # gradients the hook copied into their bucket (diagnostics / tests)
+        self._pending = {}
+        self._bidx = None
         if self.world > 1 or unused.get('_force_distributed', False):
             self.world = max(self.world, 1)
             self._force = True
@@ -194,6 +196,8 @@ class DistributedDataParallel(nn.Module):
             self.buckets.append(b)
         self._param_bucket = {}
         self._param_list = [p for b in self.buckets for p in b.params]
+        self._bidx = {id(b): i for i, b in enumerate(self.buckets)}
+        self._pending = {i: {} for i in range(len(self.buckets))}
         # weights whose gradient k11 can write straight into the bucket (4-D fp32 channels-last)
         self._dest_params = []
         for bi, b in enumerate(self.buckets):
@@ -212,6 +216,8 @@ class DistributedDataParallel(nn.Module):
             return
         self._active = True
         self._used = set()
+        for bi in self._pending:
+            self._pending[bi] = {}
         for b in self.buckets:
             b.arrived = 0
             b.expected = sum(1 for p in b.params if p.requires_grad)
@@ -234,8 +240,10 @@ class DistributedDataParallel(nn.Module):
         view = _grad_view(self.buckets[bi].flat, off, p)
         g = p.grad
         if g is not None and g.data_ptr() != view.data_ptr():
-            view.copy_(g)
-            p.grad = view
+            # deferred: the bucket's pending copies run as ONE multi-tensor copy at launch
+            # (a SPADE step hands ~270 small bias / norm gradients to this hook). p.grad stays
+            # the autograd tensor until then, so a second accumulation lands in it.
+            self._pending[bi][p] = view
             self.n_copies += 1
         self._used.add(p)
         if not self.overlap:
@@ -246,8 +254,18 @@ class DistributedDataParallel(nn.Module):
         if b.arrived == b.expected and not b.launched:
             self._launch(b)
 
+    def _flush_copies(self, bi):
+        pend = self._pending[bi]
+        if pend:
+            views = list(pend.values())
+            torch._foreach_copy_(views, [p.grad for p in pend])
+            for p, v in pend.items():
+                p.grad = v
+            self._pending[bi] = {}
+
     def _launch(self, b):
         b.launched = True
+        self._flush_copies(self._bidx[id(b)])
         if b.expected == 0:
             return
         # slices of parameters without a gradient this backward hold the previous step's
@@ -283,6 +301,8 @@ class DistributedDataParallel(nn.Module):
         for b in self.buckets:
             if not b.launched and b.expected > 0:
                 self._launch(b)
+        for bi in self._pending:  # (buckets with no expected gradient)
+            self._flush_copies(bi)
         inv = 1.0 / self.world
         for b in self.buckets:
             if b.work is not None:

@@ -10,8 +10,8 @@ for arm in plain forced; do
   extra=""; [ $arm = forced ] && extra="--force-dist"
   rm -rf /tmp/iamd_prof_$arm
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/iamd_prof_$arm \
-    -o bench -- python3 "$ROOT/bench.py" --steps 3 --warmup 4 $extra > "$OUT/bench_$arm.log" 2>&1
+    -o bench -- python3 "$ROOT/bench.py" --steps 3 --warmup 4 --verbose $extra > "$OUT/bench_$arm.log" 2>&1
   rc=$?; echo "[prof] $arm rc=$rc"; [ $rc -eq 0 ] || exit $rc
-  python3 "$ROOT/scripts/gpu/summarize_kernels.py" /tmp/iamd_prof_$arm > "$OUT/kernels_$arm.txt" || true
-  head -45 "$OUT/kernels_$arm.txt"
+  SUMMARY_ROWS=400 python3 "$ROOT/scripts/gpu/summarize_kernels.py" /tmp/iamd_prof_$arm > "$OUT/kernels_$arm.txt" || true
+  head -12 "$OUT/kernels_$arm.txt"
 done
