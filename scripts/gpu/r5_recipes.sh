@@ -7,7 +7,7 @@
 # breakdown starts at the steady-state marker bench_families.py emits after warm-up.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 ROOT=$(pwd)
-OUT=$ROOT/gpurun_out/r5rec
+OUT=${OUTDIR:-$ROOT/gpurun_out/r5rec}
 mkdir -p "$OUT"
 : > "$OUT/recipes.jsonl"
 REPS=${REPS:-2}
