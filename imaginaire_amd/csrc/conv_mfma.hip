@@ -1308,7 +1308,9 @@ bool v4_eligible(const ConvArgs& a) {
     const char* e = std::getenv("IMAGINAIRE_AMD_CONV_V4");  // 0: A/B switch back to v1 / v3
     return e != nullptr && e[0] == '0';
   }();
-  return !off && a.nz == 1 && a.omode == 0 && a.sh == 1 && a.sw == 1 && a.dh == 1 && a.dw == 1 &&
+  // (Cin = 32 runs on the row-window tile only: v4 / v5 step 64-channel k-chunks)
+  return !off && a.Cin % kBK == 0 && a.nz == 1 && a.omode == 0 && a.sh == 1 && a.sw == 1 &&
+         a.dh == 1 && a.dw == 1 &&
          (a.KW >= 3 && a.KW <= 5) && a.KH <= 31 && a.Cout % 128 == 0 &&
          (a.Wo % 256 == 0 || (a.Wo >= 16 && a.Wo <= 128 && 256 % a.Wo == 0)) &&
          ((int64_t)a.Ho * a.Wo) % 256 == 0;

@@ -426,6 +426,13 @@ def _strided_dgrad(dy, wb, H, W, s, padding, wts=None, ncv=-1, ascale=None):
 # stream (51.1-51.2 vs 52.2 images/s back to back, gpurun_out r4t) — the large dgrad and wgrad
 # grids each fill the chip, and sharing it costs both more than the launch gaps it hides.
 _OVERLAP_BWD = os.environ.get('IMAGINAIRE_AMD_CONV_BWD_OVERLAP', '0')  # '1' | 'bias' | '0'
+# 'small[:P]': the weight gradient goes to the side stream only for convs of at most P output
+# pixels (default 8192: SPADE's 16x32 / 32x64 layers at batch 4), whose split-K grids leave CUs
+# idle, and only where its spectral-norm <G, W> comes from the k11 epilogue anyway
+_OVERLAP_SMALL_PIX = int(_OVERLAP_BWD.split(':')[1]) if _OVERLAP_BWD.startswith('small:') \
+    else 8192
+if _OVERLAP_BWD.startswith('small'):
+    _OVERLAP_BWD = 'small'
 # spectral-norm weight gradient: <G, W> from the data gradient (sigma <dx, x>, one bandwidth
 # pass over dx and x) when the input has at most this many times the weight's elements, else in
 # the k11 epilogue (which re-reads W once per split-K slab). 0: always the epilogue.
@@ -436,7 +443,7 @@ _BWD_SIDE = {}
 def _bwd_side_stream():
     """The per-device side stream of the conv backward's weight gradients (None when off, in
     the conv log's timing mode, or under the eager reference path)."""
-    if _OVERLAP_BWD not in ('1', 'bias') or _CONV_LOG is not None:
+    if _OVERLAP_BWD not in ('1', 'bias', 'small') or _CONV_LOG is not None:
         return None
     dev = torch.cuda.current_device()
     st = _BWD_SIDE.get(dev)
@@ -517,6 +524,11 @@ class _MfmaConv2d(torch.autograd.Function):
         # concurrently with the data gradient: they are independent, and the small convs'
         # grids leave most CUs idle on their own
         side = _bwd_side_stream() if (need_x and (need_w or need_b)) else None
+        if side is not None and _OVERLAP_BWD == 'small' and (
+                dy.shape[0] * dy.shape[2] * dy.shape[3] > _OVERLAP_SMALL_PIX or not need_w or
+                (sn is not None and _SN_DOT_RATIO > 0 and
+                 xb.numel() <= _SN_DOT_RATIO * wb.numel())):
+            side = None
         side_bias = side is not None and slope == 1.0 and need_b
         if slope != 1.0:
             dy = _pad_channels(dy, y.shape[1], torch.bfloat16)
@@ -546,7 +558,7 @@ class _MfmaConv2d(torch.autograd.Function):
             with torch.cuda.stream(side):
                 if side_bias:  # bias gradient only: the k2 kernel reads dy, writes no dx
                     db = _ext.ext().bias_act_bwd(dy, dy, 1.0)[1]
-                if need_w_left and _OVERLAP_BWD == '1':
+                if need_w_left and _OVERLAP_BWD in ('1', 'small'):
                     dw = _wgrad(dy, xb, wb, stride, padding, dilation, cout, cin, wdt, sn)
         if need_x_left:
             pt = (dilation[0] * (kh - 1) - padding[0], dilation[1] * (kw - 1) - padding[1])

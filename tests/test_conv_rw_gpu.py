@@ -142,6 +142,20 @@ def test_rw_taken_by_default_for_long_filters():
         assert var == 6, (case, var)
 
 
+def test_cin32_never_takes_the_64_channel_tiles():
+    """A Cin = 32 conv of a shape v4 / v5 take at Cin >= 64 (3x3 stride 1, Cout % 128 == 0,
+    64-pixel rows) routes to the row-window tile: the v4 / v5 k loops step 64-channel chunks."""
+    from imaginaire_amd.ops import _ext
+    X = _ext.ext()
+    case = (2, 32, 128, 16, 64, 3, 3, 1, 1)
+    x, w, b = _inputs(case, seed=9)
+    y, var = _run(X, x, w, b, 1, 1, ver='0')
+    assert var == 6, var
+    ref = F.leaky_relu(F.conv2d(x.float(), w.float(), b, 1, 1), 0.2)
+    err = (y.float() - ref).abs().max().item()
+    assert err <= 1e-2 * max(1.0, ref.abs().max().item()), err
+
+
 # ---- tap-packed thin-input convolutions (csrc/im2col.hip + 1x1 k10 / k11) -----------------
 # B, Cin, Cout, H, W, k, stride, pad, x layout
 PACK_CASES = [
