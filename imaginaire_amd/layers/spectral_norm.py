@@ -174,6 +174,35 @@ class _SNGroup:
     def __init__(self, net, sub=False):
         self.sub = sub
         self.entries = self._collect(net)
+        self._snap = None  # (u, v) before this network forward's first iteration
+
+    def finish(self, net, inputs, output):
+        """Forward hook of the network: a layer the forward did NOT call gets its u / v back
+        (the reference iterates a layer only when it runs — e.g. vid2vid's previous-frame
+        encoder, idle on the first frame), and no stale σ is left pending for a later call."""
+        snap, self._snap = self._snap, None
+        if snap is None:
+            return
+        idle = [i for i, (_, h) in enumerate(self.entries) if getattr(h, '_batched', None)
+                is not None]
+        if not idle:
+            return
+        su, sv = snap
+        dst, src = [], []
+        ou = ov = 0
+        offs = []
+        for m, h in self.entries:
+            u, v = getattr(m, h.name + '_u'), getattr(m, h.name + '_v')
+            offs.append((ou, ov, u, v))
+            ou += u.numel()
+            ov += v.numel()
+        for i in idle:
+            o_u, o_v, u, v = offs[i]
+            dst += [u, v]
+            src += [su[o_u:o_u + u.numel()], sv[o_v:o_v + v.numel()]]
+            self.entries[i][1]._batched = None
+        with torch.no_grad():
+            torch._foreach_copy_(dst, src)
 
     @staticmethod
     def _collect(net):
@@ -207,6 +236,8 @@ class _SNGroup:
         eps = float(self.entries[0][1].eps)
         bf16 = _autocast_bf16(w0.device.type)
         with torch.no_grad():
+            if net.training and not self.sub and self._snap is None:
+                self._snap = (torch.cat(us), torch.cat(vs))
             shadows = self._shadows(ws) if (bf16 and net.training and _SN_SHADOW) else None
             fused = False
             if shadows is not None:
@@ -325,6 +356,7 @@ def install_batched_spectral_norm(net):
     group = _SNGroup(net)
     if group.entries:
         net.register_forward_pre_hook(group)
+        net.register_forward_hook(group.finish)
         net._iamd_sn_group = group
         for m in net.modules():
             if m is net or any(isinstance(h, _SNGroup) for h in m._forward_pre_hooks.values()):

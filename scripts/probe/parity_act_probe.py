@@ -21,6 +21,9 @@ import test_model_parity_gpu as P  # noqa: E402
 import imaginaire_amd.utils.trainer as T  # noqa: E402
 
 
+ALL = os.environ.get('ACT_ALL', '1') == '1'  # composite modules too (post-order)
+
+
 def _cos(a, b):
     a, b = a.reshape(-1).double(), b.reshape(-1).double()
     return float(torch.dot(a, b) / (a.norm() * b.norm()).clamp_min(1e-30))
@@ -50,7 +53,7 @@ def record(config, amp, eager, tmp, seq_len, cudnn=None):
         tr = orig(cfg, net_G, net_D, *a, **kw)
         for tag, net in (('G', tr.net_G), ('D', tr.net_D)):
             for name, m in net.named_modules():
-                if len(list(m.children())) or not name:
+                if not name or (not ALL and len(list(m.children()))):
                     continue
                 key = tag + ':' + name.replace('module.', '')
 
@@ -99,6 +102,13 @@ def main():
         cm = _cos(a, b)
         out.append((order, k, n, c, ch, cm, float(t.norm()), float(a.norm())))
     print('%d hip records, %d compared' % (len(hip), len(out)))
+    dump = os.environ.get('ACT_DUMP')  # 'a:b': every compared row with execution index in [a, b)
+    if dump:
+        a, b = (int(v) for v in dump.split(':'))
+        for r in out:
+            if a <= r[0] < b:
+                print('  =%5d %s %-70s call %d  cos(hip, torch) %.6f  mutual %.6f  |hip| %.5g '
+                      '|torch| %.5g' % r)
     bad = [r for r in out if (1 - r[4]) > 3 * (1 - r[5]) + 1e-3]
     print('rows where HIP is further from torch-bf16 than 3x the torch-bf16 mutual distance '
           '(execution order):')

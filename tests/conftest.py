@@ -1,7 +1,12 @@
 import os
 import sys
 
-import pytest
+# before anything in this process starts HIP (collection below calls torch.cuda.is_available):
+# the runtime reads this once at start-up, and imaginaire_amd refuses graph capture when HIP
+# started with packet capture on (profiles/r6/README_graph_root_cause.txt)
+os.environ.setdefault('DEBUG_CLR_GRAPH_PACKET_CAPTURE', '0')
+
+import pytest  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:

@@ -126,3 +126,46 @@ def test_sn_fused_conv_matches_materialised_and_fp32(monkeypatch, dot_ratio):
                     fb.copy_(b)
     finally:
         snm._SN_FUSED, snm._SN_SHADOW = old_fused, old_shadow
+
+
+def test_sn_group_leaves_idle_layers_alone():
+    """The batched power iteration runs for every SN layer of the network, but a layer the
+    forward does not call keeps its u / v (the reference iterates a layer only when it runs —
+    vid2vid's previous-frame encoder is idle on the first frame); the called layers advance
+    exactly one iteration, as torch's spectral_norm does."""
+    from imaginaire_amd.layers import Conv2dBlock
+    from imaginaire_amd.layers import spectral_norm as snm
+
+    class Two(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = Conv2dBlock(64, 64, 3, 1, 1, weight_norm_type='spectral')
+            self.b = Conv2dBlock(64, 64, 3, 1, 1, weight_norm_type='spectral')
+
+        def forward(self, x, use_b):
+            x = self.a(x)
+            return self.b(x) if use_b else x
+
+    torch.manual_seed(5)
+    net = Two().cuda().to(memory_format=torch.channels_last)
+    ref = Two().cuda().to(memory_format=torch.channels_last)
+    ref.load_state_dict(net.state_dict())
+    assert snm.install_batched_spectral_norm(net) == 2
+    x = torch.randn(2, 64, 16, 16, device='cuda').contiguous(memory_format=torch.channels_last)
+    bufs = lambda m: {k: v.clone() for k, v in m.state_dict().items()  # noqa: E731
+                      if k.endswith(('_u', '_v'))}
+    for use_b in (False, True, False):
+        before = bufs(net)
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            net(x, use_b).float().sum().backward()
+        with torch.autocast('cuda', enabled=False):
+            ref(x.float(), use_b)  # torch spectral_norm on the CPU-free fallback path
+        after, want = bufs(net), bufs(ref)
+        for k in after:
+            idle = k.startswith('b.') and not use_b
+            if idle:
+                assert torch.equal(after[k], before[k]), (use_b, k)
+            else:
+                assert not torch.equal(after[k], before[k]), (use_b, k)
+            # (the batched iteration's GEMVs read the bf16 shadow of W: ~1e-3 relative)
+            torch.testing.assert_close(after[k], want[k], rtol=2e-2, atol=2e-3)
