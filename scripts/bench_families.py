@@ -34,6 +34,8 @@ def main():
                    help='video families: frames per training sequence')
     p.add_argument('--pool', type=int, default=2)
     p.add_argument('--cpu', action='store_true', help='plumbing check on the CPU')
+    p.add_argument('--no-pipelined', dest='pipelined', action='store_false',
+                   help='skip the second timed block (synchronised at its ends only)')
     p.add_argument('--op-sites', action='store_true',
                    help='after the timed steps, attribute the aten glue of one more iteration '
                         'to Python call sites (scripts/probe/op_sites.py) on stderr')
@@ -264,6 +266,25 @@ def main():
         dt = float(t.item())
     st = sorted(times)
     med = st[len(st) // 2] if len(st) % 2 else 0.5 * (st[len(st) // 2 - 1] + st[len(st) // 2])
+    # the same number of iterations again, synchronised only at both ends (as train.py runs:
+    # the host prepares iteration i + 1 while the GPU still runs iteration i); the loop above
+    # makes the GPU wait for each iteration's host-side batch preparation and graph launch
+    dt_pipe = None
+    if args.pipelined and not args.ab_eager:
+        if world > 1:
+            dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        for it in range(args.steps):
+            data = step(args.warmup + args.steps + it)
+        sync()
+        if world > 1:
+            dist.barrier()
+        dt_pipe = (time.perf_counter() - t0) / args.steps
+        if world > 1:
+            t = torch.tensor([dt_pipe], dtype=torch.float64, device=coll_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt_pipe = float(t.item())
     if args.op_sites and device.type == 'cuda':
         sys.path.insert(0, os.path.join(HERE, 'probe'))
         from op_sites import record_sites
@@ -312,7 +333,7 @@ def main():
     sys.stdout = real_stdout
     if rank == 0:
         _print_row(args, cfg, ds, bs, frames, dt, med, st, device, graphed, losses, finite,
-                   world, in_sync)
+                   world, in_sync, dt_pipe)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -326,7 +347,7 @@ def main():
 
 
 def _print_row(args, cfg, ds, bs, frames, dt, med, st, device, graphed, losses, finite, world,
-               in_sync):
+               in_sync, dt_pipe=None):
     import torch
     h, w = ds.h, ds.w
     print(json.dumps({
@@ -341,6 +362,9 @@ def _print_row(args, cfg, ds, bs, frames, dt, med, st, device, graphed, losses, 
         'timed_iterations': args.steps, 'warmup': args.warmup,
         'median_ms': round(med * 1e3, 2), 'min_ms': round(st[0] * 1e3, 2),
         'max_ms': round(st[-1] * 1e3, 2),
+        # (sync only at the ends of the second timed block: see main)
+        'ms_per_iteration_pipelined': round(dt_pipe * 1e3, 2) if dt_pipe else None,
+        'frames_per_s_pipelined': round(world * bs * frames / dt_pipe, 3) if dt_pipe else None,
         'spread_pct': round(100.0 * (st[-1] - st[0]) / med, 2),
         'median_frames_per_s': round(world * bs * frames / med, 3),
         'routing': _routing(),

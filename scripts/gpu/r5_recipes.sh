@@ -9,6 +9,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 ROOT=$(pwd)
 OUT=${OUTDIR:-$ROOT/gpurun_out/r5rec}
 mkdir -p "$OUT"
+OUT=$(cd "$OUT" && pwd)  # (absolute: the profiling runs start from /tmp)
 : > "$OUT/recipes.jsonl"
 REPS=${REPS:-2}
 STEPS=${STEPS:-20}
