@@ -149,4 +149,6 @@ conv_splitk_reduce(const float* __restrict__ part, const float* __restrict__ bia
 // true when the shape is eligible (IMAGINAIRE_AMD_CONV_RW != 0), else launches nothing.
 bool run_rw(ConvArgs& a, const at::Tensor& x, bool forced);
 bool rw_eligible(const ConvArgs& a);
+// the narrow row-window variant is switched on for this shape (IMAGINAIRE_AMD_CONV_RW_SMALL=1)
+bool rw_small_pref(const ConvArgs& a);
 }  // namespace iamd

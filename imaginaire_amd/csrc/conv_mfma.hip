@@ -1486,7 +1486,7 @@ void run_conv(ConvArgs& a, const at::Tensor& x) {
   // blocks overlap one tile's loads with the other's epilogue, and those convs are latency /
   // bandwidth bound (0.55-0.86x, profiles/conv_rw_probe_mi355x.txt).
   const int64_t kfull = (int64_t)KH * KW * a.Cin;
-  const bool rw_pref = a.Cin == 32 ||
+  const bool rw_pref = a.Cin == 32 || rw_small_pref(a) ||
                        (a.KW >= 3 && ((a.sh == 1 && kfull >= 2048) || (a.sh == 2 && kfull >= 6144)));
   if ((ver == 6 || (ver == 0 && rw_pref)) && run_rw(a, x, ver == 6 || a.Cin == 32)) {
     g_last_conv_variant = 6;

@@ -9,10 +9,13 @@
 // the kernel time of the MUNIT / FUNIT / pix2pixHD / vid2vid recipes). This tile
 // takes all of them:
 //
-//   * GEMM rows are VIRTUAL output pixels: segments of SW (a power of two, 16..BM) consecutive
-//     pixels of one output row, nct = ceil(Wo / SW) segments per row, the pixels past Wo masked
-//     (zero window rows in, no store out). Any output width maps onto whole segments, and a
-//     16-row MFMA fragment never straddles two segments.
+//   * GEMM rows are VIRTUAL output pixels: R = floor(BM / SW) segments of SW (16..BM)
+//     consecutive pixels of one output row, nct = ceil(Wo / SW) segments per row, the pixels
+//     past Wo and the block's rows past R * SW masked (zero window rows in, no store out). SW is
+//     a power of two where one wastes <= 10% of the rows, else any width that wastes least
+//     (a 66-wide data gradient of a reflect-padded 3x3 conv: 3 x 22-pixel segments per row,
+//     11 per block, 94.5% of the rows live, against <= 82% for every power of two); the window
+//     row of each lane's fragment row is computed per lane, so a fragment may straddle segments.
 //   * Per segment the block stages the input pixels every tap of one filter row reads, once per
 //     (filter row, channel block) "outer step", with buffer_load ... lds (out-of-image pixels
 //     and dead segments load zeros from the buffer unit). Window layouts (LDS rows of 128 B):
@@ -59,14 +62,17 @@ __device__ __forceinline__ int rw_tapoff(int kx, int Ph) {
 
 // S: stride (1 | 2). KW: filter taps per row (PAIR: virtual taps = ceil(real KW / 2)).
 // BN: output channels per block (64 | 128). PAIR: Cin == 32.
-template <int S, int KW, int BN, bool PAIR>
-__global__ __launch_bounds__(512, 1) void conv_fwd_rw(ConvArgs a) {
+// BMT / NR: block rows (256 | 128) and window DMA rounds (5 | 3). The narrow variant (stride 1,
+// BN 64, BMT 128, NR 3: 72 KB of LDS) runs two blocks per CU, so one block's loads overlap the
+// other's epilogue on the short-K convs (3x3 over 64 channels: 9 tap steps per block).
+template <int S, int KW, int BN, bool PAIR, int BMT, int NR>
+__global__ __launch_bounds__(512, (BMT == 128 && S == 1) ? 2 : 1) void conv_fwd_rw(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  constexpr int BM = S == 1 ? 256 : 128;
+  constexpr int BM = BMT;
   constexpr int MI = BM / 64;                   // 16-row fragments per wave (BM / 4 rows)
   constexpr int NI = BN / 32;                   // 16-column fragments per wave (BN / 2 cols)
   constexpr bool DEINT = S == 2 && !PAIR;
-  constexpr int kAbytes = kNR * 64 * kRowBytes;  // 40 KB per window buffer
+  constexpr int kAbytes = NR * 64 * kRowBytes;  // 40 / 24 KB per window buffer
   constexpr int kBbytes = BN * kRowBytes;        // 8 / 16 KB per weight slot
   constexpr int WB = BN / 64;                    // weight glds per thread per tap step
   constexpr int kBoff = 2 * kAbytes;
@@ -81,8 +87,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rw(ConvArgs a) {
   const int mt = bid / a.nNt, nt = bid - mt * a.nNt;
   const int n0 = nt * BN;
   const int SW = a.SW, P = a.P, Ph = a.Ph;
-  const int swl = __builtin_ctz(SW);  // SW is a power of two
-  const int R = BM >> swl;
+  const int R = BM / SW;  // (segment decodes below divide once per lane, outside the loop)
   const int g0 = mt * R;  // first segment of this block
 
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
@@ -96,10 +101,10 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rw(ConvArgs a) {
   const int rowbytes = a.W * a.Cin * 2;
   // (P is a multiple of 8, so the 8 rows a wave moves per round lie in ONE segment: the
   // segment decode and the filter-row mask are wave-uniform scalar work, once per round)
-  uint32_t a_off[kNR];
-  uint32_t a_km[kNR];  // bit ky: filter row ky of this round's rows reads inside the image
+  uint32_t a_off[NR];
+  uint32_t a_km[NR];  // bit ky: filter row ky of this round's rows reads inside the image
 #pragma unroll
-  for (int r = 0; r < kNR; ++r) {
+  for (int r = 0; r < NR; ++r) {
     const int rbase = r * 64 + wid * 8;  // wave-uniform
     const int s = rbase / P;
     const int j = rbase - s * P + dr;
@@ -159,7 +164,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rw(ConvArgs a) {
     const int koff = ky * rowbytes + (PAIR ? 0 : cc * 2);
     char* As = smem + buf * kAbytes;
 #pragma unroll
-    for (int r = 0; r < kNR; ++r) {
+    for (int r = 0; r < NR; ++r) {
       const bool ok = live && ((a_km[r] >> (ky & 31)) & 1u);
       // (an out-of-image column keeps its out-of-range offset: kOobOffset + koff < 2^32)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
@@ -193,8 +198,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rw(ConvArgs a) {
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     const int p = wm * (BM / 4) + i * 16 + frow;
-    const int s = p >> swl;
-    wrow[i] = s * P + (p - (s << swl));
+    const int s = p / SW;
+    wrow[i] = s * P + (p - s * SW);
   }
   auto load_frags = [&](int abuf, int kx, int slot, int kk, bf16x8 (&af)[MI], bf16x8 (&bf)[NI]) {
     const char* As = smem + abuf * kAbytes;
@@ -237,7 +242,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rw(ConvArgs a) {
       // this step's weights (issued two steps ago) and window landed; younger loads may fly:
       // the weights of step q + 1 and, at kx == 1, the next window issued before them
       if (KW > 1 && kx == 1)
-        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(WB + kNR) : "memory");
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(WB + NR) : "memory");
       else
         asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(WB) : "memory");
       __builtin_amdgcn_s_barrier();
@@ -276,9 +281,9 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rw(ConvArgs a) {
 
   // virtual row rl of this block -> real output pixel (b * Ho + oh) * Wo + ow, or -1 (masked)
   auto real_row = [&](int rl) -> int {
-    const int s = rl >> swl, j = rl - (s << swl);
+    const int s = rl / SW, j = rl - s * SW;
     const int g = g0 + s;
-    if (g >= a.nseg) return -1;
+    if (s >= R || g >= a.nseg) return -1;  // (rows past R * SW: a non-power-of-two SW)
     const int ct = g % a.nct, t = g / a.nct;
     const int ow = ct * SW + j;
     return ow < a.Wo ? t * a.Wo + ow : -1;
@@ -337,6 +342,15 @@ bool rw_disabled() {
   return off;
 }
 
+// IMAGINAIRE_AMD_CONV_RW_POW2=1: power-of-two segment widths only (A/B switch)
+bool rw_pow2_only() {
+  static const bool on = [] {
+    const char* e = std::getenv("IMAGINAIRE_AMD_CONV_RW_POW2");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
+}
+
 int pow2ceil(int v) {
   int p = 1;
   while (p < v) p <<= 1;
@@ -348,7 +362,7 @@ int pow2ceil(int v) {
 // (else the least wasteful one); with min_eff > 0 a shape wasting more than 1 - min_eff of its
 // pixels is refused (default routing: a 66- or 262-wide output on 128 / 256-pixel segments ran
 // at half the useful rate of the v1 tile).
-bool rw_plan(ConvArgs& a, double min_eff = 0.0) {
+bool rw_plan(ConvArgs& a, double min_eff = 0.0, int bm = 0, int nr = kNR, bool any_sw = true) {
   if (a.nz != 1 || a.dh != 1 || a.dw != 1 || a.sh != a.sw || (a.sh != 1 && a.sh != 2))
     return false;
   if (a.Cout % 64 != 0 || a.KH > 31 || a.KH < 1 || a.KW < 1) return false;
@@ -358,7 +372,7 @@ bool rw_plan(ConvArgs& a, double min_eff = 0.0) {
   const int kwv = pair ? (a.KW + 1) / 2 : a.KW;  // (virtual) taps per filter row
   if (pair ? (kwv > 4) : (a.KW != 1 && a.KW != 3 && a.KW != 4 && a.KW != 5 && a.KW != 7))
     return false;
-  const int BM = S == 1 ? 256 : 128;
+  const int BM = bm > 0 ? bm : (S == 1 ? 256 : 128);
   int SW = 0;
   double best = -1.0;
   for (int sw = BM; sw >= (S == 1 ? 32 : 16); sw >>= 1) {
@@ -373,16 +387,32 @@ bool rw_plan(ConvArgs& a, double min_eff = 0.0) {
       SW = sw;
     }
   }
-  if (best < min_eff) return false;
   int P, Ph = 0;
+  if (any_sw && best < 0.9 - 1e-9 && S == 1 && !pair && a.omode == 0 && !rw_pow2_only()) {
+    // any segment width: live rows = (Wo / (nct SW)) (R SW / BM), the window P = SW + KW - 1
+    // rounded up to 8 rows (R P <= the 320-row window buffer)
+    for (int sw = BM; sw >= 16; --sw) {
+      const int r = BM / sw, p = (sw + a.KW - 1 + 7) / 8 * 8;
+      if (r * p > nr * 64) continue;
+      const double eff = (double)a.Wo / ((double)ceil_div(a.Wo, sw) * sw) *
+                         ((double)(r * sw) / BM);
+      if (eff > best + 1e-3) {
+        best = eff;
+        SW = sw;
+      }
+    }
+  }
+  if (best < min_eff) return false;
   if (S == 2 && !pair) {
     Ph = SW + 4;  // >= SW + (KW - 1) / 2 even columns
     P = 2 * Ph;
-  } else {
+  } else if ((SW & (SW - 1)) == 0) {
     P = SW + 8;   // >= the rows the taps read: SW + KW - 1 | SW + 2 kwv - 2 | SW + kwv - 1
+  } else {
+    P = (SW + a.KW - 1 + 7) / 8 * 8;
   }
   const int R = BM / SW;
-  if (R * P > kNR * 64) return false;
+  if (R * P > nr * 64) return false;
   a.SW = SW;
   a.P = P;
   a.Ph = Ph;
@@ -394,9 +424,9 @@ bool rw_plan(ConvArgs& a, double min_eff = 0.0) {
   return true;
 }
 
-template <int S, int KW, int BN, bool PAIR>
+template <int S, int KW, int BN, bool PAIR, int BMT = (S == 1 ? 256 : 128), int NR = kNR>
 void rw_launch(const ConvArgs& a, dim3 grid) {
-  hipLaunchKernelGGL((conv_fwd_rw<S, KW, BN, PAIR>), grid, dim3(512), 0, stream(), a);
+  hipLaunchKernelGGL((conv_fwd_rw<S, KW, BN, PAIR, BMT, NR>), grid, dim3(512), 0, stream(), a);
 }
 
 template <int S, int BN, bool PAIR>
@@ -419,7 +449,22 @@ void rw_by_kw(const ConvArgs& a, dim3 grid, int kwv) {
   }
 }
 
-void rw_dispatch(const ConvArgs& a, dim3 grid, int BN) {
+// the narrow two-blocks-per-CU variant: stride 1, BN 64, no PAIR
+void rw_small_by_kw(const ConvArgs& a, dim3 grid) {
+  switch (a.KW) {
+    case 1: rw_launch<1, 1, 64, false, 128, 3>(a, grid); break;
+    case 3: rw_launch<1, 3, 64, false, 128, 3>(a, grid); break;
+    case 4: rw_launch<1, 4, 64, false, 128, 3>(a, grid); break;
+    case 5: rw_launch<1, 5, 64, false, 128, 3>(a, grid); break;
+    default: rw_launch<1, 7, 64, false, 128, 3>(a, grid); break;
+  }
+}
+
+void rw_dispatch(const ConvArgs& a, dim3 grid, int BN, bool small) {
+  if (small) {
+    rw_small_by_kw(a, grid);
+    return;
+  }
   const bool pair = a.Cin == 32;
   const int kwv = pair ? (a.KW + 1) / 2 : a.KW;
   auto by_pair = [&](auto sv, auto bnv) {
@@ -443,9 +488,40 @@ bool rw_eligible(const ConvArgs& a) {
   return rw_plan(t);
 }
 
+// IMAGINAIRE_AMD_CONV_RW_SMALL: the narrow two-blocks-per-CU variant for stride-1 convs with
+// Cout % 128 != 0 (BN 64). 2 (default): where the filter row holds >= 1152 MACs per output
+// channel (K = KH * KW * Cin: 3x3 over >= 128 channels, 5x5 / 7x7 over 64): 1.10-1.24x v1 and
+// 1.07-1.16x the 256-row variant there, 0.97-1.01x v1 at K = 576
+// (profiles/conv_rw_small_probe_r6_mi355x.txt); 1: every such conv; 0: off.
+int rw_small_mode() {
+  static const int mode = [] {
+    const char* e = std::getenv("IMAGINAIRE_AMD_CONV_RW_SMALL");
+    return e == nullptr ? 2 : std::atoi(e);
+  }();
+  return mode;
+}
+
+bool rw_small_shape(const ConvArgs& a) {
+  return a.sh == 1 && a.sw == 1 && a.Cin % kBK == 0 && a.Cout % 128 != 0 && a.Cout % 64 == 0 &&
+         a.nz == 1 && a.dh == 1 && a.dw == 1;
+}
+
+bool rw_small_pick(const ConvArgs& a) {
+  const int mode = rw_small_mode();
+  if (mode == 0 || !rw_small_shape(a)) return false;
+  return mode == 1 || (int64_t)a.KH * a.KW * a.Cin >= 1152;
+}
+
+bool rw_small_pref(const ConvArgs& a) { return !rw_disabled() && rw_small_pick(a); }
+
 bool run_rw(ConvArgs& a, const at::Tensor& x, bool forced) {
-  if (rw_disabled() || !rw_plan(a, forced ? 0.0 : 0.85)) return false;
-  const int BM = a.sh == 1 ? 256 : 128;
+  if (rw_disabled()) return false;
+  // (segment widths other than powers of two only where the row-window tile is forced — Cin 32,
+  // IMAGINAIRE_AMD_CONV_V=6: on the 66 / 34 / 18-wide reflect-pad data gradients they ran at
+  // 0.92-0.93x v1, profiles/conv_rw_small_probe_r6_mi355x.txt)
+  bool small = rw_small_pick(a) && rw_plan(a, forced ? 0.0 : 0.85, 128, 3, forced);
+  if (!small && !rw_plan(a, forced ? 0.0 : 0.85, 0, kNR, forced)) return false;
+  const int BM = small ? 128 : (a.sh == 1 ? 256 : 128);
   const int R = BM / a.SW;
   const int BN = a.Cout % 128 == 0 ? 128 : 64;
   a.nNt = a.Cout / BN;
@@ -464,7 +540,7 @@ bool run_rw(ConvArgs& a, const at::Tensor& x, bool forced) {
     part = at::empty({(int64_t)S * a.M * a.Cout}, x.options().dtype(at::kFloat));
     a.part = part.data_ptr<float>();
   }
-  rw_dispatch(a, dim3((unsigned)tiles, (unsigned)S, 1), BN);
+  rw_dispatch(a, dim3((unsigned)tiles, (unsigned)S, 1), BN, small);
   if (S > 1) {
     IAMD_LAUNCH_CHECK();
     const int64_t MC = (int64_t)a.M * a.Cout;

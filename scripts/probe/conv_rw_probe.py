@@ -35,6 +35,12 @@ SHAPES = [
     ('SPADE 1x1 512->256 @128x256', 4, 512, 256, 128, 256, 1, 1, 1, 0),
     ('D 4x4 s1 p2 512->512 @7x15', 8, 512, 512, 7, 15, 4, 4, 1, 2),
     ('D 4x4 s2 512->512 @16x32', 8, 512, 512, 16, 32, 4, 4, 2, 1),
+    # round 6: odd-width data gradients of reflect-padded 3x3 convs (dy 64 wide -> dx 66)
+    ('MUNIT res dgrad 256 @64 -> 66', 16, 256, 256, 64, 64, 3, 3, 1, 2),
+    ('FUNIT res dgrad 1024 @16 -> 18', 16, 1024, 1024, 16, 16, 3, 3, 1, 2),
+    ('FUNIT res dgrad 512 @32 -> 34', 16, 512, 512, 32, 32, 3, 3, 1, 2),
+    ('fs 64ch 3x3 @256', 3, 64, 64, 256, 256, 3, 3, 1, 1),
+    ('fs 128->64 3x3 @256', 3, 128, 64, 256, 256, 3, 3, 1, 1),
 ]
 
 

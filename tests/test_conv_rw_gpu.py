@@ -39,6 +39,9 @@ RW_CASES = [
     (2, 32, 64, 64, 128, 3, 3, 1, 1),      # Cin 32 at a 128-wide row
     (1, 512, 128, 12, 32, 4, 4, 2, 1),     # 4x4 s2 over eight channel blocks (K 8192)
     (2, 64, 64, 16, 64, 7, 7, 1, 3),       # 7x7 stem-like, 64-pixel rows
+    (2, 64, 128, 20, 64, 3, 3, 1, 2),      # Wo 66 (reflect-pad dgrad): 22-pixel segments
+    (2, 128, 64, 16, 16, 3, 3, 1, 2),      # Wo 18: a non-power-of-two segment, BN 64
+    (1, 64, 128, 9, 128, 5, 5, 1, 3),      # Wo 130
 ]
 
 
@@ -81,7 +84,8 @@ def test_rw_forward_matches_fp32(case):
     assert err <= 1e-2 * max(1.0, ref.abs().max().item()), err
 
 
-@pytest.mark.parametrize('case', [RW_CASES[1], RW_CASES[3], RW_CASES[13], RW_CASES[14]])
+@pytest.mark.parametrize('case', [RW_CASES[1], RW_CASES[3], RW_CASES[13], RW_CASES[14],
+                                  RW_CASES[21]])
 @pytest.mark.parametrize('splitk', ['2', '3'])
 def test_rw_splitk_matches(case, splitk):
     from imaginaire_amd.ops import _ext
@@ -115,7 +119,7 @@ def test_rw_residual_and_sigma_epilogue(case):
 
 
 @pytest.mark.parametrize('case', [RW_CASES[0], RW_CASES[1], RW_CASES[3], RW_CASES[14],
-                                  RW_CASES[9]])
+                                  RW_CASES[9], RW_CASES[21], RW_CASES[22]])
 def test_rw_never_reads_unwritten_lds(case):
     """Bitwise the same output after the LDS of every CU was filled with NaN bits."""
     from imaginaire_amd.ops import _ext
@@ -140,6 +144,23 @@ def test_rw_taken_by_default_for_long_filters():
         x, w, b = _inputs(case)
         _, var = _run(X, x, w, b, case[7], case[8], ver='0')
         assert var == 6, (case, var)
+
+
+def test_default_routing_of_narrow_and_odd_width_convs():
+    """Default routing (round 6): a stride-1 Cout = 64 conv with a long filter row (3x3 over 128
+    channels, K = 1152) takes the narrow two-blocks-per-CU row-window variant; the odd-width data
+    gradient of a reflect-padded 3x3 conv (66 wide) stays on v1 (non-power-of-two segments ran at
+    0.92x there) — and both match fp32."""
+    from imaginaire_amd.ops import _ext
+    X = _ext.ext()
+    for case, want in (((2, 128, 64, 32, 64, 3, 3, 1, 1), 6),
+                       ((2, 256, 128, 16, 64, 3, 3, 1, 2), 1)):
+        x, w, b = _inputs(case, seed=10)
+        y, var = _run(X, x, w, b, case[7], case[8], ver='0')
+        assert var == want, (case, var)
+        ref = F.leaky_relu(F.conv2d(x.float(), w.float(), b, case[7], case[8]), 0.2)
+        err = (y.float() - ref).abs().max().item()
+        assert err <= 1e-2 * max(1.0, ref.abs().max().item()), (case, err)
 
 
 def test_cin32_never_takes_the_64_channel_tiles():
