@@ -165,7 +165,8 @@ at::Tensor wgrad_finalize(const at::Tensor& part, int64_t S, int64_t Cop, int64_
                           at::ScalarType dtype, const c10::optional<at::Tensor>& dst);
 at::Tensor sn_scale_backward(const at::Tensor& grad_in, const at::Tensor& weight,
                              const at::Tensor& u, const at::Tensor& v, const at::Tensor& sigma,
-                             const c10::optional<at::Tensor>& shadow);
+                             const c10::optional<at::Tensor>& shadow,
+                             const c10::optional<at::Tensor>& dst);
 void register_lmdb(pybind11::module_& m);
 void profile_marker(int64_t tag);
 std::vector<at::Tensor> mt_sn_scale_cast(const std::vector<at::Tensor>& weights,
@@ -261,7 +262,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "all s*s phase weights conv_weight_flip_t(w, s, qy, qx) of a stride-s conv in one launch");
   m.def("sn_scale_backward", &iamd::sn_scale_backward, "spectral-norm W/sigma backward (k5d)",
         py::arg("grad"), py::arg("weight"), py::arg("u"), py::arg("v"), py::arg("sigma"),
-        py::arg("shadow") = c10::optional<at::Tensor>());
+        py::arg("shadow") = c10::optional<at::Tensor>(),
+        py::arg("dst") = c10::optional<at::Tensor>());
   m.def("sync_stats_merge", &iamd::sync_stats_merge,
         "sync-BN: merge gathered per-rank (count, mean, var) rows + finalize (k1)",
         py::arg("allst"), py::arg("eps"), py::arg("weight") = py::none(),

@@ -721,7 +721,8 @@ snb_apply(const G* __restrict__ g, const float* __restrict__ u, const float* __r
 // weight for the <G, W> reduction (half the bytes of that pass)
 at::Tensor sn_scale_backward(const at::Tensor& grad_in, const at::Tensor& weight,
                              const at::Tensor& u, const at::Tensor& v, const at::Tensor& sigma,
-                             const c10::optional<at::Tensor>& shadow) {
+                             const c10::optional<at::Tensor>& shadow,
+                             const c10::optional<at::Tensor>& dst) {
   IAMD_CHECK(weight.is_cuda() && weight.scalar_type() == at::kFloat, "sn_scale_backward: fp32 W");
   IAMD_CHECK(u.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat &&
                  sigma.scalar_type() == at::kFloat && sigma.numel() >= 1,
@@ -735,7 +736,13 @@ at::Tensor sn_scale_backward(const at::Tensor& grad_in, const at::Tensor& weight
   IAMD_CHECK(u.numel() == h && v.numel() == w, "sn_scale_backward: u/v sizes");
   IAMD_CHECK(w < (1ll << 31), "sn_scale_backward: row too long");
   const int64_t cl_cin = cl ? weight.size(1) : 0, cl_khw = cl ? weight.size(2) * weight.size(3) : 0;
-  auto dw = at::empty_like(weight, fmt);
+  // dst: the parameter's DDP bucket slice (parallel/ddp.py): dW lands there, no copy after
+  const bool has_dst = dst.has_value() && dst->defined();
+  if (has_dst)
+    IAMD_CHECK(dst->is_cuda() && dst->scalar_type() == at::kFloat && dst->numel() == n &&
+                   dst->sizes() == weight.sizes() && dst->strides() == weight.strides(),
+               "sn_scale_backward: dst must be fp32 and laid out like W");
+  auto dw = has_dst ? *dst : at::empty_like(weight, fmt);
   IAMD_CHECK(n < (1ll << 31), "sn_scale_backward: weight too large");
   const int P = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (n + 4095) / 4096));
   const int P4 = (P + 3) & ~3;  // keeps vm 16-byte aligned for the vector loads

@@ -745,8 +745,10 @@ std::vector<at::Tensor> norm_stats(const at::Tensor& x, bool per_instance, doubl
   });
   IAMD_LAUNCH_CHECK();
   const int G = per_instance ? g.N : 1;
-  auto cnt = at::empty({G, g.C}, fopt), mean = at::empty({G, g.C}, fopt),
-       var = at::empty({G, g.C}, fopt);
+  // count / mean / var as rows of ONE [3, G, C] buffer: sync-BN hands it to its all-gather
+  // as is (ops/norm.py _stats_rows), no stack copy
+  auto stats3 = at::empty({3, G, g.C}, fopt);
+  auto cnt = stats3[0], mean = stats3[1], var = stats3[2];
   at::Tensor scale, shift;
   auto rstd = at::empty({G, g.C}, fopt);
   if (!partial_only) {

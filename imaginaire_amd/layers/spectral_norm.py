@@ -50,6 +50,7 @@ class _SNScale(torch.autograd.Function):
     @staticmethod
     def forward(ctx, weight, u, v, sigma):
         ctx.save_for_backward(weight, u, v, sigma)
+        ctx.wparam = weight if isinstance(weight, torch.nn.Parameter) else None
         return weight / sigma
 
     @staticmethod
@@ -57,9 +58,13 @@ class _SNScale(torch.autograd.Function):
         weight, u, v, sigma = ctx.saved_tensors
         if _ext.use_native(weight) and weight.dtype == torch.float32 and \
                 grad.dtype in (torch.float32, torch.bfloat16):
-            # <G, W> reads the bf16 shadow of W when the forward had one (half the bytes)
+            # <G, W> reads the bf16 shadow of W when the forward had one (half the bytes); dW
+            # goes straight into the parameter's DDP bucket slice when one is armed
+            from imaginaire_amd.ops.conv import _take_grad_dest
+            dest = _take_grad_dest(getattr(ctx, 'wparam', None), tuple(weight.shape))
             return _ext.ext().sn_scale_backward(grad, weight, u, v, sigma,
-                                                getattr(ctx, 'shadow', None)), None, None, None
+                                                getattr(ctx, 'shadow', None), dest), \
+                None, None, None
         g = grad.float()
         dot = (g * weight).sum()
         outer = torch.outer(u, v).view(weight.shape)
@@ -76,6 +81,7 @@ class _SNScaleCast(torch.autograd.Function):
     def forward(ctx, weight, u, v, sigma, w16, shadow=None):
         ctx.save_for_backward(weight, u, v, sigma)
         ctx.shadow = shadow  # bf16(W) (the optimizer keeps it in sync), or None
+        ctx.wparam = weight if isinstance(weight, torch.nn.Parameter) else None
         return w16
 
     @staticmethod

@@ -71,9 +71,20 @@ def _gather_rows(allst, stacked, group, async_op=False):
     return dist.all_gather(bufs, stacked, group=group, async_op=async_op)
 
 
+def _stats_rows(cnt, mean, var):
+    """(count, mean, var) as one contiguous [3, C] tensor: the [3, 1, C] buffer norm_stats
+    writes them into when they are its rows, else a stacked copy."""
+    base = cnt._base
+    if base is not None and base.dim() == 3 and base.shape[0] == 3 and base.shape[1] == 1 and \
+            base.is_contiguous() and cnt.data_ptr() == base.data_ptr() and \
+            mean.data_ptr() == base[1].data_ptr() and var.data_ptr() == base[2].data_ptr():
+        return base.view(3, -1)
+    return torch.stack([cnt.reshape(-1), mean.reshape(-1), var.reshape(-1)], 0).contiguous()
+
+
 def _gather_local(cnt, mean, var, group):
     """This rank's (count, mean, var) [1, C] rows all-gathered into [W, 3, C] (one collective)."""
-    stacked = torch.stack([cnt.reshape(-1), mean.reshape(-1), var.reshape(-1)], 0).contiguous()
+    stacked = _stats_rows(cnt, mean, var)
     allst = stacked.new_empty((_world(group),) + tuple(stacked.shape))
     _gather_rows(allst, stacked, group)
     return allst
@@ -143,7 +154,7 @@ def prefetch_sync_stats(x, eps, group):
     if getattr(x, '_iamd_bn_stats', (None,))[0] == key:
         return
     count, mean, var = _ext.ext().norm_stats(x, False, eps, None, None, True)[:3]
-    stacked = torch.stack([count.reshape(-1), mean.reshape(-1), var.reshape(-1)], 0).contiguous()
+    stacked = _stats_rows(count, mean, var)
     allst = stacked.new_empty((_world(group),) + tuple(stacked.shape))
     work = _gather_rows(allst, stacked, group, async_op=True)
     x._iamd_bn_stats = (key, 'pending', work, allst, stacked)

@@ -115,6 +115,9 @@ class DistributedDataParallel(nn.Module):
         self.n_copies = 0  # gradients the hook copied into their bucket (diagnostics / tests)
         self._pending = {}
         self._bidx = None
+        # parameters whose bucket slice may hold non-zero data (buckets start zeroed): only
+        # these need zeroing when a backward leaves them without a gradient
+        self._dirty = set()
         if self.world > 1 or unused.get('_force_distributed', False):
             self.world = max(self.world, 1)
             self._force = True
@@ -268,15 +271,17 @@ class DistributedDataParallel(nn.Module):
         self._flush_copies(self._bidx[id(b)])
         if b.expected == 0:
             return
-        # slices of parameters without a gradient this backward hold the previous step's
-        # values: zero them (runs of consecutive parameters as one fill each)
+        # slices of parameters without a gradient this backward may hold an earlier step's
+        # values: zero those (runs of consecutive parameters as one fill each; a slice that is
+        # already zero — never written, or zeroed since — is left alone)
         run0 = run1 = None
         for p, off in zip(b.params, b.offsets):
-            if p in self._used:
+            if p in self._used or p not in self._dirty:
                 if run0 is not None:
                     b.flat[run0:run1].zero_()
                     run0 = None
                 continue
+            self._dirty.discard(p)
             if run0 is None:
                 run0 = off
             run1 = off + p.numel()
@@ -337,6 +342,8 @@ class DistributedDataParallel(nn.Module):
                 flags = flags.to(self.buckets[0].flat.device)
             dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=self.process_group)
             used = flags.cpu().tolist()
+            # (after the all-reduce a slice is non-zero wherever ANY rank wrote it)
+            self._dirty = {p for p, u in zip(params, used) if u}
             for p, u in zip(params, used):
                 if not u:
                     p.grad = None
@@ -344,6 +351,7 @@ class DistributedDataParallel(nn.Module):
                     bi, off = self._param_bucket[p]
                     p.grad = _grad_view(self.buckets[bi].flat, off, p)
             return
+        self._dirty = set(self._used)  # ('local': every rank used the same parameters)
         if len(self._used) == len(params):
             return
         for p in params:
@@ -358,6 +366,7 @@ class DistributedDataParallel(nn.Module):
             return
         for b in self.buckets:
             b.flat.zero_()
+        self._dirty = set()
 
     @torch.no_grad()
     def sync_buffers(self):

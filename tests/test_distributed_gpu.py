@@ -351,16 +351,27 @@ def _zero_copy_worker(rank, world, port, q):
     C._MFMA_MIN_BLOCKS = 0
     cl = torch.channels_last
 
+    from imaginaire_amd.layers.spectral_norm import _SNScale
+    gen = torch.Generator(device='cuda').manual_seed(3)
+    su = torch.nn.functional.normalize(torch.randn(128, device='cuda', generator=gen), dim=0)
+    sv = torch.nn.functional.normalize(torch.randn(128 * 9, device='cuda', generator=gen), dim=0)
+
     class Net(torch.nn.Module):
         def __init__(self):
             super().__init__()
             self.a = torch.nn.Conv2d(64, 128, 3, padding=1)
             self.b = torch.nn.Conv2d(128, 128, 3, padding=1)  # used twice per forward
             self.g = torch.nn.Parameter(torch.ones(128))       # not a conv weight: copied
+            # materialised spectral norm (the SPADE gamma|beta path): the SN backward writes
+            # dW into the bucket (sn_scale_backward dst)
+            self.s = torch.nn.Conv2d(128, 128, 3, padding=1, bias=False)
 
         def forward(self, x):
             h = C.conv2d_act(x, self.a.weight, self.a.bias, 1, 1, 1, 0.2)
             h = C.conv2d(h, self.b.weight, self.b.bias, 1, 1) * self.g.view(1, -1, 1, 1)
+            sigma = (su @ self.s.weight.detach().permute(0, 1, 2, 3).reshape(128, -1) @ sv)
+            ws = _SNScale.apply(self.s.weight, su, sv, sigma.reshape(1))
+            h = C.conv2d(h, ws.to(torch.bfloat16), None, 1, 1)
             return C.conv2d(h, self.b.weight, None, 1, 1)
 
     torch.manual_seed(0)
