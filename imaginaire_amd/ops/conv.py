@@ -1114,6 +1114,26 @@ def _time_ms(fn, reps=3):
     return start.elapsed_time(end)
 
 
+def _time_candidates(fns, reps=3, trials=3):
+    """{name: ms} for {name: fn}: every candidate warmed, then ``trials`` rounds that time each
+    one in turn (interleaved, so clock / power drift hits all alike), the minimum per candidate.
+    (One back-to-back timing each picked different k11 variants for near-tied SPADE shapes from
+    run to run: ±1-2% on the step.)"""
+    for fn in fns.values():
+        fn()
+    best = {name: float('inf') for name in fns}
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(trials):
+        for name, fn in fns.items():
+            start.record()
+            for _ in range(reps):
+                fn()
+            end.record()
+            end.synchronize()
+            best[name] = min(best[name], start.elapsed_time(end))
+    return best
+
+
 def _agree(times):
     """Sum per-candidate timings over ranks (every rank then takes the same argmin).
     ``times``: {key: {candidate: ms}} with identical keys and candidates on every rank."""
@@ -1301,15 +1321,15 @@ def tune_pending():
                     torch.ones(1, device=dev))
             k11, miopen = _wgrad_fns(dy, xb, wb, stride, padding, dilation, cout, cin, wdt,
                                      sn=sn)
-            cand = {}
+            fns = {}
             if _MFMA_WGRAD != '1' and sn is None:
-                cand['miopen'] = _time_ms(miopen)
+                fns['miopen'] = miopen
             if len(_k11_variants(dy, xb, wb, stride, dilation)) > 1:
-                cand['k11'] = _time_ms(lambda: k11(1))
-                cand['k11v2'] = _time_ms(lambda: k11(2))
+                fns['k11'] = lambda: k11(1)
+                fns['k11v2'] = lambda: k11(2)
             else:
-                cand['k11'] = _time_ms(k11)
-            times[('w',) + key] = cand
+                fns['k11'] = k11
+            times[('w',) + key] = _time_candidates(fns)
         else:
             # a deconv key names its weight, which only the ranks that saw it hold: those time
             # it, the others report 0 and the vote below averages over the ranks that timed

@@ -369,8 +369,9 @@ def _zero_copy_worker(rank, world, port, q):
         def forward(self, x):
             h = C.conv2d_act(x, self.a.weight, self.a.bias, 1, 1, 1, 0.2)
             h = C.conv2d(h, self.b.weight, self.b.bias, 1, 1) * self.g.view(1, -1, 1, 1)
-            sigma = (su @ self.s.weight.detach().permute(0, 1, 2, 3).reshape(128, -1) @ sv)
-            ws = _SNScale.apply(self.s.weight, su, sv, sigma.reshape(1))
+            with torch.autocast('cuda', enabled=False):  # (fp32 sigma, as the SN group's)
+                sigma = su @ self.s.weight.detach().reshape(128, -1) @ sv
+                ws = _SNScale.apply(self.s.weight, su, sv, sigma.reshape(1))
             h = C.conv2d(h, ws.to(torch.bfloat16), None, 1, 1)
             return C.conv2d(h, self.b.weight, None, 1, 1)
 
