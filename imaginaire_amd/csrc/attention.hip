@@ -516,6 +516,23 @@ inline __bf16* bpm(at::Tensor& t) { return reinterpret_cast<__bf16*>(t.data_ptr(
 
 // key / query splits so a launch has >= ~2 workgroups per CU: NS divides the sequence into
 // chunks of whole 64-row blocks
+// dsum[r] = sum_j dout[r, j] * out[r, j] in fp32: one wave per row, four rows per block
+__global__ __launch_bounds__(256) void attn_dsum_kernel(const __hip_bfloat16* __restrict__ dout,
+                                                        const __hip_bfloat16* __restrict__ out,
+                                                        float* __restrict__ dsum, int64_t rows,
+                                                        int dv) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  const __hip_bfloat16* a = dout + r * dv;
+  const __hip_bfloat16* b = out + r * dv;
+  float acc = 0.f;
+  for (int j = lane; j < dv; j += 64) acc += __bfloat162float(a[j]) * __bfloat162float(b[j]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if (lane == 0) dsum[r] = acc;
+}
+
 inline int pick_splits(int64_t tiles, int64_t len) {
   const int64_t want = (512 + tiles - 1) / tiles;
   const int64_t maxs = len / 64;
@@ -532,6 +549,13 @@ inline int pick_waves(int64_t rows, int64_t other) {
   const char* e = std::getenv("IMAGINAIRE_AMD_ATTN_MIN_WG");
   const int64_t min_wg = e ? std::atoll(e) : 256;
   return (rows % 128 == 0 && other * (rows / 128) >= min_wg) ? 8 : 4;
+}
+// per-kernel override of that threshold for the backward passes (read per call, A/B):
+// IMAGINAIRE_AMD_ATTN_DKV_MIN_WG / IMAGINAIRE_AMD_ATTN_DQ_MIN_WG
+inline int pick_waves_bwd(int64_t rows, int64_t other, const char* var) {
+  const char* e = std::getenv(var);
+  if (e == nullptr) return pick_waves(rows, other);
+  return (rows % 128 == 0 && other * (rows / 128) >= std::atoll(e)) ? 8 : 4;
 }
 
 template <int D, int DV>
@@ -575,7 +599,7 @@ void launch_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
   const int64_t B = q.size(0), Lq = q.size(1), Lk = k.size(1);
   auto fo = q.options().dtype(at::kFloat);
   // dK / dV: key tiles x query splits
-  const int nwk = pick_waves(Lk, B);
+  const int nwk = pick_waves_bwd(Lk, B, "IMAGINAIRE_AMD_ATTN_DKV_MIN_WG");
   int nq = pick_splits(B * (Lk / (nwk * 16)), Lq);
   const int qlen = split_len(Lq, nq);
   nq = (int)((Lq + qlen - 1) / qlen);
@@ -620,7 +644,7 @@ void launch_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                        stream(), dvp.data_ptr<float>(), bpm(dv), nq, nv);
   }
   // dQ: query tiles x key splits
-  const int nwq = pick_waves(Lq, B);
+  const int nwq = pick_waves_bwd(Lq, B, "IMAGINAIRE_AMD_ATTN_DQ_MIN_WG");
   int nk2 = pick_splits(B * (Lq / (nwq * 16)), Lk);
   const int klen = split_len(Lk, nk2);
   nk2 = (int)((Lk + klen - 1) / klen);
@@ -672,7 +696,15 @@ std::vector<at::Tensor> attention_bwd(const at::Tensor& q, const at::Tensor& k, 
   IAMD_CHECK(dout.sizes() == out.sizes() && lse.scalar_type() == at::kFloat &&
                  lse.numel() == B * Lq && lse.is_contiguous(),
              "attention_bwd: out / dout / lse shapes");
-  const at::Tensor dsum = (dout.to(at::kFloat) * out.to(at::kFloat)).sum(-1).contiguous();
+  IAMD_CHECK(out.scalar_type() == at::kBFloat16 && out.is_contiguous(),
+             "attention_bwd: out must be contiguous bf16");
+  const int64_t rows = B * Lq;
+  const int dvv0 = (int)out.size(2);
+  auto dsum = at::empty({B, Lq}, q.options().dtype(at::kFloat));
+  hipLaunchKernelGGL(attn_dsum_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream(),
+                     reinterpret_cast<const __hip_bfloat16*>(dout.data_ptr()),
+                     reinterpret_cast<const __hip_bfloat16*>(out.data_ptr()),
+                     dsum.data_ptr<float>(), rows, dvv0);
   auto dq = at::empty_like(q), dk = at::empty_like(k), dv = at::empty_like(v);
   const float sl2 = (float)(scale * 1.4426950408889634), sc = (float)scale;
   const int64_t d = q.size(2), dvv = v.size(2);

@@ -1,0 +1,70 @@
+"""k16 backward alone at the few-shot recipe shape: 8- vs 4-wave workgroups for the dK/dV and the
+dQ kernels separately (IMAGINAIRE_AMD_ATTN_DKV_MIN_WG / IMAGINAIRE_AMD_ATTN_DQ_MIN_WG, read per
+call), interleaved, minimum of three rounds; each variant's gradients are checked against the
+default's.
+
+    python scripts/probe/attn_bwd_ab.py
+"""
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from imaginaire_amd.ops import _ext  # noqa: E402
+
+B, Lq, Lk, d, dv = 3, 16384, 32768, 128, 288  # 258 value channels, padded as fused_attention does
+scale = d ** -0.5
+torch.manual_seed(0)
+q = torch.randn(B, Lq, d, device='cuda').to(torch.bfloat16)
+k = torch.randn(B, Lk, d, device='cuda').to(torch.bfloat16)
+v = torch.randn(B, Lk, dv, device='cuda').to(torch.bfloat16)
+go = torch.randn(B, Lq, dv, device='cuda').to(torch.bfloat16)
+E = _ext.ext()
+o, lse = E.attention_fwd(q, k, v, scale)
+
+
+def bwd():
+    return E.attention_bwd(q, k, v, o, lse, go, scale)
+
+
+def timeit(iters=10):
+    bwd()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        bwd()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters * 1e3
+
+
+BIG = '100000000'
+VARIANTS = {'dkv8 dq8 (default)': (None, None), 'dkv4 dq8': (BIG, None),
+            'dkv8 dq4': (None, BIG), 'dkv4 dq4': (BIG, BIG)}
+
+
+def setenv(a, b):
+    for var, val in (('IMAGINAIRE_AMD_ATTN_DKV_MIN_WG', a), ('IMAGINAIRE_AMD_ATTN_DQ_MIN_WG', b)):
+        if val is None:
+            os.environ.pop(var, None)
+        else:
+            os.environ[var] = val
+
+
+setenv(None, None)
+ref = [t.float() for t in bwd()]
+flops = 2 * B * Lq * Lk * (2 * d + 2 * dv + d)  # S, dP, dV, dK, dQ  (recompute S: + d)
+res = {}
+for rnd in range(3):
+    for name, (a, b) in VARIANTS.items():
+        setenv(a, b)
+        res.setdefault(name, []).append(timeit())
+for name, (a, b) in VARIANTS.items():
+    setenv(a, b)
+    got = bwd()
+    err = max(float((g.float() - r).abs().max() / r.abs().max()) for g, r in zip(got, ref))
+    t = min(res[name])
+    print('%-20s bwd %.3f ms  (%.0f TF/s)  max rel diff vs default %.2e'
+          % (name, t, flops / t / 1e9, err), flush=True)
+setenv(None, None)
