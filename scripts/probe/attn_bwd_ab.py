@@ -3,7 +3,7 @@ dQ kernels separately (IMAGINAIRE_AMD_ATTN_DKV_MIN_WG / IMAGINAIRE_AMD_ATTN_DQ_M
 call), interleaved, minimum of three rounds; each variant's gradients are checked against the
 default's.
 
-    python scripts/probe/attn_bwd_ab.py
+    python scripts/probe/attn_bwd_ab.py [--default-only]
 """
 import os
 import sys
@@ -42,6 +42,8 @@ def timeit(iters=10):
 BIG = '100000000'
 VARIANTS = {'dkv8 dq8 (default)': (None, None), 'dkv4 dq8': (BIG, None),
             'dkv8 dq4': (None, BIG), 'dkv4 dq4': (BIG, BIG)}
+if '--default-only' in sys.argv:  # for a per-kernel rocprofv3 breakdown of the default
+    VARIANTS = {'dkv8 dq8 (default)': (None, None)}
 
 
 def setenv(a, b):
