@@ -12,13 +12,21 @@ import importlib
 _ALIASES = {
     'imaginaire.': 'imaginaire_amd.',
 }
+# dataset types that only this framework's unit-test configs name: the synthetic paired-video
+# and few-shot-video sets are the one generator in datasets/synthetic.py (it picks the layout
+# from the config), so those names resolve to it instead of to modules of their own
+_MODULES = {
+    'imaginaire_amd.datasets.synthetic_videos': 'imaginaire_amd.datasets.synthetic',
+    'imaginaire_amd.datasets.synthetic_few_shot_videos': 'imaginaire_amd.datasets.synthetic',
+}
 
 
 def canonical_module_name(name):
     for src, dst in _ALIASES.items():
         if name.startswith(src) and not name.startswith(dst):
-            return dst + name[len(src):]
-    return name
+            name = dst + name[len(src):]
+            break
+    return _MODULES.get(name, name)
 
 
 def import_module(name):
