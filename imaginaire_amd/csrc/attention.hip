@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 namespace iamd {
 namespace {
@@ -247,16 +248,20 @@ __global__ __launch_bounds__(256) void attn_sum_splits(const float* __restrict__
 // in blocks of 32 staged in LDS both row-major (A operands of S, dP) and transposed (A operands
 // of dV^T, dK^T). S = Q K^T and dP = dO V^T put the key in the lane's column, so P and dS feed
 // dV^T += dO^T P and dK^T += Q^T dS as B operands.
+// WDS: dS^T [B][Lk][Lq] bf16 is written to dst as well (a variant of its own: the stores cost
+// registers the other path should not pay for), and dQ = dS K is then one GEMM
+// instead of the dQ kernel (which recomputes S and dP): 288 GB of HBM holds the B x Lq x Lk
+// matrix at the few-shot shapes (3.2 GB at 3 x 16384 x 32768).
 // PFO: the dO / dO^T tiles are prefetched too (else loaded after the barrier, as the Q tiles
 // used to be): at D = 128, DV = 288 with 8 waves the full prefetch exceeds 256 VGPRs
-template <int D, int DV, int NW, bool PFO>
+template <int D, int DV, int NW, bool PFO, bool WDS>
 __global__ __launch_bounds__(NW * 64) void attn_bwd_dkv_kernel(
     const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v,
     const __bf16* __restrict__ dout, const __bf16* __restrict__ qt,
     const __bf16* __restrict__ dott, const float* __restrict__ lse2,
     const float* __restrict__ dsum, __bf16* __restrict__ dk, __bf16* __restrict__ dv, int Lq,
     int Lk, float sl2, float scale, int qlen, float* __restrict__ dkpart,
-    float* __restrict__ dvpart) {
+    float* __restrict__ dvpart, __bf16* __restrict__ dst) {
   constexpr int QB = 32, QP = D + 8, OP = DV + 8, TP = QB + 8;
   __shared__ __attribute__((aligned(16))) __bf16 Qs[QB * QP];
   __shared__ __attribute__((aligned(16))) __bf16 Qt[D * TP];
@@ -341,6 +346,17 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkv_kernel(
       }
     }
     const bf16x8 pb = pack8(p[0], p[1]), dsb = pack8(ds[0], ds[1]);
+    if constexpr (WDS) {  // dS^T row of this lane's key: queries q0 + 4g + e, q0 + 16 + 4g + e
+      __bf16* row = dst + ((int64_t)b * Lk + ki) * Lq + q0 + g * 4;
+      bf16x4 lo, hi;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        lo[e] = dsb[e];
+        hi[e] = dsb[4 + e];
+      }
+      *reinterpret_cast<bf16x4*>(row) = lo;
+      *reinterpret_cast<bf16x4*>(row + 16) = hi;
+    }
 #pragma unroll
     for (int i = 0; i < DV / 16; ++i)
       dvt[i] = mfma16(read_a_split(&Ot[(i * 16 + l16) * TP], g), pb, dvt[i]);
@@ -609,6 +625,18 @@ void launch_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
     dvp = at::empty({nq, B, Lk, (int64_t)DV}, fo);
   }
   const at::Tensor qt = q.transpose(1, 2).contiguous(), dott = dout.transpose(1, 2).contiguous();
+  // IMAGINAIRE_AMD_ATTN_DQ_GEMM: dQ from a stored dS^T by one GEMM (1, default) or by the dQ
+  // kernel (0); IMAGINAIRE_AMD_ATTN_DS_MAX_GB caps the dS^T workspace (default 16 GB)
+  const char* dq_gemm_var = std::getenv("IMAGINAIRE_AMD_ATTN_DQ_GEMM");  // read per call (A/B)
+  const bool dq_gemm_env = dq_gemm_var == nullptr || std::atoi(dq_gemm_var) != 0;
+  static const double ds_max_gb = [] {
+    const char* e = std::getenv("IMAGINAIRE_AMD_ATTN_DS_MAX_GB");
+    return e == nullptr ? 16.0 : std::atof(e);
+  }();
+  const bool dq_gemm = dq_gemm_env && (double)B * Lq * Lk * 2 <= ds_max_gb * 1e9;
+  at::Tensor dsT;
+  if (dq_gemm) dsT = at::empty({B, Lk, Lq}, q.options());
+  __bf16* dstp = dq_gemm ? bpm(dsT) : nullptr;
   {
     const dim3 grid((unsigned)(Lk / (nwk * 16)), (unsigned)nq, (unsigned)B);
     float* dkpp = nq > 1 ? dkp.data_ptr<float>() : nullptr;
@@ -620,21 +648,28 @@ void launch_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
       return e == nullptr ? -1 : std::atoi(e);
     }();
     const bool pfo = pfo_env < 0 ? !(D == 128 && DV > 256) : pfo_env != 0;
-    if (nwk == 8 && pfo)
-      hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, DV, 8, true>), grid, dim3(512), 0, stream(),
-                         bp(q), bp(k), bp(v), bp(dout), bp(qt), bp(dott), lse.data_ptr<float>(),
-                         dsum.data_ptr<float>(), bpm(dk), bpm(dv), (int)Lq, (int)Lk, sl2, sc,
-                         qlen, dkpp, dvpp);
-    else if (nwk == 8)
-      hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, DV, 8, false>), grid, dim3(512), 0, stream(),
-                         bp(q), bp(k), bp(v), bp(dout), bp(qt), bp(dott), lse.data_ptr<float>(),
-                         dsum.data_ptr<float>(), bpm(dk), bpm(dv), (int)Lq, (int)Lk, sl2, sc,
-                         qlen, dkpp, dvpp);
+    auto launch = [&](auto wds) {
+      constexpr bool W = decltype(wds)::value;
+      if (nwk == 8 && pfo)
+        hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, DV, 8, true, W>), grid, dim3(512), 0, stream(),
+                           bp(q), bp(k), bp(v), bp(dout), bp(qt), bp(dott), lse.data_ptr<float>(),
+                           dsum.data_ptr<float>(), bpm(dk), bpm(dv), (int)Lq, (int)Lk, sl2, sc,
+                           qlen, dkpp, dvpp, dstp);
+      else if (nwk == 8)
+        hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, DV, 8, false, W>), grid, dim3(512), 0, stream(),
+                           bp(q), bp(k), bp(v), bp(dout), bp(qt), bp(dott), lse.data_ptr<float>(),
+                           dsum.data_ptr<float>(), bpm(dk), bpm(dv), (int)Lq, (int)Lk, sl2, sc,
+                           qlen, dkpp, dvpp, dstp);
+      else
+        hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, DV, 4, true, W>), grid, dim3(256), 0, stream(),
+                           bp(q), bp(k), bp(v), bp(dout), bp(qt), bp(dott), lse.data_ptr<float>(),
+                           dsum.data_ptr<float>(), bpm(dk), bpm(dv), (int)Lq, (int)Lk, sl2, sc,
+                           qlen, dkpp, dvpp, dstp);
+    };
+    if (dq_gemm)
+      launch(std::true_type{});
     else
-      hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, DV, 4, true>), grid, dim3(256), 0, stream(), bp(q),
-                         bp(k), bp(v), bp(dout), bp(qt), bp(dott), lse.data_ptr<float>(),
-                         dsum.data_ptr<float>(), bpm(dk), bpm(dv), (int)Lq, (int)Lk, sl2, sc,
-                         qlen, dkpp, dvpp);
+      launch(std::false_type{});
   }
   if (nq > 1) {
     const int64_t nk = B * Lk * D, nv = B * Lk * DV;
@@ -642,6 +677,10 @@ void launch_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                        stream(), dkp.data_ptr<float>(), bpm(dk), nq, nk);
     hipLaunchKernelGGL(attn_sum_splits, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0,
                        stream(), dvp.data_ptr<float>(), bpm(dv), nq, nv);
+  }
+  if (dq_gemm) {  // dQ = dS K = (dS^T)^T K, fp32 accumulation in the GEMM
+    at::bmm_out(dq, dsT.transpose(1, 2), k);
+    return;
   }
   // dQ: query tiles x key splits
   const int nwq = pick_waves_bwd(Lq, B, "IMAGINAIRE_AMD_ATTN_DQ_MIN_WG");

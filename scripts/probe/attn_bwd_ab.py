@@ -3,7 +3,7 @@ dQ kernels separately (IMAGINAIRE_AMD_ATTN_DKV_MIN_WG / IMAGINAIRE_AMD_ATTN_DQ_M
 call), interleaved, minimum of three rounds; each variant's gradients are checked against the
 default's.
 
-    python scripts/probe/attn_bwd_ab.py [--default-only]
+    python scripts/probe/attn_bwd_ab.py [--default-only | --dq-gemm]
 """
 import os
 import sys
@@ -42,31 +42,34 @@ def timeit(iters=10):
 BIG = '100000000'
 VARIANTS = {'dkv8 dq8 (default)': (None, None), 'dkv4 dq8': (BIG, None),
             'dkv8 dq4': (None, BIG), 'dkv4 dq4': (BIG, BIG)}
+if '--dq-gemm' in sys.argv:  # dQ from the stored dS^T by one GEMM vs the dQ kernel
+    VARIANTS = {'dq gemm (default)': (None, None, '1'), 'dq kernel': (None, None, '0')}
 if '--default-only' in sys.argv:  # for a per-kernel rocprofv3 breakdown of the default
     VARIANTS = {'dkv8 dq8 (default)': (None, None)}
 
 
-def setenv(a, b):
-    for var, val in (('IMAGINAIRE_AMD_ATTN_DKV_MIN_WG', a), ('IMAGINAIRE_AMD_ATTN_DQ_MIN_WG', b)):
+def setenv(a, b, gemm=None):
+    for var, val in (('IMAGINAIRE_AMD_ATTN_DKV_MIN_WG', a), ('IMAGINAIRE_AMD_ATTN_DQ_MIN_WG', b),
+                     ('IMAGINAIRE_AMD_ATTN_DQ_GEMM', gemm)):
         if val is None:
             os.environ.pop(var, None)
         else:
             os.environ[var] = val
 
 
-setenv(None, None)
-ref = [t.float() for t in bwd()]
+setenv(None, None, '0')
+ref = [t.float() for t in bwd()]  # the dQ kernel path
 flops = 2 * B * Lq * Lk * (2 * d + 2 * dv + d)  # S, dP, dV, dK, dQ  (recompute S: + d)
 res = {}
 for rnd in range(3):
-    for name, (a, b) in VARIANTS.items():
-        setenv(a, b)
+    for name, vs in VARIANTS.items():
+        setenv(*vs)
         res.setdefault(name, []).append(timeit())
-for name, (a, b) in VARIANTS.items():
-    setenv(a, b)
+for name, vs in VARIANTS.items():
+    setenv(*vs)
     got = bwd()
     err = max(float((g.float() - r).abs().max() / r.abs().max()) for g, r in zip(got, ref))
     t = min(res[name])
-    print('%-20s bwd %.3f ms  (%.0f TF/s)  max rel diff vs default %.2e'
+    print('%-20s bwd %.3f ms  (%.0f TF/s)  max rel diff vs dQ-kernel path %.2e'
           % (name, t, flops / t / 1e9, err), flush=True)
 setenv(None, None)

@@ -1838,12 +1838,15 @@ def test_spectral_norm_shadow_result_depends_on_weights_only():
     (1, 128, 256, 64, 300, 1.0),     # above 288: two column chunks
     (16, 4096, 8192, 32, 32, 1.0),   # 8-wave workgroups (128 rows per staged tile) everywhere
 ])
-def test_fused_attention_matches_fp32_reference(B, Lq, Lk, d, dv, scale):
+@pytest.mark.parametrize('dq_gemm', ['1', '0'])
+def test_fused_attention_matches_fp32_reference(B, Lq, Lk, d, dv, scale, dq_gemm, monkeypatch):
     """k16 (csrc/attention.hip): softmax(scale q k^T) v and its gradients against the explicit
-    fp32 formulation on the same bf16-rounded inputs; no attention matrix is materialised. The
-    shapes cover the key-split forward (+ combine), the split backward (+ partial sums) and the
-    unsplit launches."""
+    fp32 formulation on the same bf16-rounded inputs; no attention matrix is materialised in the
+    forward. The shapes cover the key-split forward (+ combine), the split backward (+ partial
+    sums) and the unsplit launches; dQ both from the stored dS^T by one GEMM (default) and from
+    the dQ kernel."""
     from imaginaire_amd.ops import attention as A
+    monkeypatch.setenv('IMAGINAIRE_AMD_ATTN_DQ_GEMM', dq_gemm)
     torch.manual_seed(31)
     q = torch.randn(B, Lq, d, device='cuda').to(torch.bfloat16)
     k = torch.randn(B, Lk, d, device='cuda').to(torch.bfloat16)
