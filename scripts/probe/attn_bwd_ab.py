@@ -3,7 +3,7 @@ dQ kernels separately (IMAGINAIRE_AMD_ATTN_DKV_MIN_WG / IMAGINAIRE_AMD_ATTN_DQ_M
 call), interleaved, minimum of three rounds; each variant's gradients are checked against the
 default's.
 
-    python scripts/probe/attn_bwd_ab.py [--default-only | --dq-gemm]
+    python scripts/probe/attn_bwd_ab.py [--default-only | --dq-gemm | --gemm-waves]
 """
 import os
 import sys
@@ -44,6 +44,8 @@ VARIANTS = {'dkv8 dq8 (default)': (None, None), 'dkv4 dq8': (BIG, None),
             'dkv8 dq4': (None, BIG), 'dkv4 dq4': (BIG, BIG)}
 if '--dq-gemm' in sys.argv:  # dQ from the stored dS^T by one GEMM vs the dQ kernel
     VARIANTS = {'dq gemm (default)': (None, None, '1'), 'dq kernel': (None, None, '0')}
+if '--gemm-waves' in sys.argv:  # the GEMM path with 8- vs 4-wave dK/dV (+dS^T) workgroups
+    VARIANTS = {'gemm dkv8': (None, None, '1'), 'gemm dkv4': (BIG, None, '1')}
 if '--default-only' in sys.argv:  # for a per-kernel rocprofv3 breakdown of the default
     VARIANTS = {'dkv8 dq8 (default)': (None, None)}
 
