@@ -982,7 +982,8 @@ def test_multi_tensor_gan_loss(dtype, mode, t_real, dis_update):
     refs = [x.detach().float().requires_grad_(True) for x in xs]
     ref = sum(crit.loss(r, t_real, dis_update) for r in refs) / len(refs)
     assert got.dtype == torch.float32
-    assert abs(float(got) - float(ref)) <= 1e-5 * max(1.0, abs(float(ref))), (float(got), float(ref))
+    g0, r0 = float(got.detach()), float(ref.detach())
+    assert abs(g0 - r0) <= 1e-5 * max(1.0, abs(r0)), (g0, r0)
     got.backward()
     ref.backward()
     for x, r in zip(xs, refs):
