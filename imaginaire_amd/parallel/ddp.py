@@ -27,9 +27,10 @@ designed around how the GAN trainers actually use their networks:
   gradient (ops/conv.py ``_take_grad_dest``) writes its split-K sum straight into the bucket
   and autograd adopts that view as ``.grad``, so the hook has nothing to copy. Other gradients
   (norm affine parameters, linear layers, a weight's second use in one backward) arrive in
-  fresh memory and the hook copies them into their slice — one read + one write, instead of a
-  bucket memset plus a read-modify-write accumulate; slices of parameters that got no gradient
-  are zeroed at launch;
+  fresh memory; the hook only records them and the bucket copies them all into their slices
+  with ONE multi-tensor copy when it launches — one read + one write, instead of a bucket
+  memset plus a read-modify-write accumulate; a slice whose parameter got no gradient is zeroed
+  at launch only if an earlier backward wrote it;
 * the 1/world scaling rides in the collective (``ReduceOp.AVG`` on RCCL, probed once at
   construction) instead of a separate pass over every bucket;
 * **buffers** (SN u/v, BN running stats) are broadcast once at construction
