@@ -603,7 +603,7 @@ class _MfmaConv2d(torch.autograd.Function):
                         dy, xb, wb, None, stride, padding, dilation, False, [0, 0], 1,
                         [True, False, False])[0]
                     if sig is not None:
-                        dx = dx * (1.0 / sig).to(dx.dtype)
+                        dx = dx.div_(sig)  # one pass (fp32 divisor, no reciprocal / cast kernels)
             if sn is not None and need_w and dw is None and _SN_DOT_RATIO > 0 and \
                     xb.numel() <= _SN_DOT_RATIO * wb.numel() and dx.dtype == torch.bfloat16 and \
                     dx.shape[1] % 8 == 0 and dx.is_contiguous(memory_format=_CL):
