@@ -39,3 +39,10 @@ def test_registry_aliases():
         'imaginaire_amd.generators.spade'
     mod = import_module('imaginaire.trainers.spade')
     assert hasattr(mod, 'Trainer')
+    # the synthetic paired-video / few-shot-video types of the unit-test configs are the one
+    # synthetic generator (no re-export modules of their own)
+    from imaginaire_amd.datasets import synthetic
+    for t in ('imaginaire.datasets.synthetic_videos',
+              'imaginaire.datasets.synthetic_few_shot_videos'):
+        assert canonical_module_name(t) == 'imaginaire_amd.datasets.synthetic'
+        assert import_module(t).Dataset is synthetic.Dataset
