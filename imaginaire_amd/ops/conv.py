@@ -1275,6 +1275,8 @@ def _pending_union():
 
 
 _TUNE_STATE = {'calls': 0, 'empty': 0}
+# interleaved timing rounds per wgrad candidate set (the minimum over them decides; A/B knob)
+_TUNE_TRIALS = max(1, int(os.environ.get('IMAGINAIRE_AMD_TUNE_TRIALS', '3')))
 _TUNE_QUIET_PERIOD = 64
 
 
@@ -1329,7 +1331,7 @@ def tune_pending():
                 fns['k11v2'] = lambda: k11(2)
             else:
                 fns['k11'] = k11
-            times[('w',) + key] = _time_candidates(fns)
+            times[('w',) + key] = _time_candidates(fns, trials=_TUNE_TRIALS)
         else:
             # a deconv key names its weight, which only the ranks that saw it hold: those time
             # it, the others report 0 and the vote below averages over the ranks that timed
