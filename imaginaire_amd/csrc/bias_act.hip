@@ -8,6 +8,8 @@
 // in the same pass (per-block channel partials + one tiny sum kernel).
 #include "common.h"
 
+#include <cstdlib>
+
 namespace iamd {
 namespace {
 
@@ -39,7 +41,9 @@ bias_act_fwd_kernel(const T* __restrict__ x, T* __restrict__ out, const float* _
 // dx = dy * act'(out); per-block channel partial sums of dx (CL layout: rows x C).
 // ACT = false (identity activation): only the bias gradient is needed, dx IS dy, so the
 // kernel reads dy alone and writes no dx (a third of the bytes).
-template <typename T, int VEC, bool ACT>
+// U rows per trip with all their loads issued first (more loads in flight per lane for the
+// bias-only pass, which reads dy alone)
+template <typename T, int VEC, bool ACT, int U>
 __global__ void __launch_bounds__(kThreads)
 bias_act_bwd_cl(const T* __restrict__ out, const T* __restrict__ dy, T* __restrict__ dx,
                 int64_t rows, int C, int64_t rows_per_block, int tpr, float slope,
@@ -56,18 +60,29 @@ bias_act_bwd_cl(const T* __restrict__ out, const T* __restrict__ dy, T* __restri
 #pragma unroll
   for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
   if (active) {
-    for (int64_t row = r0 + r; row < r1; row += rpb) {
-      const int64_t e = row * C + c0;
-      float o[VEC], g[VEC];
-      load_vec<T, VEC>(dy + e, g);
-      if constexpr (ACT) {
-        load_vec<T, VEC>(out + e, o);
+    for (int64_t row = r0 + r; row < r1; row += (int64_t)rpb * U) {
+      float o[U][VEC], g[U][VEC];
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) g[k] *= act_grad(o[k], slope);
+      for (int u = 0; u < U; ++u) {
+        const int64_t rr = row + (int64_t)u * rpb;
+        if (rr < r1) {
+          load_vec<T, VEC>(dy + rr * C + c0, g[u]);
+          if constexpr (ACT) load_vec<T, VEC>(out + rr * C + c0, o[u]);
+        }
       }
 #pragma unroll
-      for (int k = 0; k < VEC; ++k) acc[k] += g[k];
-      if constexpr (ACT) store_vec<T, VEC>(dx + e, g);
+      for (int u = 0; u < U; ++u) {
+        const int64_t rr = row + (int64_t)u * rpb;
+        if (rr < r1) {
+          if constexpr (ACT) {
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) g[u][k] *= act_grad(o[u][k], slope);
+            store_vec<T, VEC>(dx + rr * C + c0, g[u]);
+          }
+#pragma unroll
+          for (int k = 0; k < VEC; ++k) acc[k] += g[u][k];
+        }
+      }
     }
   }
 #pragma unroll
@@ -226,16 +241,21 @@ std::vector<at::Tensor> bias_act_bwd(const at::Tensor& out, const at::Tensor& dy
       buf = at::empty({(int64_t)P * C + C}, fopt);
       partial = buf.narrow(0, 0, (int64_t)P * C);
       const bool act = slope != 1.0;
+      // IMAGINAIRE_AMD_BIASACT_UNROLL (read per call, A/B): rows per trip, 4 or 1. Default: 4 for
+      // the bias-only pass (1.00-1.17x), 1 with an activation (already 4.7-5.7 TB/s; 0.97-1.00x
+      // unrolled): profiles/bias_act_bwd_unroll_ab_r6_mi355x.txt
+      const char* ue = std::getenv("IMAGINAIRE_AMD_BIASACT_UNROLL");
+      const bool unroll = ue == nullptr ? !act : std::atoi(ue) != 1;
       auto launch = [&](auto vt) {
         constexpr int V = decltype(vt)::value;
-        if (act)
-          hipLaunchKernelGGL((bias_act_bwd_cl<scalar_t, V, true>), dim3(P, nzc), dim3(kThreads), 0,
-                             stream(), op, gp, dp, rows, C, rows_per_block, tpr, (float)slope,
-                             partial.data_ptr<float>());
-        else
-          hipLaunchKernelGGL((bias_act_bwd_cl<scalar_t, V, false>), dim3(P, nzc), dim3(kThreads), 0,
-                             stream(), op, gp, dp, rows, C, rows_per_block, tpr, (float)slope,
-                             partial.data_ptr<float>());
+        auto go = [&](auto kern) {
+          hipLaunchKernelGGL(kern, dim3(P, nzc), dim3(kThreads), 0, stream(), op, gp, dp, rows, C,
+                             rows_per_block, tpr, (float)slope, partial.data_ptr<float>());
+        };
+        if (act && unroll) go(bias_act_bwd_cl<scalar_t, V, true, 4>);
+        else if (act) go(bias_act_bwd_cl<scalar_t, V, true, 1>);
+        else if (unroll) go(bias_act_bwd_cl<scalar_t, V, false, 4>);
+        else go(bias_act_bwd_cl<scalar_t, V, false, 1>);
       };
       switch (vec) {
         case 8: launch(std::integral_constant<int, 8>()); break;
