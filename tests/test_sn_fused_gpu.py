@@ -26,7 +26,7 @@ def _make():
 
 
 def _rel(a, b):
-    a, b = a.float().reshape(-1), b.float().reshape(-1)
+    a, b = a.detach().float().reshape(-1), b.detach().float().reshape(-1)
     return float((a - b).norm() / b.norm().clamp_min(1e-30))
 
 
