@@ -1,5 +1,5 @@
 """A/B of the multi-tensor Adam kernel with plain vs non-temporal fp32 loads / stores
-(IMAGINAIRE_AMD_ADAM_NT, read once per process: run this script once per setting).
+(IMAGINAIRE_AMD_ADAM_NT / IMAGINAIRE_AMD_EMA_NT, read once per process: run this script once per setting).
 
 SPADE-recipe-sized parameter set: 415M fp32 parameters in 400 tensors (fp32 grads, a bf16
 shadow on the conv weights), i.e. the optimizer traffic of one bench step. Prints ms per
@@ -49,6 +49,19 @@ def main():
     print('adam NT=%s: %d params in %d tensors: %.3f ms/call, %.2f TB/s effective' % (
         os.environ.get('IMAGINAIRE_AMD_ADAM_NT', '1'), total, len(sizes), ms,
         nbytes / ms / 1e9))
+    # EMA of the same set (IMAGINAIRE_AMD_EMA_NT): 8 B read + 4 B written per parameter
+    avg = [torch.zeros(n, device=dev) for n in sizes]
+    for _ in range(3):
+        ext.mt_ema(avg, p, 0.999, None, None, 0)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(iters):
+        ext.mt_ema(avg, p, 0.999, None, None, 0)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    print('ema NT=%s: %.3f ms/call, %.2f TB/s effective' % (
+        os.environ.get('IMAGINAIRE_AMD_EMA_NT', '1'), ms, 12 * total / ms / 1e9))
 
 
 if __name__ == '__main__':
